@@ -1,0 +1,245 @@
+/*
+ * mpix_redop.h -- C-ABI of the MI355X-native local reduction library
+ * (libmpix_redop.so, built from mpich_amd/csrc/).
+ *
+ * This is the drop-in boundary for MPICH's local element-wise reduction:
+ * every entry point below replaces one reference interface, cited as
+ * reference-file:line (paths relative to the pmodels/mpich tree).
+ *
+ *   MPIX_Reduce_local        <- MPIR_Reduce_local
+ *                               src/include/mpir_coll.h:62-63,
+ *                               body src/mpi/coll/reduce_local/reduce_local.c:53-96
+ *   MPIX_Reduce_local_async  <- same contract, enqueued on a caller HIP stream
+ *                               (what the NBC engines need:
+ *                               src/mpi/coll/transports/gentran/gentran_utils.c:157-167)
+ *   MPIX_Redop_is_supported  <- MPIR_Typerep_reduce_is_supported
+ *                               src/mpi/datatype/typerep/yaksa/typerep_yaksa_pack.c:218-271,
+ *                               used by maint/gen_coll.py:546-547 for host staging
+ *   MPIX_Op_table / MPIX_SUM.. <- MPIR_Op_table + MPIR_op_function
+ *                               src/mpi/coll/op/oputil.c:10-27, src/include/mpir_op.h:206-209
+ *   MPIX_Redop_op_dt_check   <- MPIR_op_dt_check  src/include/mpir_datatype.h:780-868
+ *   MPIX_Redop_internal_op_dt_check <- MPIR_Internal_op_dt_check  mpir_datatype.h:870-933
+ *   MPIX_Datatype_internal   <- MPIR_DATATYPE_REPLACE_BUILTIN  mpir_datatype.h:169-176
+ *                               with the table of src/mpi/datatype/typeutil.c:29-109
+ *   MPIX_Reduce_local_vector <- typerep_op_fallback on an MPI_Type_vector target
+ *                               src/mpi/datatype/typerep/src/typerep_op.c:69-155
+ *   MPIX_Redop_set_fortran_booleans <- MPIR_Abi_set_fortran_booleans_impl
+ *                               src/mpi/datatype/typeutil.c:502-515
+ *
+ * Handles use MPICH's own 32-bit encoding (src/include/mpi.h.in:166-311 and
+ * src/include/mpir_datatype.h:22-125), so an MPICH build can pass its
+ * MPI_Datatype / MPI_Op values straight through.  Both the external builtin
+ * handles (MPI_FLOAT = 0x4c00040a) and the internal ones MPIR_Reduce_local
+ * receives (MPIR_FLOAT32|0x0a = 0x4c83040a) are accepted, as are the struct
+ * pair types MPI_{FLOAT,DOUBLE,LONG,SHORT}_INT (0x8c00000k).
+ *
+ * No C++ or torch types appear here: plain pointers, sizes and int codes.
+ */
+#ifndef MPIX_REDOP_H_INCLUDED
+#define MPIX_REDOP_H_INCLUDED
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int MPIX_Datatype;      /* same width/encoding as MPICH's MPI_Datatype */
+typedef int MPIX_Op;            /* same width/encoding as MPICH's MPI_Op */
+typedef intptr_t MPIX_Aint;     /* MPI_Aint on LP64 */
+
+/* ---- return codes: MPI error classes (src/include/mpi.h.in:650-677) ---- */
+#define MPIX_REDOP_SUCCESS     0
+#define MPIX_REDOP_ERR_BUFFER  1        /* MPI_ERR_BUFFER: NULL / MPI_IN_PLACE / aliased */
+#define MPIX_REDOP_ERR_COUNT   2        /* MPI_ERR_COUNT: negative count */
+#define MPIX_REDOP_ERR_TYPE    3        /* MPI_ERR_TYPE: datatype unknown or not on GPU */
+#define MPIX_REDOP_ERR_OP      9        /* MPI_ERR_OP: op undefined for this datatype */
+#define MPIX_REDOP_ERR_ARG     12       /* MPI_ERR_ARG */
+#define MPIX_REDOP_ERR_OTHER   15       /* MPI_ERR_OTHER: HIP runtime failure */
+#define MPIX_REDOP_ERR_INTERN  16       /* MPI_ERR_INTERN */
+
+/* ---- predefined ops (mpi.h.in:297-311); index = op & 0xf ---- */
+#define MPIX_OP_NULL  ((MPIX_Op)0x18000000)
+#define MPIX_MAX      ((MPIX_Op)0x58000001)
+#define MPIX_MIN      ((MPIX_Op)0x58000002)
+#define MPIX_SUM      ((MPIX_Op)0x58000003)
+#define MPIX_PROD     ((MPIX_Op)0x58000004)
+#define MPIX_LAND     ((MPIX_Op)0x58000005)
+#define MPIX_BAND     ((MPIX_Op)0x58000006)
+#define MPIX_LOR      ((MPIX_Op)0x58000007)
+#define MPIX_BOR      ((MPIX_Op)0x58000008)
+#define MPIX_LXOR     ((MPIX_Op)0x58000009)
+#define MPIX_BXOR     ((MPIX_Op)0x5800000a)
+#define MPIX_MINLOC   ((MPIX_Op)0x5800000b)
+#define MPIX_MAXLOC   ((MPIX_Op)0x5800000c)
+#define MPIX_REPLACE  ((MPIX_Op)0x5800000d)
+#define MPIX_NO_OP    ((MPIX_Op)0x5800000e)
+#define MPIX_EQUAL    ((MPIX_Op)0x5800000f)
+
+/* ---- internal datatype encoding (mpir_datatype.h:22-125) ----
+ * 0x4c | kind | size | builtin index.  Kinds: */
+#define MPIX_TYPE_INTERNAL_MASK  0x800000
+#define MPIX_TYPE_PAIR_MASK      0x400000
+#define MPIX_TYPE_KIND_MASK      0x0f0000
+#define MPIX_TYPE_FIXED          0x000000
+#define MPIX_TYPE_SIGNED         0x010000
+#define MPIX_TYPE_UNSIGNED       0x020000
+#define MPIX_TYPE_FLOAT          0x030000
+#define MPIX_TYPE_COMPLEX        0x040000
+#define MPIX_TYPE_ALT_FLOAT      0x050000
+#define MPIX_TYPE_ALT_COMPLEX    0x060000
+#define MPIX_TYPE_FORTRAN_LOGICAL 0x070000
+
+#define MPIX_INT8      ((MPIX_Datatype)0x4c810100)
+#define MPIX_INT16     ((MPIX_Datatype)0x4c810200)
+#define MPIX_INT32     ((MPIX_Datatype)0x4c810400)
+#define MPIX_INT64     ((MPIX_Datatype)0x4c810800)
+#define MPIX_INT128    ((MPIX_Datatype)0x4c811000)
+#define MPIX_UINT8     ((MPIX_Datatype)0x4c820100)
+#define MPIX_UINT16    ((MPIX_Datatype)0x4c820200)
+#define MPIX_UINT32    ((MPIX_Datatype)0x4c820400)
+#define MPIX_UINT64    ((MPIX_Datatype)0x4c820800)
+#define MPIX_UINT128   ((MPIX_Datatype)0x4c821000)
+#define MPIX_FLOAT16   ((MPIX_Datatype)0x4c830200)
+#define MPIX_FLOAT32   ((MPIX_Datatype)0x4c830400)
+#define MPIX_FLOAT64   ((MPIX_Datatype)0x4c830800)
+#define MPIX_FLOAT128  ((MPIX_Datatype)0x4c831000)
+#define MPIX_COMPLEX16 ((MPIX_Datatype)0x4c840400)  /* 2 x fp16 */
+#define MPIX_COMPLEX32 ((MPIX_Datatype)0x4c840800)  /* float _Complex */
+#define MPIX_COMPLEX64 ((MPIX_Datatype)0x4c841000)  /* double _Complex */
+#define MPIX_COMPLEX128 ((MPIX_Datatype)0x4c842000) /* 2 x __float128 */
+#define MPIX_BFLOAT16_INTERNAL ((MPIX_Datatype)0x4c850200)
+#define MPIX_ALT_FLOAT128 ((MPIX_Datatype)0x4c851000)   /* x86-64 long double */
+#define MPIX_ALT_COMPLEX128 ((MPIX_Datatype)0x4c862000) /* long double _Complex */
+#define MPIX_FORTRAN_LOGICAL8   ((MPIX_Datatype)0x4c870100)
+#define MPIX_FORTRAN_LOGICAL16  ((MPIX_Datatype)0x4c870200)
+#define MPIX_FORTRAN_LOGICAL32  ((MPIX_Datatype)0x4c870400)
+#define MPIX_FORTRAN_LOGICAL64  ((MPIX_Datatype)0x4c870800)
+#define MPIX_FORTRAN_LOGICAL128 ((MPIX_Datatype)0x4c871000)
+/* builtin pair types {T value; T loc} (mpir_datatype.h:111-125) */
+#define MPIX_2INT8     ((MPIX_Datatype)0x4cc10200)
+#define MPIX_2INT16    ((MPIX_Datatype)0x4cc10400)
+#define MPIX_2INT32    ((MPIX_Datatype)0x4cc10800)
+#define MPIX_2INT64    ((MPIX_Datatype)0x4cc11000)
+#define MPIX_2UINT8    ((MPIX_Datatype)0x4cc20200)
+#define MPIX_2UINT16   ((MPIX_Datatype)0x4cc20400)
+#define MPIX_2UINT32   ((MPIX_Datatype)0x4cc20800)
+#define MPIX_2UINT64   ((MPIX_Datatype)0x4cc21000)
+#define MPIX_2FLOAT16  ((MPIX_Datatype)0x4cc30400)
+#define MPIX_2FLOAT32  ((MPIX_Datatype)0x4cc30800)
+#define MPIX_2FLOAT64  ((MPIX_Datatype)0x4cc31000)
+
+/* ---- a few external builtin handles (mpi.h.in:166-264) ---- */
+#define MPIX_MPI_CHAR          ((MPIX_Datatype)0x4c000101)
+#define MPIX_MPI_INT           ((MPIX_Datatype)0x4c000405)
+#define MPIX_MPI_LONG          ((MPIX_Datatype)0x4c000807)
+#define MPIX_MPI_FLOAT         ((MPIX_Datatype)0x4c00040a)
+#define MPIX_MPI_DOUBLE        ((MPIX_Datatype)0x4c00080b)
+#define MPIX_MPI_BYTE          ((MPIX_Datatype)0x4c00010d)
+#define MPIX_MPI_2INT          ((MPIX_Datatype)0x4c000816)
+#define MPIX_MPI_C_FLOAT16     ((MPIX_Datatype)0x4c000246)
+#define MPIX_MPI_BFLOAT16      ((MPIX_Datatype)0x4c00024c)
+/* struct pair types, created by MPIR_Datatype_init_pairtypes (pairtypes.c:99-121) */
+#define MPIX_MPI_FLOAT_INT       ((MPIX_Datatype)0x8c000000)
+#define MPIX_MPI_DOUBLE_INT      ((MPIX_Datatype)0x8c000001)
+#define MPIX_MPI_LONG_INT        ((MPIX_Datatype)0x8c000002)
+#define MPIX_MPI_SHORT_INT       ((MPIX_Datatype)0x8c000003)
+#define MPIX_MPI_LONG_DOUBLE_INT ((MPIX_Datatype)0x8c000004)
+
+/* ---- library lifetime ----
+ * init is optional (every entry point initialises lazily); finalize frees
+ * the per-thread streams and the host-staging scratch. */
+int MPIX_Redop_init(void);
+int MPIX_Redop_finalize(void);
+
+/* ---- the hot path ----
+ * inoutbuf[i] = inoutbuf[i] OP inbuf[i] for i < count elements of
+ * `datatype` (extent-strided, i.e. pair padding preserved).
+ *
+ * MPIX_Reduce_local: synchronous, like MPIR_Reduce_local.  Buffers may be
+ * device memory (hipMalloc / managed) or host memory; host operands are
+ * staged through device scratch with hipMemcpyAsync.  count == 0 is a
+ * successful no-op (reduce_local.c:59-60).
+ *
+ * MPIX_Reduce_local_async: both buffers must be device-accessible; the
+ * kernel is enqueued on `stream` (a hipStream_t, NULL = legacy default
+ * stream) and the call returns without waiting. */
+int MPIX_Reduce_local(const void *inbuf, void *inoutbuf, MPIX_Aint count,
+                      MPIX_Datatype datatype, MPIX_Op op);
+int MPIX_Reduce_local_async(const void *inbuf, void *inoutbuf, MPIX_Aint count,
+                            MPIX_Datatype datatype, MPIX_Op op, void *stream);
+
+/* Derived (vector) target, packed source -- typerep_op.c:115-150 with the
+ * target an MPI_Type_vector(count, blocklen, stride, basic_type):
+ *   for b < count, j < blocklen:
+ *     inout[b*stride + j] = inout[b*stride + j] OP in[b*blocklen + j]
+ * (stride and blocklen in elements; gaps in the target are never written).
+ * Device buffers only; the sync form waits on its stream. */
+int MPIX_Reduce_local_vector_async(const void *inbuf, void *inoutbuf, MPIX_Aint count,
+                                   MPIX_Aint blocklen, MPIX_Aint stride,
+                                   MPIX_Datatype basic_type, MPIX_Op op, void *stream);
+int MPIX_Reduce_local_vector(const void *inbuf, void *inoutbuf, MPIX_Aint count,
+                             MPIX_Aint blocklen, MPIX_Aint stride,
+                             MPIX_Datatype basic_type, MPIX_Op op);
+
+/* 1 if (op, datatype) runs on the GPU path, else 0.  `count` is accepted
+ * for signature parity and ignored (the reference passes 0 here too,
+ * reduce_local.c:66-68).  When 0, a caller keeps its own CPU op table. */
+int MPIX_Redop_is_supported(MPIX_Op op, MPIX_Aint count, MPIX_Datatype datatype);
+
+/* Binding-level and internal legality of (op, datatype): 1 legal, 0 not. */
+int MPIX_Redop_op_dt_check(MPIX_Op op, MPIX_Datatype datatype);
+int MPIX_Redop_internal_op_dt_check(MPIX_Op op, MPIX_Datatype datatype);
+
+/* External builtin -> internal type (identity for internal / pair handles,
+ * MPIX_DATATYPE_NULL (0x0c000000) for unknown builtins). */
+MPIX_Datatype MPIX_Datatype_internal(MPIX_Datatype datatype);
+/* Extent in bytes of one element (pair types include padding); 0 if unknown. */
+MPIX_Aint MPIX_Datatype_extent(MPIX_Datatype datatype);
+
+/* Fortran .TRUE./.FALSE. used by LAND/LOR/LXOR on Fortran logicals
+ * (mpii_fortlogical.h:15,28; defaults 1 / 0 as typeutil.c:502-510). */
+int MPIX_Redop_set_fortran_booleans(int true_value, int false_value);
+
+/* ---- per-op function table, MPIR_op_function signature (mpir_op.h:206) ----
+ * Synchronous; same pointer rules as MPIX_Reduce_local.  The op functions
+ * return void like the reference's; a failure is recorded and can be read
+ * with MPIX_Redop_last_error() (the reference MPIR_Assert()s instead). */
+typedef void MPIX_op_function(void *invec, void *inoutvec, MPIX_Aint *len,
+                              MPIX_Datatype *type);
+extern MPIX_op_function *const MPIX_Op_table[16];
+void MPIX_MAXF(void *invec, void *inoutvec, MPIX_Aint *len, MPIX_Datatype *type);
+void MPIX_MINF(void *invec, void *inoutvec, MPIX_Aint *len, MPIX_Datatype *type);
+void MPIX_SUM_fn(void *invec, void *inoutvec, MPIX_Aint *len, MPIX_Datatype *type);
+void MPIX_PROD_fn(void *invec, void *inoutvec, MPIX_Aint *len, MPIX_Datatype *type);
+void MPIX_LAND_fn(void *invec, void *inoutvec, MPIX_Aint *len, MPIX_Datatype *type);
+void MPIX_BAND_fn(void *invec, void *inoutvec, MPIX_Aint *len, MPIX_Datatype *type);
+void MPIX_LOR_fn(void *invec, void *inoutvec, MPIX_Aint *len, MPIX_Datatype *type);
+void MPIX_BOR_fn(void *invec, void *inoutvec, MPIX_Aint *len, MPIX_Datatype *type);
+void MPIX_LXOR_fn(void *invec, void *inoutvec, MPIX_Aint *len, MPIX_Datatype *type);
+void MPIX_BXOR_fn(void *invec, void *inoutvec, MPIX_Aint *len, MPIX_Datatype *type);
+void MPIX_MINLOC_fn(void *invec, void *inoutvec, MPIX_Aint *len, MPIX_Datatype *type);
+void MPIX_MAXLOC_fn(void *invec, void *inoutvec, MPIX_Aint *len, MPIX_Datatype *type);
+void MPIX_REPLACE_fn(void *invec, void *inoutvec, MPIX_Aint *len, MPIX_Datatype *type);
+void MPIX_NO_OP_fn(void *invec, void *inoutvec, MPIX_Aint *len, MPIX_Datatype *type);
+
+int MPIX_Redop_last_error(void);
+const char *MPIX_Redop_error_string(int code);
+
+/* ---- launch geometry (performance knob, not semantics) ----
+ * threads per block and a cap on the grid (0 = one tile per block, no
+ * grid-stride loop).  The packets-per-thread unroll is a compile-time
+ * constant (MPIX_REDOP_UNROLL).  Env MPIX_REDOP_BLOCK / MPIX_REDOP_MAXGRID
+ * override the defaults at first use. */
+int MPIX_Redop_set_launch(int block_threads, int max_grid);
+int MPIX_Redop_get_launch(int *block_threads, int *unroll, int *max_grid);
+
+/* Build identification: the gfx target the code object was compiled for. */
+const char *MPIX_Redop_build_info(void);
+
+#define MPIX_DATATYPE_NULL ((MPIX_Datatype)0x0c000000)
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPIX_REDOP_H_INCLUDED */

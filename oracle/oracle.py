@@ -1,0 +1,109 @@
+"""ORACLE loader -- TEST INFRASTRUCTURE ONLY.
+
+ctypes binding of oracle/build/liboracle_redop.so (the clean-room CPU
+restatement in redop_oracle.c).  Only tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg may import this module; the product package
+mpich_amd/ never does.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, 'build', 'liboracle_redop.so')
+
+_lib = None
+
+
+def build(force=False):
+    """Compile the oracle with gcc (oracle/Makefile)."""
+    if force or not os.path.exists(LIB_PATH) or \
+            os.path.getmtime(LIB_PATH) < os.path.getmtime(os.path.join(HERE, 'redop_oracle.c')):
+        subprocess.check_call(['make', '-s', '-C', HERE])
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        vp, i32, il = ctypes.c_void_p, ctypes.c_int, ctypes.c_long
+        L.oracle_reduce_local.argtypes = [vp, vp, il, i32, i32]
+        L.oracle_reduce_local_mt.argtypes = [vp, vp, il, i32, i32, i32]
+        L.oracle_reduce_local_vector.argtypes = [vp, vp, il, il, il, i32, i32]
+        L.oracle_internal.argtypes = [i32]
+        L.oracle_extent.argtypes = [i32]
+        L.oracle_extent.restype = il
+        L.oracle_op_dt_check.argtypes = [i32, i32]
+        L.oracle_internal_op_dt_check.argtypes = [i32, i32]
+        L.oracle_set_fortran_booleans.argtypes = [i32, i32]
+        L.oracle_set_fortran_booleans.restype = None
+        L.oracle_rsb_recursive_halving.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(vp), il,
+                                                   i32, i32, i32]
+        L.oracle_wtime.restype = ctypes.c_double
+        _lib = L
+    return _lib
+
+
+def _i32(h):
+    """MPI handles above 0x7fffffff (pair types 0x8c......) as C int."""
+    return ctypes.c_int(h - (1 << 32) if h >= (1 << 31) else h).value
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def reduce_local(inbuf, inoutbuf, count, datatype, op, nthreads=1):
+    """inoutbuf = inoutbuf OP inbuf on numpy buffers; returns the MPI error class."""
+    if nthreads > 1:
+        return lib().oracle_reduce_local_mt(_ptr(inbuf), _ptr(inoutbuf), count, _i32(datatype),
+                                            _i32(op), nthreads)
+    return lib().oracle_reduce_local(_ptr(inbuf), _ptr(inoutbuf), count, _i32(datatype), _i32(op))
+
+
+def reduce_local_vector(inbuf, inoutbuf, count, blocklen, stride, datatype, op):
+    return lib().oracle_reduce_local_vector(_ptr(inbuf), _ptr(inoutbuf), count, blocklen, stride,
+                                            _i32(datatype), _i32(op))
+
+
+def internal(datatype):
+    return lib().oracle_internal(_i32(datatype)) & 0xffffffff
+
+
+def extent(datatype):
+    return lib().oracle_extent(_i32(datatype))
+
+
+def op_dt_check(op, datatype):
+    return bool(lib().oracle_op_dt_check(_i32(op), _i32(datatype)))
+
+
+def internal_op_dt_check(op, datatype):
+    return bool(lib().oracle_internal_op_dt_check(_i32(op), _i32(datatype)))
+
+
+def set_fortran_booleans(t, f):
+    lib().oracle_set_fortran_booleans(t, f)
+
+
+def rsb_recursive_halving(sendbufs, recvcount, datatype, op):
+    """Simulate MPI_Reduce_scatter_block (recursive halving) over P ranks in
+    one process; returns the list of per-rank result arrays."""
+    P = len(sendbufs)
+    ext = extent(datatype)
+    recvs = [np.zeros(recvcount * ext, np.uint8) for _ in range(P)]
+    sp = (ctypes.c_void_p * P)(*[s.ctypes.data for s in sendbufs])
+    rp = (ctypes.c_void_p * P)(*[r.ctypes.data for r in recvs])
+    rc = lib().oracle_rsb_recursive_halving(sp, rp, recvcount, _i32(datatype), _i32(op), P)
+    if rc:
+        raise RuntimeError('oracle rsb failed: %d' % rc)
+    return recvs
+
+
+def wtime():
+    return lib().oracle_wtime()
