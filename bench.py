@@ -1,0 +1,347 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident MPI_Reduce_local (fp32 SUM, 1 GiB) on MI355X.
+
+BASELINE.json metric "GiB/s device-resident MPI_Reduce_local (fp32 SUM,
+1 GiB) vs HBM roofline", on configs[1]: count = 2^28 MPI_FLOAT per operand,
+both operands resident in HBM before the timed region.  One step = one
+MPIX_Reduce_local call (the synchronous MPIR_Reduce_local drop-in) over the
+whole buffer; GiB/s = algorithmic bytes 3 * count * 4 (read in, read inout,
+write inout) / wall time.
+
+N > 1 (torchrun, one rank per GPU): every rank reduces its own 1 GiB shard
+(no data-path collective: the path is element-wise), value = all ranks'
+bytes / max-over-ranks time ("weak" scaling).  Those runs also time the
+recursive-halving MPI_Reduce_scatter_block (BASELINE config 4) as a
+secondary figure.
+
+Also reported (not `value`): kernel-only rate from HIP events on the launch
+stream -> `roofline`; a measured STREAM triad on the same GPU; the
+host-resident end-to-end rate (pinned H2D + kernel + D2H); and the
+`cpu_baseline` -- the oracle (clean-room C restatement of MPICH's op loop)
+timed on this host's cores on BASELINE config 1 (16 MiB fp32 SUM).
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from mpich_amd import handles as H  # noqa: E402
+from mpich_amd import redop  # noqa: E402
+
+METRIC = "GiB/s device-resident MPI_Reduce_local (fp32 SUM, 1 GiB) vs HBM roofline"
+HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+GIB = float(1 << 30)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument('--gpus', type=int, default=1)
+    p.add_argument('--steps', type=int, default=50)
+    p.add_argument('--warmup', type=int, default=5)
+    p.add_argument('--count', type=int, default=1 << 28, help='fp32 elements per operand')
+    p.add_argument('--cpu-seconds', type=float, default=12.0,
+                   help='bounded CPU-baseline sample duration per leg')
+    p.add_argument('--no-cpu-baseline', action='store_true')
+    p.add_argument('--no-extras', action='store_true',
+                   help='skip triad / end-to-end / sweep side measurements')
+    p.add_argument('--sweep', action='store_true', help='config 2 chunk/size sweep')
+    p.add_argument('--rsb', action='store_true', help='time reduce_scatter_block even at N=1')
+    p.add_argument('--rsb-bytes', type=int, default=4 << 30, help='RSB vector bytes per rank')
+    p.add_argument('--pmc', default=os.path.join(ROOT, 'profiles', 'r01_pmc_summary.json'),
+                   help='PMC traffic summary (from tools/pmc_summary.py) to quote as traffic')
+    return p.parse_args()
+
+
+def bench_lib():
+    path = os.path.join(ROOT, 'mpich_amd', 'libmpix_bench.so')
+    L = ctypes.CDLL(path)
+    L.mpix_bench_triad.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                   ctypes.c_float, ctypes.c_uint64, ctypes.c_void_p]
+    return L
+
+
+def event_time_per_launch(launch, reps, stream):
+    """average duration of `launch()` measured with HIP events on `stream`"""
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(reps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(reps)]
+    for i in range(reps):
+        starts[i].record(stream)
+        launch()
+        ends[i].record(stream)
+    stream.synchronize()
+    ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
+    ms.sort()
+    return sum(ms) / len(ms), ms[len(ms) // 2], ms[0]
+
+
+def fill_uniform(t, seed):
+    g = torch.Generator(device=t.device)
+    g.manual_seed(seed)
+    t.uniform_(-1.0, 1.0, generator=g)
+
+
+def cpu_baseline(seconds):
+    """oracle (CPU restatement) on BASELINE config 1: 16 MiB fp32 SUM."""
+    import numpy as np
+    from oracle import oracle as orc
+    orc.build()
+    n = 4194304
+    rng = np.random.default_rng(0x5EED0001)
+    a = rng.uniform(-1, 1, n).astype(np.float32)
+    b = rng.uniform(-1, 1, n).astype(np.float32)
+    out = {}
+    ncores = len(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') else os.cpu_count()
+    threads_all = max(1, min(16, ncores))
+    for label, nth in (('1core', 1), ('allcores', threads_all)):
+        reps, t_list = 0, []
+        t_end = time.perf_counter() + seconds / 2
+        while time.perf_counter() < t_end or reps < 3:
+            t0 = orc.wtime()
+            orc.reduce_local(b, a, n, H.MPI_FLOAT, H.MPI_SUM, nthreads=nth)
+            t_list.append(orc.wtime() - t0)
+            reps += 1
+        t_list.sort()
+        med = t_list[len(t_list) // 2]
+        out[label] = dict(gibs_median=3 * n * 4 / GIB / med, gibs_best=3 * n * 4 / GIB / t_list[0],
+                          reps=reps, threads=nth)
+    model = ''
+    try:
+        for line in open('/proc/cpuinfo'):
+            if line.startswith('model name'):
+                model = line.split(':', 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return dict(
+        value=round(out['1core']['gibs_median'], 3), unit='GiB/s', cores=1, kind='port',
+        sample='BASELINE config 1: MPI_Reduce_local(MPI_SUM, MPI_FLOAT) 16 MiB (4,194,304 '
+               'elements), oracle/redop_oracle.c scalar loop, %d reps in %.0f s, median'
+               % (out['1core']['reps'], seconds / 2),
+        best=round(out['1core']['gibs_best'], 3),
+        allcores=dict(value=round(out['allcores']['gibs_median'], 3), threads=threads_all,
+                      reps=out['allcores']['reps']),
+        host_cpu=model, nproc=os.cpu_count())
+
+
+def load_pmc(path, count):
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    k = d.get('kernels', {}).get('reduce_local_fp32_sum')
+    if not k or k.get('count') != count:
+        return None
+    return k.get('hbm_bytes_per_launch')
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    dev = torch.device('cuda', local)
+    torch.cuda.set_device(dev)
+    assert redop.lib().MPIX_Redop_init() == 0
+
+    n = args.count
+    nbytes_alg = 3 * n * 4
+    inout = torch.empty(n, dtype=torch.float32, device=dev)
+    inb = torch.empty(n, dtype=torch.float32, device=dev)
+    fill_uniform(inout, 0x5EED0001 + 2 * rank)
+    fill_uniform(inb, 0x5EED0002 + 2 * rank)
+    torch.cuda.synchronize()
+
+    def step():
+        redop.check(redop.MPI_Reduce_local(inb, inout, n, H.MPI_FLOAT, H.MPI_SUM))
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([t], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t = float(tt.item())
+    ms_per_step = 1e3 * t / args.steps
+    value = world * nbytes_alg * args.steps / t / GIB
+
+    # kernel-only: the same launch, async on torch's stream, timed by events
+    stream = torch.cuda.current_stream()
+    kreps = max(10, min(args.steps, 50))
+    k_avg, k_med, k_min = event_time_per_launch(
+        lambda: redop.check(redop.reduce_local_async(inb, inout, n, H.MPI_FLOAT, H.MPI_SUM,
+                                                     stream)), kreps, stream)
+    achieved = nbytes_alg / (k_avg * 1e-3) / 1e9
+    result = {
+        'metric': METRIC,
+        'value': round(value, 2),
+        'unit': 'GiB/s',
+        'n_gpus': world,
+        'steps': args.steps,
+        'warmup': args.warmup,
+        'ms_per_step': round(ms_per_step, 4),
+        'higher_is_better': True,
+        'scaling': 'weak',
+        'vs_baseline': None,
+        'dtype': 'f32',
+        'data': 'synthetic (uniform [-1,1), seeded per rank)',
+        'config': {
+            'workload': 'MPI_Reduce_local(MPI_SUM, MPI_FLOAT) device-resident, BASELINE configs[1] '
+                        'at its 1 GiB point',
+            'count': n, 'bytes_per_operand': 4 * n, 'algorithmic_bytes_per_step': nbytes_alg,
+            'parallelism': 'replicas' if world == 1 else 'dp%d shards (no collective)' % world,
+            'launch': redop.get_launch(),
+        },
+        'roofline': {
+            'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+            'frac': round(achieved / HBM_PEAK_GBS, 4),
+            'traffic': load_pmc(args.pmc, n),
+            'kernel_ms_avg': round(k_avg, 4), 'kernel_ms_median': round(k_med, 4),
+            'kernel_ms_min': round(k_min, 4), 'kernel_launches_timed': kreps,
+            'algorithmic_bytes_per_launch': nbytes_alg,
+        },
+    }
+
+    if not args.no_extras and rank == 0:
+        # STREAM triad on the same GPU (three separate 1 GiB fp32 arrays)
+        try:
+            B = bench_lib()
+            a3 = torch.empty(n, dtype=torch.float32, device=dev)
+            tri_avg, tri_med, _ = event_time_per_launch(
+                lambda: B.mpix_bench_triad(a3.data_ptr(), inb.data_ptr(), inout.data_ptr(),
+                                           ctypes.c_float(0.5), n, stream.cuda_stream),
+                kreps, stream)
+            triad = nbytes_alg / (tri_avg * 1e-3) / 1e9
+            result['roofline']['triad_measured_GBs'] = round(triad, 1)
+            result['roofline']['frac_of_triad'] = round(achieved / triad, 4)
+            del a3
+        except OSError as e:
+            result['roofline']['triad_measured_GBs'] = None
+            result['roofline']['triad_error'] = str(e)
+        # host-resident end-to-end: pinned host in/inout -> MPIX_Reduce_local
+        # stages H2D + kernel + D2H (3 x 1 GiB over PCIe)
+        hn = n
+        hin = torch.empty(hn, dtype=torch.float32).pin_memory()
+        hio = torch.empty(hn, dtype=torch.float32).pin_memory()
+        hin.uniform_(-1, 1)
+        hio.uniform_(-1, 1)
+        redop.check(redop.MPI_Reduce_local(hin, hio, hn, H.MPI_FLOAT, H.MPI_SUM))
+        reps = 3
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            redop.check(redop.MPI_Reduce_local(hin, hio, hn, H.MPI_FLOAT, H.MPI_SUM))
+        te = (time.perf_counter() - t0) / reps
+        result['end_to_end_host'] = dict(gibs=round(3 * hn * 4 / GIB / te, 2),
+                                         ms_per_call=round(te * 1e3, 2),
+                                         note='pinned host buffers, chunked H2D/kernel/D2H '
+                                              'staging inside MPIX_Reduce_local; never `value`')
+        del hin, hio
+
+    if args.sweep and rank == 0:
+        sweep = []
+        for mib in (16, 64, 256, 1024):
+            m = mib * (1 << 20) // 4
+            if m > n:
+                break
+            avg, _, _ = event_time_per_launch(
+                lambda: redop.check(redop.reduce_local_async(inb, inout, m, H.MPI_FLOAT,
+                                                             H.MPI_SUM, stream)), 20, stream)
+            sweep.append(dict(mib=mib, kernel_ms=round(avg, 4),
+                              GBs=round(3 * m * 4 / (avg * 1e-3) / 1e9, 1)))
+        chunks = []
+        for ck in (64 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20, 64 << 20, 256 << 20, 1 << 30):
+            m = ck // 4
+            nch = n // m
+            t0 = time.perf_counter()
+            torch.cuda.synchronize()
+            for k in range(nch):
+                redop.check(redop.reduce_local_async(inb[k * m:], inout[k * m:], m, H.MPI_FLOAT,
+                                                     H.MPI_SUM, stream))
+            torch.cuda.synchronize()
+            tt = time.perf_counter() - t0
+            chunks.append(dict(chunk_bytes=ck, calls=nch, GiBs=round(nbytes_alg / tt / GIB, 1)))
+        result['sweep'] = dict(size_kernel=sweep, chunked_1gib_async=chunks)
+
+    del inout, inb
+    torch.cuda.empty_cache()
+
+    if world > 1 or args.rsb:
+        result['reduce_scatter_block'] = rsb_bench(args, world, rank, dev)
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result['cpu_baseline'] = cpu_baseline(args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def rsb_bench(args, world, rank, dev):
+    """BASELINE config 4: MPI_Reduce_scatter_block fp32 SUM, recursive halving,
+    fixed vector per rank (strong scaling), RCCL/xGMI chunk transport."""
+    from mpich_amd import coll
+    if world == 1 or not dist.is_initialized():
+        return dict(note='P=1 is a local copy (coll_api.txt:402-411); see value for the combine')
+    total = args.rsb_bytes // 4
+    recvcount = total // world
+    total = recvcount * world
+    send = torch.empty(total, dtype=torch.float32, device=dev)
+    fill_uniform(send, 0x5EED0100 + rank)
+    recv = torch.empty(recvcount, dtype=torch.float32, device=dev)
+    ws = (torch.empty(total * 4, dtype=torch.uint8, device=dev),
+          torch.empty(total * 4, dtype=torch.uint8, device=dev))
+
+    def once():
+        coll.reduce_scatter_block(send, recv, recvcount, H.MPI_FLOAT, H.MPI_SUM, workspace=ws,
+                                  extent=4)
+    once()
+    reps = max(3, min(10, args.steps))
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        once()
+    torch.cuda.synchronize()
+    dist.barrier()
+    t = (time.perf_counter() - t0) / reps
+    tt = torch.tensor([t], dtype=torch.float64, device=dev)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    t = float(tt.item())
+    busbytes = (world - 1) / world * total * 4
+    pof2 = 1
+    while pof2 * 2 <= world:
+        pof2 *= 2
+    # bytes each rank receives over its single active link in the pof2 steps
+    link_bytes = (pof2 - 1) / pof2 * total * 4
+    del send, recv, ws
+    torch.cuda.empty_cache()
+    return dict(P=world, bytes_per_rank=total * 4, recvcount=recvcount, ms=round(t * 1e3, 3),
+                busbw_GBs=round(busbytes / t / 1e9, 2),
+                link_GBs=round(link_bytes / t / 1e9, 2),
+                frac_of_xgmi_link=round(link_bytes / t / 1e9 / 153.0, 4),
+                algorithm='recursive halving (reduce_scatter_block_intra_recursive_halving.c)')
+
+
+if __name__ == '__main__':
+    main()

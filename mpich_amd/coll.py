@@ -1,0 +1,153 @@
+"""Recursive-halving MPI_Reduce_scatter_block over torch.distributed.
+
+Restates MPIR_Reduce_scatter_block_intra_recursive_halving
+(src/mpi/coll/reduce_scatter_block/reduce_scatter_block_intra_recursive_halving.c:38-260)
+for one process per GPU:
+
+  * the temporaries live in device memory (the reference mallocs them on the
+    host, :80-88, and so reduces on the CPU even for device buffers);
+  * the partial chunks move with torch.distributed point-to-point ops -- the
+    "nccl" backend is RCCL on ROCm, so each step is one grouped
+    ncclSend/ncclRecv pair over the xGMI link to the partner;
+  * every received chunk is combined by the HIP kernel through the C-ABI
+    (MPIX_Reduce_local_async on torch's current stream, which already waits
+    for the receive), in the reference's operand order
+    MPIR_Reduce_local(tmp_recvbuf, tmp_results) -- so the fp association, and
+    therefore every bit, matches the CPU schedule.
+
+The combine can be injected (`combine=`) so the schedule itself can be
+exercised on CPU with the gloo backend; the default is the HIP path and
+there is no CPU fallback.
+"""
+import torch
+import torch.distributed as dist
+
+TAG = 0
+
+
+def _pof2(n):
+    p = 1
+    while p * 2 <= n:
+        p *= 2
+    return p
+
+
+def _default_combine(datatype, op):
+    from . import redop
+
+    def combine(inbuf, inoutbuf, count):
+        redop.check(redop.reduce_local_async(inbuf, inoutbuf, count, datatype, op),
+                    'MPIX_Reduce_local_async')
+    return combine
+
+
+def _exchange(send_t, dst_send, recv_t, src_recv, group):
+    ops = []
+    if send_t is not None:
+        ops.append(dist.P2POp(dist.isend, send_t, dst_send, group=group, tag=TAG))
+    if recv_t is not None:
+        ops.append(dist.P2POp(dist.irecv, recv_t, src_recv, group=group, tag=TAG))
+    if not ops:
+        return
+    for w in dist.batch_isend_irecv(ops):
+        w.wait()
+
+
+def plan(rank, comm_size, recvcount):
+    """The per-step schedule of the reference for `rank`: a list of
+    (peer, send_off, send_cnt, recv_off, recv_cnt) in elements, plus the
+    non-power-of-two prologue/epilogue roles.  Pure index arithmetic
+    (…recursive_halving.c:98-229)."""
+    pof2 = _pof2(comm_size)
+    rem = comm_size - pof2
+    if rank < 2 * rem:
+        newrank = -1 if rank % 2 == 0 else rank // 2
+    else:
+        newrank = rank - rem
+    steps = []
+    if newrank != -1:
+        newcnts = []
+        for i in range(pof2):
+            old_i = i * 2 + 1 if i < rem else i + rem
+            newcnts.append(2 * recvcount if old_i < 2 * rem else recvcount)
+        newdisps = [0] * pof2
+        for i in range(1, pof2):
+            newdisps[i] = newdisps[i - 1] + newcnts[i - 1]
+        mask = pof2 >> 1
+        send_idx = recv_idx = 0
+        last_idx = pof2
+        while mask > 0:
+            newdst = newrank ^ mask
+            dst = newdst * 2 + 1 if newdst < rem else newdst + rem
+            if newrank < newdst:
+                send_idx = recv_idx + mask
+                send_cnt = sum(newcnts[send_idx:last_idx])
+                recv_cnt = sum(newcnts[recv_idx:send_idx])
+            else:
+                recv_idx = send_idx + mask
+                send_cnt = sum(newcnts[send_idx:recv_idx])
+                recv_cnt = sum(newcnts[recv_idx:last_idx])
+            steps.append((dst, newdisps[send_idx], send_cnt, newdisps[recv_idx], recv_cnt))
+            send_idx = recv_idx
+            last_idx = recv_idx + mask
+            mask >>= 1
+    return dict(pof2=pof2, rem=rem, newrank=newrank, steps=steps)
+
+
+def reduce_scatter_block(sendbuf, recvbuf, recvcount, datatype, op, group=None, combine=None,
+                         extent=None, workspace=None):
+    """MPI_Reduce_scatter_block(sendbuf, recvbuf, recvcount, datatype, op, comm).
+
+    sendbuf: tensor holding comm_size*recvcount elements (any torch dtype;
+    it is addressed as bytes); recvbuf: tensor of recvcount elements.  The
+    op must be commutative (all predefined ops are; :62-67).
+    workspace: optional (tmp_results, tmp_recvbuf) byte tensors to reuse.
+    """
+    rank = dist.get_rank(group)
+    size = dist.get_world_size(group)
+    if extent is None:
+        from . import redop
+        extent = redop.datatype_extent(datatype)
+    if combine is None:
+        combine = _default_combine(datatype, op)
+    g2l = (lambda r: dist.get_global_rank(group, r)) if group is not None else (lambda r: r)
+    total = size * recvcount
+    sb = sendbuf.reshape(-1).view(torch.uint8)
+    rb = recvbuf.reshape(-1).view(torch.uint8)
+    if size == 1:
+        rb.copy_(sb[:recvcount * extent])
+        return recvbuf
+    if workspace is not None:
+        tmp_results, tmp_recvbuf = workspace
+        tmp_results = tmp_results[:total * extent]
+        tmp_recvbuf = tmp_recvbuf[:total * extent]
+    else:
+        tmp_results = torch.empty(total * extent, dtype=torch.uint8, device=sb.device)
+        tmp_recvbuf = torch.empty_like(tmp_results)
+    tmp_results.copy_(sb[:total * extent])                          # :91-96
+
+    def el(off, cnt):
+        return slice(off * extent, (off + cnt) * extent)
+
+    p = plan(rank, size, recvcount)
+    rem = p['rem']
+    if rank < 2 * rem:                                              # :110-137
+        if rank % 2 == 0:
+            _exchange(tmp_results, g2l(rank + 1), None, None, group)
+        else:
+            _exchange(None, None, tmp_recvbuf, g2l(rank - 1), group)
+            combine(tmp_recvbuf, tmp_results, total)
+    for dst, soff, scnt, roff, rcnt in p['steps']:                  # :164-229
+        _exchange(tmp_results[el(soff, scnt)] if scnt else None, g2l(dst),
+                  tmp_recvbuf[el(roff, rcnt)] if rcnt else None, g2l(dst), group)
+        if rcnt:
+            combine(tmp_recvbuf[el(roff, rcnt)], tmp_results[el(roff, rcnt)], rcnt)
+    if p['newrank'] != -1:                                          # :232-234
+        rb.copy_(tmp_results[el(rank * recvcount, recvcount)])
+    if rank < 2 * rem:                                              # :241-253
+        if rank % 2:
+            _exchange(tmp_results[el((rank - 1) * recvcount, recvcount)], g2l(rank - 1),
+                      None, None, group)
+        else:
+            _exchange(None, None, rb, g2l(rank + 1), group)
+    return recvbuf

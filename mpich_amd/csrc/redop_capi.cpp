@@ -1,0 +1,630 @@
+// redop_capi.cpp -- the C-ABI of libmpix_redop.so (include/mpix_redop.h).
+//
+// Host side of the drop-in for MPIR_Reduce_local
+// (src/mpi/coll/reduce_local/reduce_local.c:53-96): handle decoding,
+// (op, datatype) legality, pointer classification, the per-thread stream,
+// host-buffer staging, and the dispatch to the gfx950 kernels instantiated in
+// inst_{int,fp,pair}.hip.  There is no CPU compute path here: a combination
+// the GPU path does not cover returns MPIX_REDOP_ERR_TYPE and
+// MPIX_Redop_is_supported() says so, so the caller keeps its own op table
+// for it (exactly how reduce_local.c:66-76 falls back when yaksa declines).
+#include <hip/hip_runtime_api.h>
+
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <atomic>
+#include <mutex>
+
+#include "mpix_redop.h"
+#include "redop_dispatch.h"
+
+using mpix::Entry;
+using mpix::LaunchCfg;
+using mpix::Params;
+
+namespace {
+
+// ---------------------------------------------------------------- handles
+// Builtin index -> internal type (raw, index bits clear) and the binding
+// group used by MPIR_op_dt_check.  LP64 x86-64 with Fortran: INTEGER, REAL,
+// LOGICAL 4 bytes; DOUBLE PRECISION 8; long double 16 (x87 80-bit); bool 1.
+// Source: src/mpi/datatype/typeutil.c:29-109 resolved by configure.ac:3446-3609.
+enum Group { GN = 0, GCI, GFI, GFP, GLOG, GCPX, GBYTE, GMULTI };
+
+struct Builtin {
+    uint32_t internal;
+    uint8_t group;
+};
+
+constexpr uint32_t I8 = 0x4c810100u, I16 = 0x4c810200u, I32 = 0x4c810400u, I64 = 0x4c810800u,
+    I128 = 0x4c811000u, U8 = 0x4c820100u, U16 = 0x4c820200u, U32 = 0x4c820400u,
+    U64 = 0x4c820800u, F16 = 0x4c830200u, F32 = 0x4c830400u, F64 = 0x4c830800u,
+    F128 = 0x4c831000u, C16 = 0x4c840400u, C32 = 0x4c840800u, C64 = 0x4c841000u,
+    C128 = 0x4c842000u, BF16 = 0x4c850200u, LD = 0x4c851000u, LDC = 0x4c862000u,
+    L8 = 0x4c870100u, L16 = 0x4c870200u, L32 = 0x4c870400u, L64 = 0x4c870800u,
+    L128 = 0x4c871000u, FX0 = 0x4c800000u, FX8 = 0x4c800100u, P2I32 = 0x4cc10800u,
+    P2F32 = 0x4cc30800u, P2F64 = 0x4cc31000u;
+
+struct BuiltinTable {
+    Builtin e[0x4d];
+    BuiltinTable() : e()
+    {
+        auto set = [this](int i, uint32_t t, uint8_t g) { e[i] = Builtin{t, g}; };
+        set(0x01, I8, GCI);    set(0x02, U8, GCI);    set(0x03, I16, GCI);   set(0x04, U16, GCI);
+        set(0x05, I32, GCI);   set(0x06, U32, GCI);   set(0x07, I64, GCI);   set(0x08, U64, GCI);
+        set(0x09, I64, GCI);   set(0x0a, F32, GFP);   set(0x0b, F64, GFP);   set(0x0c, LD, GFP);
+        set(0x0d, U8, GBYTE);  set(0x0e, I32, GN);    set(0x0f, FX8, GN);    set(0x10, FX0, GN);
+        set(0x11, FX0, GN);    set(0x16, P2I32, GN);  set(0x18, I8, GCI);    set(0x19, U64, GCI);
+        set(0x1a, I8, GN);     set(0x1b, I32, GFI);   set(0x1c, F32, GFP);   set(0x1d, L32, GLOG);
+        set(0x1e, C32, GCPX);  set(0x1f, F64, GFP);   set(0x20, P2I32, GN);  set(0x21, P2F32, GN);
+        set(0x22, C64, GCPX);  set(0x23, P2F64, GN);  set(0x26, F16, GFP);   set(0x27, F32, GFP);
+        set(0x28, C32, GCPX);  set(0x29, F64, GFP);   set(0x2a, C64, GCPX);  set(0x2b, F128, GFP);
+        set(0x2c, C128, GCPX); set(0x2d, I8, GFI);    set(0x2e, C16, GCPX);  set(0x2f, I16, GFI);
+        set(0x30, I32, GFI);   set(0x31, I64, GFI);   set(0x32, I128, GFI);  set(0x33, I8, GLOG);
+        set(0x34, C32, GCPX);  set(0x35, C64, GCPX);  set(0x36, LDC, GCPX);  set(0x37, I8, GCI);
+        set(0x38, I16, GCI);   set(0x39, I32, GCI);   set(0x3a, I64, GCI);   set(0x3b, U8, GCI);
+        set(0x3c, U16, GCI);   set(0x3d, U32, GCI);   set(0x3e, U64, GCI);   set(0x3f, I8, GLOG);
+        set(0x40, C32, GCPX);  set(0x41, C64, GCPX);  set(0x42, LDC, GCPX);  set(0x43, I64, GMULTI);
+        set(0x44, I64, GMULTI); set(0x45, I64, GMULTI); set(0x46, F16, GFP); set(0x47, L8, GLOG);
+        set(0x48, L16, GLOG);  set(0x49, L32, GLOG);  set(0x4a, L64, GLOG);  set(0x4b, L128, GLOG);
+        set(0x4c, BF16, GFP);
+    }
+};
+const BuiltinTable kBuiltins;
+
+constexpr uint32_t kNull = 0x0c000000u;
+
+inline bool is_builtin(uint32_t h) { return (h >> 30) == 1u; }
+inline bool is_struct_pair(uint32_t h) { return (h & 0xffffff00u) == 0x8c000000u && (h & 0xff) < 5; }
+inline bool is_builtin_op(uint32_t op) { return (op >> 24) == 0x58u; }
+
+// MPIR_DATATYPE_REPLACE_BUILTIN (mpir_datatype.h:169-176)
+uint32_t to_internal(uint32_t dt)
+{
+    if (!is_builtin(dt) || (dt & 0x800000u))
+        return dt;
+    uint32_t idx = dt & 0xff;
+    if (idx == 0 || idx >= 0x4d || kBuiltins.e[idx].internal == 0)
+        return kNull;
+    return kBuiltins.e[idx].internal | idx;
+}
+
+// element extent in bytes (pair padding included; pairtypes.c:15-21)
+uint64_t extent_of(uint32_t it)
+{
+    if (is_struct_pair(it)) {
+        static const uint64_t ext[5] = {8, 16, 16, 8, 32};
+        return ext[it & 0xff];
+    }
+    if (!is_builtin(it) || it == kNull)
+        return 0;
+    return (it >> 8) & 0xff;
+}
+
+bool is_pairtype(uint32_t it)
+{
+    return is_struct_pair(it) || (is_builtin(it) && (it & 0x400000u));
+}
+
+// MPIR_Internal_op_dt_check (mpir_datatype.h:870-933)
+bool internal_ok(uint32_t op, uint32_t it)
+{
+    if (!is_builtin_op(op))
+        return false;
+    uint32_t opi = op & 0xf;
+    if (opi == 11 || opi == 12)
+        return is_pairtype(it);
+    if (opi >= 13)
+        return true;
+    if (!is_builtin(it) || !(it & 0x800000u) || (it & 0x400000u))
+        return false;
+    uint32_t kind = it & 0x0f0000u;
+    switch (opi) {
+        case 1: case 2:
+            return kind == 0x010000u || kind == 0x020000u || kind == 0x030000u || kind == 0x050000u;
+        case 3: case 4:
+            return kind >= 0x010000u && kind <= 0x060000u;
+        case 5: case 7: case 9:
+            return kind == 0x010000u || kind == 0x020000u || kind == 0x070000u;
+        case 6: case 8: case 10:
+            return kind == 0x010000u || kind == 0x020000u;
+        default:
+            return false;
+    }
+}
+
+// MPIR_op_dt_check (mpir_datatype.h:780-868), builtin datatypes
+bool binding_ok(uint32_t op, uint32_t dt)
+{
+    if (!is_builtin_op(op))
+        return false;
+    uint32_t opi = op & 0xf;
+    if (opi == 11 || opi == 12)
+        return is_pairtype(to_internal(dt));
+    if (opi >= 13)
+        return true;
+    if (!is_builtin(dt))
+        return false;
+    if (dt & 0x800000u)
+        return internal_ok(op, dt);
+    uint32_t idx = dt & 0xff;
+    if (idx == 0 || idx >= 0x4d || kBuiltins.e[idx].internal == 0)
+        return false;
+    uint8_t g = kBuiltins.e[idx].group;
+    switch (opi) {
+        case 1: case 2: return g == GCI || g == GFI || g == GFP || g == GMULTI;
+        case 3: case 4: return g == GCI || g == GFI || g == GFP || g == GCPX || g == GMULTI;
+        case 5: case 7: case 9: return g == GCI || g == GLOG || g == GMULTI;
+        case 6: case 8: case 10: return g == GCI || g == GFI || g == GBYTE || g == GMULTI;
+        default: return false;
+    }
+}
+
+extern "C" const char *mpix_build_info(void);
+
+const Entry *gpu_entry(uint32_t opi, uint32_t it)
+{
+    uint32_t raw = is_struct_pair(it) ? it : (it & 0xffffff00u);
+    const Entry *e = mpix::lookup_fp((int) raw, (int) opi);
+    if (!e)
+        e = mpix::lookup_int((int) raw, (int) opi);
+    if (!e)
+        e = mpix::lookup_pair((int) raw, (int) opi);
+    return e;
+}
+
+// ---------------------------------------------------------------- state
+std::atomic<long long> g_ftrue{1}, g_ffalse{0};
+std::atomic<int> g_block{256}, g_max_grid{0};
+std::once_flag g_env_once;
+size_t g_stage_chunk = (size_t) 64 << 20;
+
+void read_env()
+{
+    if (const char *s = getenv("MPIX_REDOP_BLOCK")) {
+        int b = atoi(s);
+        if (b >= 64 && b <= 1024 && b % 64 == 0)
+            g_block = b;
+    }
+    if (const char *s = getenv("MPIX_REDOP_MAXGRID"))
+        g_max_grid = atoi(s) > 0 ? atoi(s) : 0;
+    if (const char *s = getenv("MPIX_REDOP_STAGE_CHUNK")) {
+        long long c = atoll(s);
+        if (c >= 4096)
+            g_stage_chunk = (size_t) c;
+    }
+}
+
+thread_local int t_last_error = 0;
+
+constexpr int kMaxDev = 64;
+struct DevState {
+    bool init = false;
+    hipStream_t s[2] = {nullptr, nullptr};
+    void *scratch = nullptr;    // 2 slots x (in chunk + inout chunk)
+    size_t scratch_bytes = 0;
+};
+thread_local DevState *t_dev = nullptr;   // array of kMaxDev, never freed implicitly
+
+int set_err(int e)
+{
+    t_last_error = e;
+    return e;
+}
+
+int hip_err(hipError_t e)
+{
+    if (e == hipSuccess)
+        return MPIX_REDOP_SUCCESS;
+    if (getenv("MPIX_REDOP_VERBOSE"))
+        fprintf(stderr, "mpix_redop: HIP error %d (%s)\n", (int) e, hipGetErrorString(e));
+    return MPIX_REDOP_ERR_OTHER;
+}
+
+DevState *dev_state(int dev)
+{
+    if (dev < 0 || dev >= kMaxDev)
+        return nullptr;
+    if (!t_dev)
+        t_dev = new DevState[kMaxDev];
+    DevState &d = t_dev[dev];
+    if (!d.init) {
+        for (int k = 0; k < 2; ++k)
+            if (hipStreamCreateWithFlags(&d.s[k], hipStreamNonBlocking) != hipSuccess)
+                return nullptr;
+        d.init = true;
+    }
+    return &d;
+}
+
+LaunchCfg launch_cfg()
+{
+    std::call_once(g_env_once, read_env);
+    return LaunchCfg{g_block.load(), g_max_grid.load()};
+}
+
+Params params() { return Params{g_ftrue.load(), g_ffalse.load()}; }
+
+enum class Where { Device, Host };
+
+Where classify(const void *p, int *dev)
+{
+    hipPointerAttribute_t a;
+    hipError_t e = hipPointerGetAttributes(&a, p);
+    if (e != hipSuccess) {
+        (void) hipGetLastError();
+        return Where::Host;
+    }
+    if (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged) {
+        *dev = a.device;
+        return Where::Device;
+    }
+    return Where::Host;
+}
+
+bool overlaps(const void *a, const void *b, uint64_t bytes)
+{
+    uintptr_t x = (uintptr_t) a, y = (uintptr_t) b;
+    return x < y + bytes && y < x + bytes;
+}
+
+// Argument checks shared by every entry point: the binding-layer checks of
+// MPI_Reduce_local (binding_c.py:2774-2783: op/datatype legality, buffer
+// aliasing, no MPI_IN_PLACE) plus count < 0.  On success *it holds the
+// internal type and *ext its extent.
+int validate(const void *in, const void *io, MPIX_Aint count, uint32_t dt, uint32_t op,
+             uint32_t *it, uint64_t *ext)
+{
+    if (count < 0)
+        return MPIX_REDOP_ERR_COUNT;
+    if (!is_builtin_op(op))
+        return MPIX_REDOP_ERR_OP;
+    *it = to_internal(dt);
+    if (*it == kNull)
+        return MPIX_REDOP_ERR_TYPE;
+    *ext = extent_of(*it);
+    if (*ext == 0)
+        return MPIX_REDOP_ERR_TYPE;
+    if (!internal_ok(op, *it))
+        return MPIX_REDOP_ERR_OP;
+    if (count == 0)
+        return MPIX_REDOP_SUCCESS;
+    if (!in || !io || in == (const void *) -1 || io == (const void *) -1)
+        return MPIX_REDOP_ERR_BUFFER;
+    if (overlaps(in, io, (uint64_t) count * *ext))
+        return MPIX_REDOP_ERR_BUFFER;
+    return MPIX_REDOP_SUCCESS;
+}
+
+// Enqueue on a stream; both buffers device-accessible, arguments validated.
+int enqueue(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext, uint32_t op,
+            hipStream_t s)
+{
+    uint32_t opi = op & 0xf;
+    if (opi == 14)      // MPI_NO_OP
+        return MPIX_REDOP_SUCCESS;
+    if (opi == 13)      // MPI_REPLACE = MPIR_Localcopy (op_fns.c:445-457)
+        return hip_err(hipMemcpyAsync(io, in, count * ext, hipMemcpyDeviceToDevice, s));
+    const Entry *e = gpu_entry(opi, it);
+    if (!e)
+        return MPIX_REDOP_ERR_TYPE;
+    return hip_err(e->contig(in, io, count, params(), launch_cfg(), s));
+}
+
+// Host-resident operand(s): stream them through device scratch in chunks,
+// alternating two streams so chunk k+1's copies overlap chunk k's kernel.
+int staged(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext, uint32_t op,
+           bool in_host, bool io_host, int dev)
+{
+    DevState *d = dev_state(dev);
+    if (!d)
+        return MPIX_REDOP_ERR_OTHER;
+    launch_cfg();
+    uint64_t chunk_elems = g_stage_chunk / ext;
+    if (chunk_elems == 0)
+        chunk_elems = 1;
+    if (chunk_elems > count)
+        chunk_elems = count;
+    size_t slot_bytes = (size_t) (chunk_elems * ext + 255) & ~(size_t) 255;
+    size_t need = 4 * slot_bytes;
+    if (d->scratch_bytes < need) {
+        if (d->scratch)
+            (void) hipFree(d->scratch);
+        d->scratch = nullptr;
+        d->scratch_bytes = 0;
+        if (hipMalloc(&d->scratch, need) != hipSuccess)
+            return MPIX_REDOP_ERR_OTHER;
+        d->scratch_bytes = need;
+    }
+    int rc = MPIX_REDOP_SUCCESS;
+    for (uint64_t off = 0, k = 0; off < count && rc == MPIX_REDOP_SUCCESS; off += chunk_elems, ++k) {
+        uint64_t n = (count - off < chunk_elems) ? count - off : chunk_elems;
+        hipStream_t s = d->s[k & 1];
+        char *slot = (char *) d->scratch + (k & 1) * 2 * slot_bytes;
+        const char *src_in = (const char *) in + off * ext;
+        char *dst_io = (char *) io + off * ext;
+        const void *kin = src_in;
+        void *kio = dst_io;
+        if (in_host) {
+            rc = hip_err(hipMemcpyAsync(slot, src_in, n * ext, hipMemcpyHostToDevice, s));
+            kin = slot;
+        }
+        if (rc == MPIX_REDOP_SUCCESS && io_host) {
+            rc = hip_err(hipMemcpyAsync(slot + slot_bytes, dst_io, n * ext,
+                                        hipMemcpyHostToDevice, s));
+            kio = slot + slot_bytes;
+        }
+        if (rc == MPIX_REDOP_SUCCESS)
+            rc = enqueue(kin, kio, n, it, ext, op, s);
+        if (rc == MPIX_REDOP_SUCCESS && io_host)
+            rc = hip_err(hipMemcpyAsync(dst_io, kio, n * ext, hipMemcpyDeviceToHost, s));
+    }
+    int rc2 = hip_err(hipStreamSynchronize(d->s[0]));
+    int rc3 = hip_err(hipStreamSynchronize(d->s[1]));
+    return rc ? rc : (rc2 ? rc2 : rc3);
+}
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev)
+    {
+        if (hipGetDevice(&prev) == hipSuccess && prev != dev)
+            (void) hipSetDevice(dev);
+        else
+            prev = -1;
+    }
+    ~DeviceGuard()
+    {
+        if (prev >= 0)
+            (void) hipSetDevice(prev);
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+int MPIX_Redop_init(void)
+{
+    launch_cfg();
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess)
+        return set_err(MPIX_REDOP_ERR_OTHER);
+    return set_err(dev_state(dev) ? MPIX_REDOP_SUCCESS : MPIX_REDOP_ERR_OTHER);
+}
+
+int MPIX_Redop_finalize(void)
+{
+    if (!t_dev)
+        return MPIX_REDOP_SUCCESS;
+    for (int i = 0; i < kMaxDev; ++i) {
+        DevState &d = t_dev[i];
+        if (!d.init)
+            continue;
+        DeviceGuard g(i);
+        for (int k = 0; k < 2; ++k)
+            if (d.s[k])
+                (void) hipStreamDestroy(d.s[k]);
+        if (d.scratch)
+            (void) hipFree(d.scratch);
+        d = DevState();
+    }
+    delete[] t_dev;
+    t_dev = nullptr;
+    return MPIX_REDOP_SUCCESS;
+}
+
+int MPIX_Reduce_local_async(const void *inbuf, void *inoutbuf, MPIX_Aint count,
+                            MPIX_Datatype datatype, MPIX_Op op, void *stream)
+{
+    uint32_t it;
+    uint64_t ext;
+    int rc = validate(inbuf, inoutbuf, count, (uint32_t) datatype, (uint32_t) op, &it, &ext);
+    if (rc != MPIX_REDOP_SUCCESS || count == 0)
+        return set_err(rc);
+    return set_err(enqueue(inbuf, inoutbuf, (uint64_t) count, it, ext, (uint32_t) op,
+                           (hipStream_t) stream));
+}
+
+int MPIX_Reduce_local(const void *inbuf, void *inoutbuf, MPIX_Aint count, MPIX_Datatype datatype,
+                      MPIX_Op op)
+{
+    uint32_t it;
+    uint64_t ext;
+    int rc = validate(inbuf, inoutbuf, count, (uint32_t) datatype, (uint32_t) op, &it, &ext);
+    if (rc != MPIX_REDOP_SUCCESS || count == 0)
+        return set_err(rc);
+    uint32_t opi = (uint32_t) op & 0xf;
+    if (opi != 13 && opi != 14 && !gpu_entry(opi, it))
+        return set_err(MPIX_REDOP_ERR_TYPE);
+    int din = -1, dio = -1, cur = 0;
+    (void) hipGetDevice(&cur);
+    bool in_host = classify(inbuf, &din) == Where::Host;
+    bool io_host = classify(inoutbuf, &dio) == Where::Host;
+    int dev = !io_host ? dio : (!in_host ? din : cur);
+    DeviceGuard guard(dev);
+    if (in_host || io_host)
+        return set_err(staged(inbuf, inoutbuf, (uint64_t) count, it, ext, (uint32_t) op, in_host,
+                              io_host, dev));
+    DevState *d = dev_state(dev);
+    if (!d)
+        return set_err(MPIX_REDOP_ERR_OTHER);
+    rc = enqueue(inbuf, inoutbuf, (uint64_t) count, it, ext, (uint32_t) op, d->s[0]);
+    int rc2 = hip_err(hipStreamSynchronize(d->s[0]));
+    return set_err(rc ? rc : rc2);
+}
+
+int MPIX_Reduce_local_vector_async(const void *inbuf, void *inoutbuf, MPIX_Aint count,
+                                   MPIX_Aint blocklen, MPIX_Aint stride,
+                                   MPIX_Datatype basic_type, MPIX_Op op, void *stream)
+{
+    if (count < 0 || blocklen < 0)
+        return set_err(MPIX_REDOP_ERR_COUNT);
+    if (stride < blocklen)
+        return set_err(MPIX_REDOP_ERR_ARG);     // overlapping target runs
+    uint32_t it;
+    uint64_t ext;
+    int rc = validate(inbuf, inoutbuf, 0, (uint32_t) basic_type, (uint32_t) op, &it, &ext);
+    if (rc != MPIX_REDOP_SUCCESS)
+        return set_err(rc);
+    uint64_t n = (uint64_t) count * (uint64_t) blocklen;
+    if (n == 0)
+        return set_err(MPIX_REDOP_SUCCESS);
+    if (!inbuf || !inoutbuf || inbuf == (const void *) -1 || inoutbuf == (void *) -1)
+        return set_err(MPIX_REDOP_ERR_BUFFER);
+    uint64_t span = ((uint64_t) (count - 1) * (uint64_t) stride + (uint64_t) blocklen) * ext;
+    uintptr_t x = (uintptr_t) inbuf, y = (uintptr_t) inoutbuf;
+    if (x < y + span && y < x + n * ext)
+        return set_err(MPIX_REDOP_ERR_BUFFER);
+    uint32_t opi = (uint32_t) op & 0xf;
+    if (opi == 14)
+        return set_err(MPIX_REDOP_SUCCESS);
+    if (opi == 13) {
+        rc = hip_err(hipMemcpy2DAsync(inoutbuf, (size_t) stride * ext, inbuf,
+                                      (size_t) blocklen * ext, (size_t) blocklen * ext,
+                                      (size_t) count, hipMemcpyDeviceToDevice,
+                                      (hipStream_t) stream));
+        return set_err(rc);
+    }
+    const Entry *e = gpu_entry(opi, it);
+    if (!e)
+        return set_err(MPIX_REDOP_ERR_TYPE);
+    return set_err(hip_err(e->vector(inbuf, inoutbuf, (uint64_t) count, (uint64_t) blocklen,
+                                     (uint64_t) stride, params(), launch_cfg(),
+                                     (hipStream_t) stream)));
+}
+
+int MPIX_Reduce_local_vector(const void *inbuf, void *inoutbuf, MPIX_Aint count,
+                             MPIX_Aint blocklen, MPIX_Aint stride, MPIX_Datatype basic_type,
+                             MPIX_Op op)
+{
+    int dev = 0;
+    if (classify(inoutbuf, &dev) != Where::Device)
+        return set_err(MPIX_REDOP_ERR_BUFFER);
+    DeviceGuard guard(dev);
+    DevState *d = dev_state(dev);
+    if (!d)
+        return set_err(MPIX_REDOP_ERR_OTHER);
+    int rc = MPIX_Reduce_local_vector_async(inbuf, inoutbuf, count, blocklen, stride, basic_type,
+                                            op, d->s[0]);
+    int rc2 = hip_err(hipStreamSynchronize(d->s[0]));
+    return set_err(rc ? rc : rc2);
+}
+
+int MPIX_Redop_is_supported(MPIX_Op op, MPIX_Aint count, MPIX_Datatype datatype)
+{
+    (void) count;
+    uint32_t it = to_internal((uint32_t) datatype);
+    if (it == kNull || extent_of(it) == 0 || !internal_ok((uint32_t) op, it))
+        return 0;
+    uint32_t opi = (uint32_t) op & 0xf;
+    if (opi == 13 || opi == 14)
+        return 1;
+    return gpu_entry(opi, it) ? 1 : 0;
+}
+
+int MPIX_Redop_op_dt_check(MPIX_Op op, MPIX_Datatype datatype)
+{
+    return binding_ok((uint32_t) op, (uint32_t) datatype) ? 1 : 0;
+}
+
+int MPIX_Redop_internal_op_dt_check(MPIX_Op op, MPIX_Datatype datatype)
+{
+    return internal_ok((uint32_t) op, (uint32_t) datatype) ? 1 : 0;
+}
+
+MPIX_Datatype MPIX_Datatype_internal(MPIX_Datatype datatype)
+{
+    return (MPIX_Datatype) to_internal((uint32_t) datatype);
+}
+
+MPIX_Aint MPIX_Datatype_extent(MPIX_Datatype datatype)
+{
+    return (MPIX_Aint) extent_of(to_internal((uint32_t) datatype));
+}
+
+int MPIX_Redop_set_fortran_booleans(int true_value, int false_value)
+{
+    g_ftrue = true_value;
+    g_ffalse = false_value;
+    return MPIX_REDOP_SUCCESS;
+}
+
+int MPIX_Redop_set_launch(int block_threads, int max_grid)
+{
+    launch_cfg();
+    if (block_threads < 64 || block_threads > 1024 || block_threads % 64 || max_grid < 0)
+        return MPIX_REDOP_ERR_ARG;
+    g_block = block_threads;
+    g_max_grid = max_grid;
+    return MPIX_REDOP_SUCCESS;
+}
+
+int MPIX_Redop_get_launch(int *block_threads, int *unroll, int *max_grid)
+{
+    LaunchCfg c = launch_cfg();
+    if (block_threads)
+        *block_threads = c.block;
+    if (unroll)
+        *unroll = mpix::unroll();
+    if (max_grid)
+        *max_grid = c.max_grid;
+    return MPIX_REDOP_SUCCESS;
+}
+
+int MPIX_Redop_last_error(void) { return t_last_error; }
+
+const char *MPIX_Redop_error_string(int code)
+{
+    switch (code) {
+        case MPIX_REDOP_SUCCESS: return "success";
+        case MPIX_REDOP_ERR_BUFFER: return "invalid buffer (NULL, MPI_IN_PLACE or aliased)";
+        case MPIX_REDOP_ERR_COUNT: return "invalid count";
+        case MPIX_REDOP_ERR_TYPE: return "datatype unknown or not supported on the GPU path";
+        case MPIX_REDOP_ERR_OP: return "operation not defined for this datatype";
+        case MPIX_REDOP_ERR_ARG: return "invalid argument";
+        case MPIX_REDOP_ERR_OTHER: return "HIP runtime error";
+        default: return "internal error";
+    }
+}
+
+const char *MPIX_Redop_build_info(void)
+{
+#define MPIX_STR2(x) #x
+#define MPIX_STR(x) MPIX_STR2(x)
+    return mpix_build_info();
+}
+
+// ------------------------------------------------ MPIR_op_function table
+#define MPIX_OPFN(name, handle)                                                           \
+    void name(void *invec, void *inoutvec, MPIX_Aint *len, MPIX_Datatype *type)           \
+    {                                                                                     \
+        (void) MPIX_Reduce_local(invec, inoutvec, *len, *type, handle);                  \
+    }
+MPIX_OPFN(MPIX_MAXF, MPIX_MAX)
+MPIX_OPFN(MPIX_MINF, MPIX_MIN)
+MPIX_OPFN(MPIX_SUM_fn, MPIX_SUM)
+MPIX_OPFN(MPIX_PROD_fn, MPIX_PROD)
+MPIX_OPFN(MPIX_LAND_fn, MPIX_LAND)
+MPIX_OPFN(MPIX_BAND_fn, MPIX_BAND)
+MPIX_OPFN(MPIX_LOR_fn, MPIX_LOR)
+MPIX_OPFN(MPIX_BOR_fn, MPIX_BOR)
+MPIX_OPFN(MPIX_LXOR_fn, MPIX_LXOR)
+MPIX_OPFN(MPIX_BXOR_fn, MPIX_BXOR)
+MPIX_OPFN(MPIX_MINLOC_fn, MPIX_MINLOC)
+MPIX_OPFN(MPIX_MAXLOC_fn, MPIX_MAXLOC)
+MPIX_OPFN(MPIX_REPLACE_fn, MPIX_REPLACE)
+MPIX_OPFN(MPIX_NO_OP_fn, MPIX_NO_OP)
+#undef MPIX_OPFN
+
+// order of src/mpi/coll/op/oputil.c:10-27 / mpi.h.in:297-311
+MPIX_op_function *const MPIX_Op_table[16] = {
+    nullptr, MPIX_MAXF, MPIX_MINF, MPIX_SUM_fn, MPIX_PROD_fn, MPIX_LAND_fn, MPIX_BAND_fn,
+    MPIX_LOR_fn, MPIX_BOR_fn, MPIX_LXOR_fn, MPIX_BXOR_fn, MPIX_MINLOC_fn, MPIX_MAXLOC_fn,
+    MPIX_REPLACE_fn, MPIX_NO_OP_fn, nullptr,
+};
+
+}  // extern "C"

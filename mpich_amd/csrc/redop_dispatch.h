@@ -1,0 +1,41 @@
+// redop_dispatch.h -- host-visible interface between the C-ABI
+// (redop_capi.cpp, plain host C++) and the kernel instantiation units
+// (inst_*.hip).  No device code here.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+namespace mpix {
+
+// Runtime parameters some combiners need (Fortran .TRUE./.FALSE.,
+// src/include/mpii_fortlogical.h:15,28).
+struct Params {
+    long long ftrue;
+    long long ffalse;
+};
+
+struct LaunchCfg {
+    int block;          // threads per block (multiple of 64)
+    int max_grid;       // 0 = no cap (one tile per block)
+};
+
+// One (op, type) pair: launchers for the contiguous and the vector-target form.
+struct Entry {
+    hipError_t (*contig)(const void *in, void *io, uint64_t count, const Params &,
+                         const LaunchCfg &, hipStream_t);
+    hipError_t (*vector)(const void *in, void *io, uint64_t count, uint64_t blocklen,
+                         uint64_t stride, const Params &, const LaunchCfg &, hipStream_t);
+};
+
+// Each instantiation unit resolves (raw internal type, op index) to an Entry
+// or returns nullptr.  raw = handle & 0xffffff00 for builtins; struct pair
+// handles 0x8c00000k are passed unchanged.
+const Entry *lookup_int(int raw, int opi);
+const Entry *lookup_fp(int raw, int opi);
+const Entry *lookup_pair(int raw, int opi);
+
+// compile-time unroll of the packet kernel (packets per lane per operand)
+int unroll();
+
+}  // namespace mpix

@@ -1,0 +1,207 @@
+// redop_kernels.h -- streaming kernels for the local reduction (gfx950).
+//
+// The combine is a pure HBM stream: per element 2 loads + 1 store and O(1)
+// integer/fp work, so the kernels are built around the memory system, not
+// the ALUs (no MFMA, no LDS on the contiguous path):
+//   * both operands are read as 16-byte packets (global_load_dwordx4), each
+//     lane keeping MPIX_REDOP_UNROLL packets per operand in flight before the
+//     first combine, so a 256-thread block has 256*U*32 B outstanding;
+//   * inout is written back with 16-byte stores to the lines it just read;
+//   * each packet holds 16/sizeof(unit) elements, combined in registers;
+//   * elements before the first 16-byte boundary of inout (head) and after
+//     the last full packet (tail) are done element-wise by block 0;
+//   * if in and inout disagree modulo 16 bytes, an element-wise grid-stride
+//     kernel is used instead (still coalesced for >= 4-byte units).
+// Launch geometry: one tile of blockDim*U packets per block, grid =
+// ceil(npk / tile) (optionally capped, then grid-stride).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "redop_ops.h"
+
+#ifndef MPIX_REDOP_UNROLL
+#define MPIX_REDOP_UNROLL 4
+#endif
+#ifndef MPIX_REDOP_NT_LOAD
+#define MPIX_REDOP_NT_LOAD 1
+#endif
+#ifndef MPIX_REDOP_NT_STORE
+#define MPIX_REDOP_NT_STORE 1
+#endif
+
+namespace mpix {
+
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+
+template <bool NT> __device__ __forceinline__ v4u ld16(const v4u *p)
+{
+    if constexpr (NT)
+        return __builtin_nontemporal_load(p);
+    else
+        return *p;
+}
+
+template <bool NT> __device__ __forceinline__ void st16(v4u *p, v4u v)
+{
+    if constexpr (NT)
+        __builtin_nontemporal_store(v, p);
+    else
+        *p = v;
+}
+
+template <class C> __device__ __forceinline__ v4u combine16(v4u a, v4u b, const Params &prm)
+{
+    using T = typename C::unit;
+    constexpr int E = 16 / sizeof(T);
+    struct alignas(16) Pk { T u[E]; };
+    static_assert(sizeof(Pk) == 16, "unit must divide 16 bytes");
+    Pk pa = __builtin_bit_cast(Pk, a);
+    Pk pb = __builtin_bit_cast(Pk, b);
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+        pa.u[e] = C::apply(pa.u[e], pb.u[e], prm);
+    return __builtin_bit_cast(v4u, pa);
+}
+
+template <class C, int U, bool NTL, bool NTS>
+__global__ void __launch_bounds__(1024)
+k_contig(const typename C::unit *__restrict__ in, typename C::unit *__restrict__ io,
+         uint64_t head, uint64_t npk, uint64_t tail_start, uint32_t ntail, Params prm)
+{
+    const v4u *__restrict__ vin = reinterpret_cast<const v4u *>(in + head);
+    v4u *__restrict__ vio = reinterpret_cast<v4u *>(io + head);
+    const uint64_t nt = blockDim.x;
+    const uint64_t tile = nt * U;
+    const uint64_t stride = (uint64_t) gridDim.x * tile;
+    for (uint64_t i = (uint64_t) blockIdx.x * tile + threadIdx.x; i < npk; i += stride) {
+        if (i + (U - 1) * nt < npk) {
+            v4u a[U], b[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                a[u] = ld16<NTL>(vio + i + u * nt);
+                b[u] = ld16<NTL>(vin + i + u * nt);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                st16<NTS>(vio + i + u * nt, combine16<C>(a[u], b[u], prm));
+        } else {
+            for (int u = 0; u < U; ++u) {
+                uint64_t k = i + u * nt;
+                if (k < npk)
+                    st16<NTS>(vio + k, combine16<C>(ld16<NTL>(vio + k), ld16<NTL>(vin + k), prm));
+            }
+        }
+    }
+    if (blockIdx.x == 0) {
+        for (uint64_t t = threadIdx.x; t < head; t += nt)
+            io[t] = C::apply(io[t], in[t], prm);
+        for (uint64_t t = threadIdx.x; t < ntail; t += nt)
+            io[tail_start + t] = C::apply(io[tail_start + t], in[tail_start + t], prm);
+    }
+}
+
+template <class C>
+__global__ void __launch_bounds__(1024)
+k_elem(const typename C::unit *__restrict__ in, typename C::unit *__restrict__ io, uint64_t n,
+       Params prm)
+{
+    const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        io[i] = C::apply(io[i], in[i], prm);
+}
+
+// Vector target (typerep_op.c:115-150 for MPI_Type_vector(count, bl, stride)):
+// packed source element j = b*bl + k lands on target element b*stride + k.
+// Thread per source element: the source stream is fully coalesced, the
+// target reads/writes are coalesced within each block run; gap elements are
+// never loaded or stored.
+template <class C>
+__global__ void __launch_bounds__(1024)
+k_vector(const typename C::unit *__restrict__ in, typename C::unit *__restrict__ io, uint64_t n,
+         uint64_t bl, uint64_t st, Params prm)
+{
+    const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
+    for (uint64_t j = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride) {
+        uint64_t b = j / bl, k = j - b * bl;
+        uint64_t t = b * st + k;
+        io[t] = C::apply(io[t], in[j], prm);
+    }
+}
+
+// bl == 1 specialisation: no division
+template <class C>
+__global__ void __launch_bounds__(1024)
+k_vector1(const typename C::unit *__restrict__ in, typename C::unit *__restrict__ io, uint64_t n,
+          uint64_t st, Params prm)
+{
+    const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
+    for (uint64_t j = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride)
+        io[j * st] = C::apply(io[j * st], in[j], prm);
+}
+
+static inline unsigned grid_for(uint64_t work_per_block_units, uint64_t n, int max_grid)
+{
+    uint64_t g = (n + work_per_block_units - 1) / work_per_block_units;
+    if (g == 0)
+        g = 1;
+    if (max_grid > 0 && g > (uint64_t) max_grid)
+        g = (uint64_t) max_grid;
+    if (g > 0x7fffffffull)
+        g = 0x7fffffffull;
+    return (unsigned) g;
+}
+
+// Contiguous launcher: chooses the packet or the element-wise kernel.
+template <class C>
+hipError_t launch_contig(const void *in, void *io, uint64_t count, const Params &prm,
+                         const LaunchCfg &cfg, hipStream_t s)
+{
+    using T = typename C::unit;
+    constexpr uint64_t E = 16 / sizeof(T);
+    const T *tin = static_cast<const T *>(in);
+    T *tio = static_cast<T *>(io);
+    uintptr_t ai = reinterpret_cast<uintptr_t>(in), ao = reinterpret_cast<uintptr_t>(io);
+    if ((ai & 15) == (ao & 15) && (ao % sizeof(T)) == 0) {
+        uint64_t head = ((16 - (ao & 15)) & 15) / sizeof(T);
+        if (head > count)
+            head = count;
+        uint64_t npk = (count - head) / E;
+        uint64_t tail_start = head + npk * E;
+        uint32_t ntail = (uint32_t) (count - tail_start);
+        const uint64_t tile = (uint64_t) cfg.block * MPIX_REDOP_UNROLL;
+        unsigned grid = grid_for(tile, npk, cfg.max_grid);
+        hipLaunchKernelGGL((k_contig<C, MPIX_REDOP_UNROLL, MPIX_REDOP_NT_LOAD, MPIX_REDOP_NT_STORE>),
+                           dim3(grid), dim3(cfg.block), 0, s, tin, tio, head, npk, tail_start,
+                           ntail, prm);
+    } else {
+        unsigned grid = grid_for((uint64_t) cfg.block * 4, count, cfg.max_grid);
+        hipLaunchKernelGGL((k_elem<C>), dim3(grid), dim3(cfg.block), 0, s, tin, tio, count, prm);
+    }
+    return hipGetLastError();
+}
+
+template <class C>
+hipError_t launch_vector(const void *in, void *io, uint64_t count, uint64_t bl, uint64_t st,
+                         const Params &prm, const LaunchCfg &cfg, hipStream_t s)
+{
+    using T = typename C::unit;
+    uint64_t n = count * bl;
+    if (n == 0)
+        return hipSuccess;
+    if (bl == st)       // contiguous after all
+        return launch_contig<C>(in, io, n, prm, cfg, s);
+    unsigned grid = grid_for((uint64_t) cfg.block * 4, n, cfg.max_grid);
+    if (bl == 1)
+        hipLaunchKernelGGL((k_vector1<C>), dim3(grid), dim3(cfg.block), 0, s,
+                           static_cast<const T *>(in), static_cast<T *>(io), n, st, prm);
+    else
+        hipLaunchKernelGGL((k_vector<C>), dim3(grid), dim3(cfg.block), 0, s,
+                           static_cast<const T *>(in), static_cast<T *>(io), n, bl, st, prm);
+    return hipGetLastError();
+}
+
+template <class C> constexpr Entry entry() { return Entry{&launch_contig<C>, &launch_vector<C>}; }
+
+}  // namespace mpix

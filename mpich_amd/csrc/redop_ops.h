@@ -1,0 +1,267 @@
+// redop_ops.h -- CDNA4 (gfx950) element combiners for the predefined MPI_Ops.
+//
+// One combiner per (op, element type).  Each has
+//     using unit = <storage of one element, 1..16 bytes>;
+//     static __device__ unit apply(unit a, unit b, const Params &p);
+// computing the new inout element from a = inoutvec[i], b = invec[i], which is
+// MPICH's operand order (src/include/mpir_op_util.h:46-53).  The semantics
+// restate src/mpi/coll/op/op_fns.c; see DESIGN.md §Semantics for the full
+// table and the oracle/ restatement they are checked against.
+//
+// Compile with -ffp-contract=off and no fast-math: every floating-point result
+// must be the single IEEE-rounded operation the C loop performs.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "redop_dispatch.h"
+
+namespace mpix {
+
+#define MPIX_DEV __device__ __forceinline__
+
+// ---------------------------------------------------------------- integers
+// SUM/PROD are computed in an unsigned type at least int-wide and cast back:
+// the reference's "(c_type_) (a OP b)" on promoted operands, i.e. wrap modulo
+// 2^bits, without the signed-overflow UB.
+template <typename T> struct Wide { using type = uint32_t; };
+template <> struct Wide<int64_t> { using type = uint64_t; };
+template <> struct Wide<uint64_t> { using type = uint64_t; };
+template <> struct Wide<__int128> { using type = unsigned __int128; };
+template <> struct Wide<unsigned __int128> { using type = unsigned __int128; };
+
+template <typename T> struct IMax {
+    using unit = T;
+    static MPIX_DEV T apply(T a, T b, const Params &) { return (a > b) ? a : b; }
+};
+template <typename T> struct IMin {
+    using unit = T;
+    static MPIX_DEV T apply(T a, T b, const Params &) { return (a < b) ? a : b; }
+};
+template <typename T> struct ISum {
+    using unit = T;
+    using W = typename Wide<T>::type;
+    static MPIX_DEV T apply(T a, T b, const Params &) { return (T) ((W) a + (W) b); }
+};
+template <typename T> struct IProd {
+    using unit = T;
+    using W = typename Wide<T>::type;
+    static MPIX_DEV T apply(T a, T b, const Params &) { return (T) ((W) a * (W) b); }
+};
+template <typename T> struct ILand {
+    using unit = T;
+    static MPIX_DEV T apply(T a, T b, const Params &) { return (T) ((a != 0) & (b != 0)); }
+};
+template <typename T> struct ILor {
+    using unit = T;
+    static MPIX_DEV T apply(T a, T b, const Params &) { return (T) ((a != 0) | (b != 0)); }
+};
+template <typename T> struct ILxor {
+    using unit = T;
+    static MPIX_DEV T apply(T a, T b, const Params &) { return (T) ((a != 0) ^ (b != 0)); }
+};
+template <typename T> struct IBand {
+    using unit = T;
+    static MPIX_DEV T apply(T a, T b, const Params &) { return a & b; }
+};
+template <typename T> struct IBor {
+    using unit = T;
+    static MPIX_DEV T apply(T a, T b, const Params &) { return a | b; }
+};
+template <typename T> struct IBxor {
+    using unit = T;
+    static MPIX_DEV T apply(T a, T b, const Params &) { return a ^ b; }
+};
+
+// Fortran logicals: MPII_FROM_FLOG(x) = (x == .FALSE. ? 0 : 1), compared after
+// the usual promotion; MPII_TO_FLOG(c) = c ? .TRUE. : .FALSE. cast to T.
+template <typename T> struct FlogW { using type = long long; };
+template <> struct FlogW<__int128> { using type = __int128; };
+template <typename T> MPIX_DEV int flog_from(T x, const Params &p)
+{
+    using W = typename FlogW<T>::type;
+    return ((W) x == (W) p.ffalse) ? 0 : 1;
+}
+template <typename T> MPIX_DEV T flog_to(int c, const Params &p)
+{
+    return (T) (c ? p.ftrue : p.ffalse);
+}
+template <typename T> struct FLand {
+    using unit = T;
+    static MPIX_DEV T apply(T a, T b, const Params &p)
+    {
+        return flog_to<T>(flog_from(a, p) & flog_from(b, p), p);
+    }
+};
+template <typename T> struct FLor {
+    using unit = T;
+    static MPIX_DEV T apply(T a, T b, const Params &p)
+    {
+        return flog_to<T>(flog_from(a, p) | flog_from(b, p), p);
+    }
+};
+template <typename T> struct FLxor {
+    using unit = T;
+    static MPIX_DEV T apply(T a, T b, const Params &p)
+    {
+        return flog_to<T>(flog_from(a, p) ^ flog_from(b, p), p);
+    }
+};
+
+// ------------------------------------------------------------ floating point
+// MAX/MIN are MPL_MAX/MPL_MIN selects (src/mpl/include/mpl_base.h:105-106):
+// with a NaN on either side the result is b, bit for bit; MAX(+0,-0) = -0.
+// hipcc lowers these to v_cmp + v_cndmask (not v_max_*, whose NaN/zero
+// rules differ).
+template <typename T> struct FMax {
+    using unit = T;
+    static MPIX_DEV T apply(T a, T b, const Params &) { return (a > b) ? a : b; }
+};
+template <typename T> struct FMin {
+    using unit = T;
+    static MPIX_DEV T apply(T a, T b, const Params &) { return (a < b) ? a : b; }
+};
+template <typename T> struct FSum {
+    using unit = T;
+    static MPIX_DEV T apply(T a, T b, const Params &) { return a + b; }
+};
+template <typename T> struct FProd {
+    using unit = T;
+    static MPIX_DEV T apply(T a, T b, const Params &) { return a * b; }
+};
+
+// bf16 SUM (op_fns.c:459-493): widen, fp32 add, store (u>>16) + ((u&0x8000)?1:0),
+// i.e. round half away on the magnitude bits, no NaN special case.
+struct Bf16Sum {
+    using unit = uint16_t;
+    static MPIX_DEV uint16_t apply(uint16_t a, uint16_t b, const Params &)
+    {
+        float fa = __builtin_bit_cast(float, (uint32_t) a << 16);
+        float fb = __builtin_bit_cast(float, (uint32_t) b << 16);
+        uint32_t u = __builtin_bit_cast(uint32_t, fa + fb);
+        return (uint16_t) ((u >> 16) + ((u & 0x8000u) ? 1u : 0u));
+    }
+};
+
+// ------------------------------------------------------------------ complex
+template <typename R> struct alignas(2 * sizeof(R)) Cplx {
+    R re, im;
+};
+
+// component-wise SUM (op_fns.c:27-42)
+template <typename R> struct CSum {
+    using unit = Cplx<R>;
+    static MPIX_DEV unit apply(unit a, unit b, const Params &)
+    {
+        unit c;
+        c.re = a.re + b.re;
+        c.im = a.im + b.im;
+        return c;
+    }
+};
+
+// C-native complex product (MPIR_OP_TYPE_GROUP(C_COMPLEX), op_fns.c:61-71):
+// what "a * b" on float/double _Complex computes under C99 Annex G -- the
+// plain (ac-bd, ad+bc) and, only when both parts come out NaN, the
+// infinity-recovery of G.5.1 (libgcc __mulsc3/__muldc3).  a = inout, b = in.
+template <typename R> MPIX_DEV R cpsign(R mag, R sgn) { return __builtin_copysign(mag, sgn); }
+template <> MPIX_DEV float cpsign<float>(float mag, float sgn) { return __builtin_copysignf(mag, sgn); }
+
+template <typename R> struct CProdAnnexG {
+    using unit = Cplx<R>;
+    static MPIX_DEV unit apply(unit x, unit y, const Params &)
+    {
+        R a = x.re, b = x.im, c = y.re, d = y.im;
+        R ac = a * c, bd = b * d, ad = a * d, bc = b * c;
+        unit z;
+        z.re = ac - bd;
+        z.im = ad + bc;
+        if (__builtin_expect(__builtin_isnan(z.re) && __builtin_isnan(z.im), 0))
+            z = recover(a, b, c, d, ac, bd, ad, bc, z);
+        return z;
+    }
+    static __device__ __noinline__ unit recover(R a, R b, R c, R d, R ac, R bd, R ad, R bc, unit z)
+    {
+        bool recalc = false;
+        const R one = 1, zero = 0;
+        if (__builtin_isinf(a) || __builtin_isinf(b)) {
+            a = cpsign(__builtin_isinf(a) ? one : zero, a);
+            b = cpsign(__builtin_isinf(b) ? one : zero, b);
+            if (__builtin_isnan(c)) c = cpsign(zero, c);
+            if (__builtin_isnan(d)) d = cpsign(zero, d);
+            recalc = true;
+        }
+        if (__builtin_isinf(c) || __builtin_isinf(d)) {
+            c = cpsign(__builtin_isinf(c) ? one : zero, c);
+            d = cpsign(__builtin_isinf(d) ? one : zero, d);
+            if (__builtin_isnan(a)) a = cpsign(zero, a);
+            if (__builtin_isnan(b)) b = cpsign(zero, b);
+            recalc = true;
+        }
+        if (!recalc && (__builtin_isinf(ac) || __builtin_isinf(bd) ||
+                        __builtin_isinf(ad) || __builtin_isinf(bc))) {
+            if (__builtin_isnan(a)) a = cpsign(zero, a);
+            if (__builtin_isnan(b)) b = cpsign(zero, b);
+            if (__builtin_isnan(c)) c = cpsign(zero, c);
+            if (__builtin_isnan(d)) d = cpsign(zero, d);
+            recalc = true;
+        }
+        if (recalc) {
+            const R inf = __builtin_huge_val();
+            R t0 = a * c, t1 = b * d, t2 = a * d, t3 = b * c;
+            z.re = inf * (t0 - t1);
+            z.im = inf * (t2 + t3);
+        }
+        return z;
+    }
+};
+
+// struct complex (MPIR_OP_TYPE_GROUP(COMPLEX), op_fns.c:74-85) on fp16 parts:
+// re = c.re*b.re - c.im*b.im; im = c.im*b.re + c.re*b.im, each fp16 op
+// rounded (native _Float16, no excess precision on gfx950).
+struct CProdHalf {
+    using unit = Cplx<_Float16>;
+    static MPIX_DEV unit apply(unit x, unit y, const Params &)
+    {
+        _Float16 p1 = x.re * y.re, p2 = x.im * y.im, p3 = x.im * y.re, p4 = x.re * y.im;
+        unit z;
+        z.re = p1 - p2;
+        z.im = p3 + p4;
+        return z;
+    }
+};
+
+// -------------------------------------------------------------- pair types
+// MAXLOC/MINLOC (op_fns.c:299-435): if a.v < b.v (MAXLOC) take b's value and
+// loc; else if a.v <= b.v (a tie) loc = MPL_MIN(a.loc, b.loc); NaN in either
+// value leaves a unchanged.  Padding bytes of a are preserved.
+template <typename V, typename L> struct alignas(sizeof(V) >= sizeof(L) ? sizeof(V) : sizeof(L)) BPair {
+    V v;
+    L l;
+};
+struct alignas(8) FloatInt { float v; int32_t l; };
+struct alignas(8) DoubleIntBody { double v; int32_t l; int32_t pad; };
+struct alignas(8) LongIntBody { int64_t v; int32_t l; int32_t pad; };
+struct alignas(8) ShortInt { int16_t v; int16_t pad; int32_t l; };
+
+template <typename P, bool IsMax> struct Loc {
+    using unit = P;
+    static MPIX_DEV P apply(P a, P b, const Params &)
+    {
+        bool take = IsMax ? (a.v < b.v) : (a.v > b.v);
+        bool tie = IsMax ? (a.v <= b.v) : (a.v >= b.v);
+        P r = a;
+        if (take) {
+            r.v = b.v;
+            r.l = b.l;
+        } else if (tie) {
+            r.l = (a.l < b.l) ? a.l : b.l;
+        }
+        return r;
+    }
+};
+
+#undef MPIX_DEV
+
+}  // namespace mpix

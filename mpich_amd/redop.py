@@ -1,0 +1,165 @@
+"""Host-side binding of libmpix_redop.so -- the MI355X local reduction.
+
+Mirrors the reference interface for this path: MPI_Reduce_local /
+MPIR_Reduce_local (src/mpi/coll/reduce_local/reduce_local.c:53-96) with the
+same argument meaning (inbuf, inoutbuf, count, datatype, op) and MPI error
+classes as return values, plus the stream-ordered and vector-target forms of
+include/mpix_redop.h.  Buffers may be torch tensors, numpy arrays or raw
+integer addresses.
+
+This module never computes anything itself: every call goes to the HIP
+library, and importing it fails loudly if the library was not built.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (load torch's HIP runtime first: one runtime per process)
+
+from . import handles as H
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libmpix_redop.so')
+
+_lib = None
+
+
+class RedopError(RuntimeError):
+    def __init__(self, code, what=''):
+        self.code = code
+        super().__init__('%s: MPI error class %d (%s)' % (what or 'mpix_redop', code,
+                                                         error_string(code) if _lib else '?'))
+
+
+def lib():
+    """The loaded C-ABI library (raises if the HIP build is missing)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError('libmpix_redop.so is not built (%s); run '
+                              '`python -c "import __graft_entry__ as g; g.build()"` '
+                              'or `make -C mpich_amd/csrc`' % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        vp, i32, aint = ctypes.c_void_p, ctypes.c_int, ctypes.c_ssize_t
+        sig = {
+            'MPIX_Redop_init': ([], i32),
+            'MPIX_Redop_finalize': ([], i32),
+            'MPIX_Reduce_local': ([vp, vp, aint, i32, i32], i32),
+            'MPIX_Reduce_local_async': ([vp, vp, aint, i32, i32, vp], i32),
+            'MPIX_Reduce_local_vector': ([vp, vp, aint, aint, aint, i32, i32], i32),
+            'MPIX_Reduce_local_vector_async': ([vp, vp, aint, aint, aint, i32, i32, vp], i32),
+            'MPIX_Redop_is_supported': ([i32, aint, i32], i32),
+            'MPIX_Redop_op_dt_check': ([i32, i32], i32),
+            'MPIX_Redop_internal_op_dt_check': ([i32, i32], i32),
+            'MPIX_Datatype_internal': ([i32], i32),
+            'MPIX_Datatype_extent': ([i32], aint),
+            'MPIX_Redop_set_fortran_booleans': ([i32, i32], i32),
+            'MPIX_Redop_set_launch': ([i32, i32], i32),
+            'MPIX_Redop_get_launch': ([ctypes.POINTER(i32)] * 3, i32),
+            'MPIX_Redop_last_error': ([], i32),
+            'MPIX_Redop_error_string': ([i32], ctypes.c_char_p),
+            'MPIX_Redop_build_info': ([], ctypes.c_char_p),
+        }
+        for name, (args, res) in sig.items():
+            f = getattr(L, name)
+            f.argtypes = args
+            f.restype = res
+        _lib = L
+    return _lib
+
+
+def _addr(buf):
+    if buf is None:
+        return None
+    if isinstance(buf, int):
+        return buf
+    if isinstance(buf, torch.Tensor):
+        return buf.data_ptr()
+    if hasattr(buf, 'ctypes'):          # numpy
+        return buf.ctypes.data
+    raise TypeError('unsupported buffer type %r' % type(buf))
+
+
+def _stream_ptr(stream):
+    if stream is None:
+        return torch.cuda.current_stream().cuda_stream
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream
+
+
+def MPI_Reduce_local(inbuf, inoutbuf, count, datatype, op):
+    """inoutbuf = inoutbuf OP inbuf, synchronous; returns an MPI error class.
+
+    Device buffers must be ready (the caller orders its own streams, as an
+    MPI caller does); host buffers are staged through the device."""
+    return lib().MPIX_Reduce_local(_addr(inbuf), _addr(inoutbuf), count, H.as_c_int(datatype),
+                                   H.as_c_int(op))
+
+
+def reduce_local_async(inbuf, inoutbuf, count, datatype, op, stream=None):
+    """Enqueue the combine on `stream` (default: torch's current stream)."""
+    return lib().MPIX_Reduce_local_async(_addr(inbuf), _addr(inoutbuf), count,
+                                         H.as_c_int(datatype), H.as_c_int(op),
+                                         _stream_ptr(stream))
+
+
+def reduce_local_vector(inbuf, inoutbuf, count, blocklen, stride, basic_type, op, stream=None,
+                        sync=False):
+    """Vector target / packed source (typerep_op.c:115-150)."""
+    if sync:
+        return lib().MPIX_Reduce_local_vector(_addr(inbuf), _addr(inoutbuf), count, blocklen,
+                                              stride, H.as_c_int(basic_type), H.as_c_int(op))
+    return lib().MPIX_Reduce_local_vector_async(_addr(inbuf), _addr(inoutbuf), count, blocklen,
+                                                stride, H.as_c_int(basic_type), H.as_c_int(op),
+                                                _stream_ptr(stream))
+
+
+def check(rc, what='MPI_Reduce_local'):
+    if rc != H.MPI_SUCCESS:
+        raise RedopError(rc, what)
+    return rc
+
+
+def is_supported(op, datatype, count=0):
+    return bool(lib().MPIX_Redop_is_supported(H.as_c_int(op), count, H.as_c_int(datatype)))
+
+
+def op_dt_check(op, datatype):
+    return bool(lib().MPIX_Redop_op_dt_check(H.as_c_int(op), H.as_c_int(datatype)))
+
+
+def internal_op_dt_check(op, datatype):
+    return bool(lib().MPIX_Redop_internal_op_dt_check(H.as_c_int(op), H.as_c_int(datatype)))
+
+
+def datatype_internal(datatype):
+    return lib().MPIX_Datatype_internal(H.as_c_int(datatype)) & 0xffffffff
+
+
+def datatype_extent(datatype):
+    return lib().MPIX_Datatype_extent(H.as_c_int(datatype))
+
+
+def set_fortran_booleans(true_value, false_value):
+    return lib().MPIX_Redop_set_fortran_booleans(true_value, false_value)
+
+
+def set_launch(block_threads=256, max_grid=0):
+    return lib().MPIX_Redop_set_launch(block_threads, max_grid)
+
+
+def get_launch():
+    b, u, g = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    lib().MPIX_Redop_get_launch(ctypes.byref(b), ctypes.byref(u), ctypes.byref(g))
+    return dict(block=b.value, unroll=u.value, max_grid=g.value)
+
+
+def error_string(code):
+    return lib().MPIX_Redop_error_string(code).decode()
+
+
+def build_info():
+    return lib().MPIX_Redop_build_info().decode()
+
+
+def finalize():
+    return lib().MPIX_Redop_finalize()

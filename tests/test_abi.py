@@ -1,0 +1,126 @@
+"""CPU-side checks of the C-ABI boundary (no GPU compute calls):
+libmpix_redop.so loads, exports every function/object include/mpix_redop.h
+declares, and its handle tables / legality matrix / support predicate agree
+with the oracle's independent restatement of the reference's tables."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, 'include', 'mpix_redop.h')
+
+
+def declared_symbols():
+    src = open(HEADER).read()
+    src = re.sub(r'/\*.*?\*/', '', src, flags=re.S)
+    funcs = set(re.findall(r'\b(MPIX_\w+)\s*\(', src))
+    funcs -= {m for m in funcs if re.search(r'#define\s+' + m + r'\b', src)}
+    funcs -= set(re.findall(r'typedef\s+\w+\s+(MPIX_\w+)\s*\(', src))
+    objs = set(re.findall(r'extern\s+MPIX_op_function\s*\*\s*const\s+(MPIX_\w+)', src))
+    return funcs | objs
+
+
+@pytest.fixture(scope='module')
+def R():
+    from mpich_amd import redop
+    return redop
+
+
+def test_library_exports_every_declared_symbol(R):
+    L = R.lib()
+    syms = declared_symbols()
+    assert len(syms) >= 30
+    missing = [s for s in sorted(syms) if not hasattr(L, s)]
+    assert not missing, missing
+
+
+def test_op_table_layout(R):
+    L = R.lib()
+    tab = (ctypes.c_void_p * 16).in_dll(L, 'MPIX_Op_table')
+    # oputil.c:10-27 order: NULL, MAX, MIN, SUM, PROD, LAND, BAND, LOR, BOR,
+    # LXOR, BXOR, MINLOC, MAXLOC, REPLACE, NO_OP, (EQUAL not provided)
+    names = [None, 'MPIX_MAXF', 'MPIX_MINF', 'MPIX_SUM_fn', 'MPIX_PROD_fn', 'MPIX_LAND_fn',
+             'MPIX_BAND_fn', 'MPIX_LOR_fn', 'MPIX_BOR_fn', 'MPIX_LXOR_fn', 'MPIX_BXOR_fn',
+             'MPIX_MINLOC_fn', 'MPIX_MAXLOC_fn', 'MPIX_REPLACE_fn', 'MPIX_NO_OP_fn', None]
+    for i, n in enumerate(names):
+        if n is None:
+            assert not tab[i]
+        else:
+            assert tab[i] == ctypes.cast(getattr(L, n), ctypes.c_void_p).value
+
+
+def all_handles():
+    from mpich_amd import handles as H
+    ext = [v for k, v in vars(H).items() if k.startswith(('MPI_', 'MPIX_')) and isinstance(v, int)
+           and (v >> 24) in (0x4c, 0x8c)]
+    internal = [v for k, v in vars(H).items() if k.startswith('MPIR_')]
+    return sorted(set(ext + internal + [0x4c0000ff, 0x4c000012, 0x8c000007]))
+
+
+def test_tables_agree_with_oracle(R, oracle):
+    from mpich_amd import handles as H
+    for dt in all_handles():
+        assert R.datatype_internal(dt) == oracle.internal(dt), hex(dt)
+        assert R.datatype_extent(dt) == oracle.extent(dt), hex(dt)
+        for op in H.OPS.values():
+            assert R.op_dt_check(op, dt) == oracle.op_dt_check(op, dt), (hex(op), hex(dt))
+            it = R.datatype_internal(dt)
+            assert R.internal_op_dt_check(op, it) == oracle.internal_op_dt_check(op, it), \
+                (hex(op), hex(dt))
+
+
+def test_support_predicate(R):
+    """MPIR_Typerep_reduce_is_supported mirror: everything legal except the
+    types with no gfx950 arithmetic (x87 long double, __float128) and the bf16
+    ops the reference itself asserts on."""
+    from mpich_amd import handles as H
+    unsupported_types = {H.MPI_LONG_DOUBLE, H.MPI_REAL16, H.MPI_COMPLEX32,
+                         H.MPI_C_LONG_DOUBLE_COMPLEX, H.MPI_CXX_LONG_DOUBLE_COMPLEX,
+                         H.MPI_LONG_DOUBLE_INT}
+    no_gpu_raw = {H.MPIR_FLOAT128, H.MPIR_COMPLEX128, H.MPIR_ALT_FLOAT128, H.MPIR_ALT_COMPLEX128}
+    n_supported = 0
+    for dt in all_handles():
+        for name, op in H.OPS.items():
+            legal = R.internal_op_dt_check(op, R.datatype_internal(dt))
+            sup = R.is_supported(op, dt)
+            if sup:
+                n_supported += 1
+                assert legal
+            elif legal and op not in (H.MPI_REPLACE, H.MPI_NO_OP):
+                raw = R.datatype_internal(dt) & 0xffffff00
+                ok = (dt in unsupported_types or raw in no_gpu_raw or
+                      (raw == H.MPIR_BFLOAT16 and op != H.MPI_SUM))
+                assert ok, (name, hex(dt))
+    assert n_supported > 300
+    assert R.is_supported(H.MPI_SUM, H.MPI_FLOAT)
+    assert R.is_supported(H.MPI_MAXLOC, H.MPI_SHORT_INT)
+    assert not R.is_supported(H.MPI_SUM, H.MPI_LONG_DOUBLE)
+    assert not R.is_supported(H.MPI_BAND, H.MPI_FLOAT)
+
+
+def test_errors_without_gpu(R):
+    """argument errors are detected before any device work
+    (binding_c.py:2774-2783 checks; count==0 is a no-op, reduce_local.c:59-60)."""
+    from mpich_amd import handles as H
+    assert R.MPI_Reduce_local(0, 0, 0, H.MPI_FLOAT, H.MPI_SUM) == H.MPI_SUCCESS
+    assert R.MPI_Reduce_local(4096, 8192, -1, H.MPI_FLOAT, H.MPI_SUM) == H.MPI_ERR_COUNT
+    assert R.MPI_Reduce_local(4096, 4096, 10, H.MPI_FLOAT, H.MPI_SUM) == H.MPI_ERR_BUFFER
+    assert R.MPI_Reduce_local(4096, 4100, 10, H.MPI_FLOAT, H.MPI_SUM) == H.MPI_ERR_BUFFER
+    assert R.MPI_Reduce_local(2 ** 64 - 1, 8192, 10, H.MPI_INT, H.MPI_SUM) == H.MPI_ERR_BUFFER
+    assert R.MPI_Reduce_local(0, 8192, 10, H.MPI_INT, H.MPI_SUM) == H.MPI_ERR_BUFFER
+    assert R.MPI_Reduce_local(4096, 1 << 20, 10, H.MPI_FLOAT, H.MPI_BAND) == H.MPI_ERR_OP
+    assert R.MPI_Reduce_local(4096, 1 << 20, 10, H.MPI_INT, H.MPI_MAXLOC) == H.MPI_ERR_OP
+    assert R.MPI_Reduce_local(4096, 1 << 20, 10, H.MPI_PACKED, H.MPI_SUM) == H.MPI_ERR_OP
+    assert R.MPI_Reduce_local(4096, 1 << 20, 10, 0x4c0000ff, H.MPI_SUM) == H.MPI_ERR_TYPE
+    assert R.MPI_Reduce_local(4096, 1 << 20, 10, H.MPI_INT, H.MPI_OP_NULL) == H.MPI_ERR_OP
+    assert R.MPI_Reduce_local(4096, 1 << 20, 10, H.MPI_LONG_DOUBLE, H.MPI_SUM) == H.MPI_ERR_TYPE
+
+
+def test_launch_knobs(R):
+    cfg = R.get_launch()
+    assert cfg['block'] % 64 == 0 and cfg['unroll'] >= 1
+    assert R.set_launch(100, 0) == 12
+    assert R.set_launch(cfg['block'], cfg['max_grid']) == 0
+    assert 'gfx950' in R.build_info()

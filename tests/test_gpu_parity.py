@@ -1,0 +1,409 @@
+"""GPU parity: the HIP path through the C-ABI against the oracle and the
+golden vectors.  Bit-exact for integer, logical, bitwise, MAX/MIN and
+MAXLOC/MINLOC; bit-exact for FP SUM/PROD too (one IEEE op per element on
+both sides) except that a NaN result only has to be a NaN (payload bits of
+arithmetic NaNs are unpinned: x86 and gfx950 pick different default NaNs).
+
+Sizes: MPIX_PARITY_BYTES per operand (default 4 MiB) for the random sweep;
+the BASELINE configs' full sizes are covered by the *_full tests.
+"""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from tests import golden_util as gu
+
+pytestmark = pytest.mark.gpu
+
+SWEEP_BYTES = int(os.environ.get('MPIX_PARITY_BYTES', 4 << 20))
+
+
+@pytest.fixture(scope='module')
+def R():
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    from mpich_amd import redop
+    assert redop.lib().MPIX_Redop_init() == 0
+    return redop
+
+
+@pytest.fixture(scope='module')
+def H():
+    from mpich_amd import handles
+    return handles
+
+
+def dev(a):
+    """numpy bytes -> device uint8 tensor (synchronised)"""
+    t = torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1).copy()).cuda()
+    torch.cuda.synchronize()
+    return t
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+# --------------------------------------------------------------- generators
+def gen_int(rng, n, size, logical=False):
+    a = rng.integers(0, 256, n * size, dtype=np.uint8)
+    if logical:
+        z = rng.random(n) < 0.3
+        a.reshape(n, size)[z] = 0
+    return a
+
+
+def gen_float(rng, n, npt):
+    x = rng.uniform(-1, 1, n).astype(npt)
+    sp = np.array([0.0, -0.0, np.inf, -np.inf, np.nan], npt)
+    k = rng.random(n) < 0.01
+    x[k] = sp[rng.integers(0, len(sp), k.sum())]
+    if npt == np.float32:
+        d = rng.random(n) < 0.003        # subnormals must not be flushed
+        x[d] = (rng.uniform(-1, 1, d.sum()) * 1e-39).astype(np.float32)
+    return x.view(np.uint8)
+
+
+def gen_bf16(rng, n):
+    f = rng.uniform(-4, 4, n).astype(np.float32)
+    k = rng.random(n) < 0.01
+    f[k] = np.array([np.inf, -np.inf, 0.0, -0.0], np.float32)[rng.integers(0, 4, k.sum())]
+    b = (f.view(np.uint32) >> 16).astype(np.uint16)
+    b ^= rng.integers(0, 2, n, dtype=np.uint16)      # odd low bits: ties-away cases
+    b[((b & 0x7f80) == 0x7f80) & ((b & 0x7f) != 0)] = 0x3f80
+    return b.view(np.uint8)
+
+
+def gen_logical(rng, n, size):
+    vals = np.array([0, 1, -1, 5, 0], np.int64)
+    v = vals[rng.integers(0, len(vals), n)]
+    return v.astype('<i%d' % size).view(np.uint8) if size <= 8 else \
+        np.stack([v, np.where(v < 0, -1, 0)], 1).astype('<i8').view(np.uint8).reshape(-1)
+
+
+def gen_pair(rng, n, vdt, ldt, ext, loff, floaty):
+    buf = rng.integers(0, 256, n * ext, dtype=np.uint8).reshape(n, ext)   # random padding
+    if floaty:
+        v = rng.integers(0, 16, n).astype(vdt)
+        v[rng.random(n) < 0.02] = np.nan
+    else:
+        v = rng.integers(0, 16, n).astype(vdt)
+    lv = rng.integers(-1000, 1000, n).astype(ldt)
+    buf[:, :np.dtype(vdt).itemsize] = v.view(np.uint8).reshape(n, -1)
+    buf[:, loff:loff + np.dtype(ldt).itemsize] = lv.view(np.uint8).reshape(n, -1)
+    return buf.reshape(-1)
+
+
+def _sweep():
+    from mpich_amd import handles as H
+    I = ['MPI_MAX', 'MPI_MIN', 'MPI_SUM', 'MPI_PROD', 'MPI_LAND', 'MPI_BAND', 'MPI_LOR',
+         'MPI_BOR', 'MPI_LXOR', 'MPI_BXOR']
+    F = ['MPI_MAX', 'MPI_MIN', 'MPI_SUM', 'MPI_PROD']
+    L = ['MPI_LAND', 'MPI_LOR', 'MPI_LXOR']
+    LOC = ['MPI_MAXLOC', 'MPI_MINLOC']
+    out = []
+    for nm, size in (('MPI_INT8_T', 1), ('MPI_INT16_T', 2), ('MPI_INT32_T', 4), ('MPI_INT64_T', 8),
+                     ('MPI_UINT8_T', 1), ('MPI_UINT16_T', 2), ('MPI_UINT32_T', 4),
+                     ('MPI_UINT64_T', 8), ('MPI_INTEGER16', 16), ('MPIR_UINT128', 16)):
+        for op in I:
+            out.append((nm, op, 'int', size))
+    for op in ('MPI_BAND', 'MPI_BOR', 'MPI_BXOR'):
+        out.append(('MPI_BYTE', op, 'int', 1))
+    for op in L:
+        out.append(('MPI_C_BOOL', op, 'int', 1))
+        for nm, size in (('MPI_LOGICAL1', 1), ('MPI_LOGICAL2', 2), ('MPI_LOGICAL4', 4),
+                         ('MPI_LOGICAL8', 8), ('MPI_LOGICAL16', 16)):
+            out.append((nm, op, 'flog', size))
+    for nm, size in (('MPIX_C_FLOAT16', 2), ('MPI_FLOAT', 4), ('MPI_DOUBLE', 8)):
+        for op in F:
+            out.append((nm, op, 'fp', size))
+    out.append(('MPIX_BFLOAT16', 'MPI_SUM', 'bf16', 2))
+    for nm, size in (('MPI_COMPLEX4', 2), ('MPI_C_FLOAT_COMPLEX', 4), ('MPI_C_DOUBLE_COMPLEX', 8)):
+        for op in ('MPI_SUM', 'MPI_PROD'):
+            out.append((nm, op, 'cplx', size))
+    pairs = [('MPI_2INT', '<i4', '<i4', 8, 4), ('MPI_2REAL', '<f4', '<f4', 8, 4),
+             ('MPI_2DOUBLE_PRECISION', '<f8', '<f8', 16, 8), ('MPI_FLOAT_INT', '<f4', '<i4', 8, 4),
+             ('MPI_DOUBLE_INT', '<f8', '<i4', 16, 8), ('MPI_LONG_INT', '<i8', '<i4', 16, 8),
+             ('MPI_SHORT_INT', '<i2', '<i4', 8, 4), ('MPIR_2INT8', '<i1', '<i1', 2, 1),
+             ('MPIR_2INT16', '<i2', '<i2', 4, 2), ('MPIR_2INT64', '<i8', '<i8', 16, 8),
+             ('MPIR_2UINT8', '<u1', '<u1', 2, 1), ('MPIR_2UINT16', '<u2', '<u2', 4, 2),
+             ('MPIR_2UINT32', '<u4', '<u4', 8, 4), ('MPIR_2UINT64', '<u8', '<u8', 16, 8),
+             ('MPIR_2FLOAT16', '<f2', '<f2', 4, 2)]
+    for p in pairs:
+        for op in LOC:
+            out.append((p[0], op, ('pair',) + p[1:], None))
+    del H
+    return out
+
+
+SWEEP = _sweep()
+
+
+def make_operand(rng, kind, size, n, dtname):
+    if kind == 'int':
+        return gen_int(rng, n, size, logical=True)
+    if kind == 'flog':
+        return gen_logical(rng, n, size)
+    if kind == 'fp':
+        return gen_float(rng, n, {2: np.float16, 4: np.float32, 8: np.float64}[size])
+    if kind == 'bf16':
+        return gen_bf16(rng, n)
+    if kind == 'cplx':
+        return gen_float(rng, 2 * n, {2: np.float16, 4: np.float32, 8: np.float64}[size])
+    vdt, ldt, ext, loff = kind[1:]
+    return gen_pair(rng, n, vdt, ldt, ext, loff, vdt.startswith('<f'))
+
+
+def nan_mask(raw, kind, size):
+    """per-element NaN flag of a result buffer for the nan-equivalent kinds"""
+    if kind == 'fp':
+        return np.isnan(raw.view({2: np.float16, 4: np.float32, 8: np.float64}[size]))
+    if kind == 'cplx':
+        f = np.isnan(raw.view({2: np.float16, 4: np.float32, 8: np.float64}[size]))
+        return f.reshape(-1, 2).any(1)
+    if kind == 'bf16':
+        b = raw.view(np.uint16)
+        return ((b & 0x7f80) == 0x7f80) & ((b & 0x7f) != 0)
+    return None
+
+
+def compare(got, exp, kind, size, op, ext):
+    """number of mismatching elements under the module's parity rule"""
+    g = got.reshape(-1, ext)
+    e = exp.reshape(-1, ext)
+    bad = (g != e).any(1)
+    if op in ('MPI_SUM', 'MPI_PROD') and kind in ('fp', 'cplx', 'bf16'):
+        gn = nan_mask(got, kind, size)
+        en = nan_mask(exp, kind, size)
+        if kind == 'cplx':
+            # a NaN component must be NaN on both sides, the rest bit-exact
+            comp = {2: np.float16, 4: np.float32, 8: np.float64}[size]
+            gc, ec = got.view(comp).reshape(-1, 2), exp.view(comp).reshape(-1, 2)
+            gcn, ecn = np.isnan(gc), np.isnan(ec)
+            cmp_bits = (gc.view(np.uint8).reshape(len(gc), 2, size) !=
+                        ec.view(np.uint8).reshape(len(ec), 2, size)).any(2)
+            cbad = np.where(gcn | ecn, gcn != ecn, cmp_bits).any(1)
+            return int(cbad.sum())
+        bad = np.where(gn | en, gn != en, bad)
+    return int(bad.sum())
+
+
+@pytest.mark.parametrize('dtname,opname,kind,size', SWEEP,
+                         ids=['%s-%s' % (s[0], s[1]) for s in SWEEP])
+def test_random_parity(R, H, oracle, dtname, opname, kind, size):
+    dt, op = getattr(H, dtname), getattr(H, opname)
+    assert R.is_supported(op, dt), (dtname, opname)
+    ext = R.datatype_extent(dt)
+    n = max(1, SWEEP_BYTES // ext) + 7          # ragged: not a multiple of any packet
+    rng = np.random.default_rng((0x5EED0003 * 31 + dt * 7 + op) & 0xffffffff)
+    a = make_operand(rng, kind, size, n, dtname)
+    b = make_operand(rng, kind, size, n, dtname)
+    exp = a.copy()
+    assert oracle.reduce_local(b.copy(), exp, n, dt, op) == 0
+    da, db = dev(a), dev(b)
+    assert R.MPI_Reduce_local(db, da, n, dt, op) == 0
+    got = host(da)
+    assert np.array_equal(host(db), b)          # inbuf untouched
+    assert compare(got, exp, kind, size, opname, ext) == 0
+
+
+@pytest.mark.parametrize('case', gu.load_cases(), ids=lambda c: c['id'] + ' ' + c['name'])
+def test_golden_on_gpu(R, case):
+    sup = R.is_supported(case['op'], case['datatype'])
+    if not sup:
+        # only the x87 long double pairs have no GPU path; they must refuse
+        assert case['datatype'] == 0x8c000004
+        return
+
+    def fn(inb, inoutb, count, dt, op):
+        di, dio = dev(inb), dev(inoutb)
+        rc = R.MPI_Reduce_local(di, dio, count, dt, op)
+        inoutb[:] = host(dio)
+        return rc
+    rc, acc = gu.fold(case, fn)
+    assert rc == 0
+    assert gu.mismatches(case, acc) == 0
+
+
+@pytest.mark.parametrize('count', [0, 1, 2, 3, 4, 5, 15, 16, 17, 63, 64, 65, 1023, 4099,
+                                   (1 << 20) + 3])
+@pytest.mark.parametrize('offs', [(0, 0), (4, 4), (8, 8), (12, 12), (0, 4), (4, 0), (8, 12)])
+def test_ragged_and_misaligned(R, H, oracle, count, offs):
+    """head/tail element paths and the element-wise (relatively misaligned)
+    kernel, fp32 SUM, against the oracle."""
+    rng = np.random.default_rng(count * 131 + offs[0] * 7 + offs[1])
+    a = rng.uniform(-1, 1, count + 8).astype(np.float32)
+    b = rng.uniform(-1, 1, count + 8).astype(np.float32)
+    da, db = dev(a), dev(b)
+    oa, ob = offs
+    assert R.MPI_Reduce_local(db.data_ptr() + ob, da.data_ptr() + oa, count, H.MPI_FLOAT,
+                              H.MPI_SUM) == 0
+    exp = a.copy()
+    ev = exp.view(np.uint8)[oa:oa + 4 * count].view(np.float32)
+    bv = b.view(np.uint8)[ob:ob + 4 * count].view(np.float32).copy()
+    oracle.reduce_local(bv, ev, count, H.MPI_FLOAT, H.MPI_SUM)
+    assert np.array_equal(host(da).view(np.float32), exp)
+
+
+@pytest.mark.parametrize('dtname,ext', [('MPI_CHAR', 1), ('MPI_SHORT', 2), ('MPI_DOUBLE', 8),
+                                        ('MPI_C_DOUBLE_COMPLEX', 16)])
+def test_ragged_small_units(R, H, oracle, dtname, ext):
+    dt = getattr(H, dtname)
+    for count in (1, 7, 15, 33, 1000):
+        for off in (0, ext, 3 * ext):
+            rng = np.random.default_rng(count + off)
+            a = rng.integers(0, 256, (count + 8) * ext, dtype=np.uint8)
+            b = rng.integers(0, 256, (count + 8) * ext, dtype=np.uint8)
+            if dtname == 'MPI_DOUBLE' or 'COMPLEX' in dtname:
+                a = rng.uniform(-1, 1, len(a) // 8).view(np.uint8)
+                b = rng.uniform(-1, 1, len(b) // 8).view(np.uint8)
+            da, db = dev(a), dev(b)
+            assert R.MPI_Reduce_local(db.data_ptr() + off, da.data_ptr() + off, count, dt,
+                                      H.MPI_SUM) == 0
+            exp = a.copy()
+            oracle.reduce_local(b[off:off + count * ext].copy(), exp[off:], count, dt, H.MPI_SUM)
+            assert np.array_equal(host(da), exp)
+
+
+def test_host_buffers_are_staged(R, H, oracle):
+    """host (pageable numpy) operands go H2D -> kernel -> D2H in chunks."""
+    rng = np.random.default_rng(7)
+    n = (3 << 20) + 5
+    a = rng.uniform(-1, 1, n).astype(np.float32)
+    b = rng.uniform(-1, 1, n).astype(np.float32)
+    exp = a.copy()
+    oracle.reduce_local(b, exp, n, H.MPI_FLOAT, H.MPI_SUM)
+    got = a.copy()
+    assert R.MPI_Reduce_local(b, got, n, H.MPI_FLOAT, H.MPI_SUM) == 0
+    assert np.array_equal(got, exp)
+    # mixed: device in, host inout; and pinned host
+    got = a.copy()
+    assert R.MPI_Reduce_local(dev(b), got, n, H.MPI_FLOAT, H.MPI_SUM) == 0
+    assert np.array_equal(got, exp)
+    pa = torch.from_numpy(a.copy()).pin_memory()
+    pb = torch.from_numpy(b.copy()).pin_memory()
+    assert R.MPI_Reduce_local(pb, pa, n, H.MPI_FLOAT, H.MPI_SUM) == 0
+    assert np.array_equal(pa.numpy(), exp)
+
+
+def test_async_on_torch_stream(R, H, oracle):
+    rng = np.random.default_rng(11)
+    n = 1 << 22
+    a = rng.uniform(-1, 1, n).astype(np.float32)
+    b = rng.uniform(-1, 1, n).astype(np.float32)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        da = torch.from_numpy(a).cuda(non_blocking=False)
+        db = torch.from_numpy(b).cuda(non_blocking=False)
+        for _ in range(3):
+            assert R.reduce_local_async(db, da, n, H.MPI_FLOAT, H.MPI_SUM) == 0
+    s.synchronize()
+    exp = a.copy()
+    for _ in range(3):
+        oracle.reduce_local(b, exp, n, H.MPI_FLOAT, H.MPI_SUM)
+    assert np.array_equal(da.cpu().numpy(), exp)
+
+
+def test_op_table_functions(R, H, oracle):
+    """MPIR_op_function ABI (mpir_op.h:206): len and type by pointer."""
+    L = R.lib()
+    tab = (ctypes.c_void_p * 16).in_dll(L, 'MPIX_Op_table')
+    fnt = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p,
+                           ctypes.POINTER(ctypes.c_ssize_t), ctypes.POINTER(ctypes.c_int))
+    rng = np.random.default_rng(3)
+    n = 100003
+    for opi in (1, 2, 3, 4, 6, 8, 10):
+        a = rng.integers(-1000, 1000, n).astype(np.int32)
+        b = rng.integers(-1000, 1000, n).astype(np.int32)
+        da, db = dev(a), dev(b)
+        ln = ctypes.c_ssize_t(n)
+        ty = ctypes.c_int(H.as_c_int(0x4c810405))       # MPIR_INT32 | MPI_INT's index
+        fnt(tab[opi])(db.data_ptr(), da.data_ptr(), ctypes.byref(ln), ctypes.byref(ty))
+        assert L.MPIX_Redop_last_error() == 0
+        exp = a.copy()
+        oracle.reduce_local(b, exp, n, 0x4c810405, 0x58000000 | opi)
+        assert np.array_equal(host(da).view(np.int32), exp), opi
+
+
+def test_errors_on_gpu(R, H):
+    x = torch.zeros(1024, device='cuda')
+    y = torch.zeros(1024, device='cuda')
+    assert R.MPI_Reduce_local(x, x, 1024, H.MPI_FLOAT, H.MPI_SUM) == H.MPI_ERR_BUFFER
+    assert R.MPI_Reduce_local(-1, y, 1024, H.MPI_FLOAT, H.MPI_SUM) == H.MPI_ERR_BUFFER
+    assert R.MPI_Reduce_local(x, y, 1024, H.MPI_LONG_DOUBLE, H.MPI_SUM) == H.MPI_ERR_TYPE
+    assert R.MPI_Reduce_local(x, y, 1024, H.MPIX_BFLOAT16, H.MPI_MAX) == H.MPI_ERR_TYPE
+    assert R.MPI_Reduce_local(x, y, 10, H.MPI_FLOAT, H.MPI_LXOR) == H.MPI_ERR_OP
+    assert R.MPI_Reduce_local(x, y, 0, H.MPI_FLOAT, H.MPI_SUM) == H.MPI_SUCCESS
+
+
+def test_fortran_booleans(R, H, oracle):
+    """MPII_TO/FROM_FLOG with a non-default .TRUE. (e.g. -1)."""
+    rng = np.random.default_rng(5)
+    n = 4097
+    a = rng.integers(-2, 3, n).astype(np.int32)
+    b = rng.integers(-2, 3, n).astype(np.int32)
+    try:
+        R.set_fortran_booleans(-1, 0)
+        oracle.set_fortran_booleans(-1, 0)
+        for op in (H.MPI_LAND, H.MPI_LOR, H.MPI_LXOR):
+            da, db = dev(a), dev(b)
+            assert R.MPI_Reduce_local(db, da, n, H.MPI_LOGICAL, op) == 0
+            exp = a.copy()
+            oracle.reduce_local(b, exp, n, H.MPI_LOGICAL, op)
+            assert np.array_equal(host(da).view(np.int32), exp)
+    finally:
+        R.set_fortran_booleans(1, 0)
+        oracle.set_fortran_booleans(1, 0)
+
+
+@pytest.mark.parametrize('blocklen,stride', [(1, 2), (1, 3), (3, 7), (4, 4), (5, 8)])
+def test_vector_target(R, H, oracle, blocklen, stride):
+    """config 5 semantics (typerep_op.c:115-150): vector target, packed source;
+    gap elements must be untouched."""
+    rng = np.random.default_rng(blocklen * 10 + stride)
+    count = 100003
+    src = rng.uniform(-1, 1, count * blocklen)
+    dst = rng.uniform(-1, 1, count * stride)
+    dd, ds = dev(dst), dev(src)
+    assert R.reduce_local_vector(ds, dd, count, blocklen, stride, H.MPI_DOUBLE, H.MPI_SUM,
+                                 sync=True) == 0
+    exp = dst.copy()
+    oracle.reduce_local_vector(src, exp, count, blocklen, stride, H.MPI_DOUBLE, H.MPI_SUM)
+    assert np.array_equal(host(dd).view(np.float64), exp)
+
+
+def test_full_1gib_fp32_sum(R, H, oracle):
+    """BASELINE config 2 at its largest size: 1 GiB per operand, checked
+    element-for-element against the oracle (8 host threads)."""
+    n = 1 << 28
+    rng = np.random.default_rng(0x5EED0001)
+    a = rng.uniform(-1, 1, n).astype(np.float32)
+    b = rng.uniform(-1, 1, n).astype(np.float32)
+    da = torch.from_numpy(a).cuda()
+    db = torch.from_numpy(b).cuda()
+    torch.cuda.synchronize()
+    assert R.MPI_Reduce_local(db, da, n, H.MPI_FLOAT, H.MPI_SUM) == 0
+    oracle.reduce_local(b, a, n, H.MPI_FLOAT, H.MPI_SUM, nthreads=8)
+    got = da.cpu().numpy()
+    assert np.array_equal(got, a)
+    del da, db
+    torch.cuda.empty_cache()
+
+
+def test_full_vector_stride2_fp64(R, H, oracle):
+    """BASELINE config 5 at full size: vector(67108864, 1, 2, MPI_DOUBLE)."""
+    count = 67108864
+    rng = np.random.default_rng(0x5EED0005)
+    src = rng.uniform(-1, 1, count)
+    dst = rng.uniform(-1, 1, 2 * count)
+    dd, ds = torch.from_numpy(dst).cuda(), torch.from_numpy(src).cuda()
+    torch.cuda.synchronize()
+    assert R.reduce_local_vector(ds, dd, count, 1, 2, H.MPI_DOUBLE, H.MPI_SUM, sync=True) == 0
+    oracle.reduce_local_vector(src, dst, count, 1, 2, H.MPI_DOUBLE, H.MPI_SUM)
+    assert np.array_equal(dd.cpu().numpy(), dst)
+    del dd, ds
+    torch.cuda.empty_cache()
