@@ -47,7 +47,7 @@ def parse():
     p.add_argument('--steps', type=int, default=50)
     p.add_argument('--warmup', type=int, default=5)
     p.add_argument('--count', type=int, default=1 << 28, help='fp32 elements per operand')
-    p.add_argument('--cpu-seconds', type=float, default=12.0,
+    p.add_argument('--cpu-seconds', type=float, default=20.0,
                    help='bounded CPU-baseline sample duration per leg')
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--no-extras', action='store_true',
@@ -68,18 +68,23 @@ def bench_lib():
     return L
 
 
-def event_time_per_launch(launch, reps, stream):
-    """average duration of `launch()` measured with HIP events on `stream`"""
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(reps)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(reps)]
-    for i in range(reps):
-        starts[i].record(stream)
-        launch()
-        ends[i].record(stream)
-    stream.synchronize()
-    ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
-    ms.sort()
-    return sum(ms) / len(ms), ms[len(ms) // 2], ms[0]
+def event_time_per_launch(launch, reps, stream, rounds=3):
+    """average duration of one `launch()` measured with HIP events on
+    `stream`: one event pair brackets `reps` back-to-back launches (so the
+    event-record overhead is amortised and the figure is comparable with the
+    per-dispatch durations rocprofv3 reports); `rounds` such batches."""
+    per = []
+    for _ in range(rounds):
+        s0 = torch.cuda.Event(enable_timing=True)
+        s1 = torch.cuda.Event(enable_timing=True)
+        s0.record(stream)
+        for _ in range(reps):
+            launch()
+        s1.record(stream)
+        stream.synchronize()
+        per.append(s0.elapsed_time(s1) / reps)
+    per.sort()
+    return sum(per) / len(per), per[len(per) // 2], per[0]
 
 
 def fill_uniform(t, seed):
@@ -88,30 +93,37 @@ def fill_uniform(t, seed):
     t.uniform_(-1.0, 1.0, generator=g)
 
 
-def cpu_baseline(seconds):
-    """oracle (CPU restatement) on BASELINE config 1: 16 MiB fp32 SUM."""
+def cpu_baseline(seconds, count):
+    """The oracle (clean-room C restatement of MPICH's op_fns.c loop) on a
+    bounded sample of the SAME workload: MPI_Reduce_local(MPI_SUM, MPI_FLOAT)
+    on `count`-element (1 GiB) host operands, repeated for ~seconds/2 on one
+    core (MPICH's path is one thread per rank) and ~seconds/2 on all cores
+    of this process's share.  BASELINE config 1 (16 MiB, cache-resident on
+    this host) is reported beside it."""
     import numpy as np
     from oracle import oracle as orc
     orc.build()
-    n = 4194304
-    rng = np.random.default_rng(0x5EED0001)
-    a = rng.uniform(-1, 1, n).astype(np.float32)
-    b = rng.uniform(-1, 1, n).astype(np.float32)
-    out = {}
     ncores = len(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') else os.cpu_count()
     threads_all = max(1, min(16, ncores))
-    for label, nth in (('1core', 1), ('allcores', threads_all)):
-        reps, t_list = 0, []
-        t_end = time.perf_counter() + seconds / 2
-        while time.perf_counter() < t_end or reps < 3:
+
+    def leg(n, nth, budget):
+        rng = np.random.default_rng(0x5EED0001)
+        a = rng.uniform(-1, 1, n).astype(np.float32)
+        b = rng.uniform(-1, 1, n).astype(np.float32)
+        t_list = []
+        t_end = time.perf_counter() + budget
+        while time.perf_counter() < t_end or len(t_list) < 3:
             t0 = orc.wtime()
             orc.reduce_local(b, a, n, H.MPI_FLOAT, H.MPI_SUM, nthreads=nth)
             t_list.append(orc.wtime() - t0)
-            reps += 1
         t_list.sort()
         med = t_list[len(t_list) // 2]
-        out[label] = dict(gibs_median=3 * n * 4 / GIB / med, gibs_best=3 * n * 4 / GIB / t_list[0],
-                          reps=reps, threads=nth)
+        return dict(gibs=round(3 * n * 4 / GIB / med, 3), best=round(3 * n * 4 / GIB / t_list[0], 3),
+                    reps=len(t_list), threads=nth)
+
+    one = leg(count, 1, seconds * 0.45)
+    allc = leg(count, threads_all, seconds * 0.35)
+    c1 = leg(4194304, 1, seconds * 0.2)
     model = ''
     try:
         for line in open('/proc/cpuinfo'):
@@ -121,14 +133,17 @@ def cpu_baseline(seconds):
     except OSError:
         pass
     return dict(
-        value=round(out['1core']['gibs_median'], 3), unit='GiB/s', cores=1, kind='port',
-        sample='BASELINE config 1: MPI_Reduce_local(MPI_SUM, MPI_FLOAT) 16 MiB (4,194,304 '
-               'elements), oracle/redop_oracle.c scalar loop, %d reps in %.0f s, median'
-               % (out['1core']['reps'], seconds / 2),
-        best=round(out['1core']['gibs_best'], 3),
-        allcores=dict(value=round(out['allcores']['gibs_median'], 3), threads=threads_all,
-                      reps=out['allcores']['reps']),
-        host_cpu=model, nproc=os.cpu_count())
+        value=one['gibs'], unit='GiB/s', cores=1, kind='port',
+        sample='same workload (MPI_Reduce_local MPI_SUM MPI_FLOAT, %d elements = %d MiB per '
+               'operand, host-resident) through oracle/redop_oracle.c, 1 thread, %d calls, median'
+               % (count, count * 4 >> 20, one['reps']),
+        best=one['best'],
+        allcores=dict(value=allc['gibs'], threads=threads_all, reps=allc['reps'],
+                      note='disjoint slices, one thread per core of this process share'),
+        config1_16MiB_1core=dict(value=c1['gibs'], reps=c1['reps'],
+                                 note='BASELINE config 1; 48 MiB per call is cache-resident on '
+                                      'this host'),
+        host_cpu=model, nproc=os.cpu_count(), affinity_cpus=ncores)
 
 
 def load_pmc(path, count):
@@ -216,8 +231,8 @@ def main():
             'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
             'frac': round(achieved / HBM_PEAK_GBS, 4),
             'traffic': load_pmc(args.pmc, n),
-            'kernel_ms_avg': round(k_avg, 4), 'kernel_ms_median': round(k_med, 4),
-            'kernel_ms_min': round(k_min, 4), 'kernel_launches_timed': kreps,
+            'kernel_ms_avg': round(k_avg, 4), 'kernel_ms_median_batch': round(k_med, 4),
+            'kernel_ms_min_batch': round(k_min, 4), 'kernel_launches_timed': 3 * kreps,
             'algorithmic_bytes_per_launch': nbytes_alg,
         },
     }
@@ -289,7 +304,7 @@ def main():
         result['reduce_scatter_block'] = rsb_bench(args, world, rank, dev)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result['cpu_baseline'] = cpu_baseline(args.cpu_seconds)
+        result['cpu_baseline'] = cpu_baseline(args.cpu_seconds, args.count)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -179,6 +179,7 @@ const Entry *gpu_entry(uint32_t opi, uint32_t it)
 // ---------------------------------------------------------------- state
 std::atomic<long long> g_ftrue{1}, g_ffalse{0};
 std::atomic<int> g_block{256}, g_max_grid{0};
+std::atomic<bool> g_spin{true};     // MPIX_REDOP_SYNC=block selects hipStreamSynchronize
 std::once_flag g_env_once;
 size_t g_stage_chunk = (size_t) 64 << 20;
 
@@ -191,6 +192,8 @@ void read_env()
     }
     if (const char *s = getenv("MPIX_REDOP_MAXGRID"))
         g_max_grid = atoi(s) > 0 ? atoi(s) : 0;
+    if (const char *s = getenv("MPIX_REDOP_SYNC"))
+        g_spin = strcmp(s, "block") != 0;
     if (const char *s = getenv("MPIX_REDOP_STAGE_CHUNK")) {
         long long c = atoll(s);
         if (c >= 4096)
@@ -204,6 +207,7 @@ constexpr int kMaxDev = 64;
 struct DevState {
     bool init = false;
     hipStream_t s[2] = {nullptr, nullptr};
+    hipEvent_t done = nullptr;          // completion marker for the spin wait
     void *scratch = nullptr;    // 2 slots x (in chunk + inout chunk)
     size_t scratch_bytes = 0;
 };
@@ -235,6 +239,8 @@ DevState *dev_state(int dev)
         for (int k = 0; k < 2; ++k)
             if (hipStreamCreateWithFlags(&d.s[k], hipStreamNonBlocking) != hipSuccess)
                 return nullptr;
+        if (hipEventCreateWithFlags(&d.done, hipEventDisableTiming) != hipSuccess)
+            return nullptr;
         d.init = true;
     }
     return &d;
@@ -247,6 +253,21 @@ LaunchCfg launch_cfg()
 }
 
 Params params() { return Params{g_ftrue.load(), g_ffalse.load()}; }
+
+// Completion wait of the synchronous entry points.  MPI progress engines
+// poll; a blocking hipStreamSynchronize costs ~tens of microseconds of
+// wake-up latency per call, so by default completion is polled on an event.
+int wait_stream(DevState *d, hipStream_t s)
+{
+    if (!g_spin.load())
+        return hip_err(hipStreamSynchronize(s));
+    hipError_t e = hipEventRecord(d->done, s);
+    if (e != hipSuccess)
+        return hip_err(e);
+    while ((e = hipEventQuery(d->done)) == hipErrorNotReady) {
+    }
+    return hip_err(e);
+}
 
 enum class Where { Device, Host };
 
@@ -362,8 +383,8 @@ int staged(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext, 
         if (rc == MPIX_REDOP_SUCCESS && io_host)
             rc = hip_err(hipMemcpyAsync(dst_io, kio, n * ext, hipMemcpyDeviceToHost, s));
     }
-    int rc2 = hip_err(hipStreamSynchronize(d->s[0]));
-    int rc3 = hip_err(hipStreamSynchronize(d->s[1]));
+    int rc2 = wait_stream(d, d->s[0]);
+    int rc3 = wait_stream(d, d->s[1]);
     return rc ? rc : (rc2 ? rc2 : rc3);
 }
 
@@ -408,6 +429,8 @@ int MPIX_Redop_finalize(void)
         for (int k = 0; k < 2; ++k)
             if (d.s[k])
                 (void) hipStreamDestroy(d.s[k]);
+        if (d.done)
+            (void) hipEventDestroy(d.done);
         if (d.scratch)
             (void) hipFree(d.scratch);
         d = DevState();
@@ -453,7 +476,7 @@ int MPIX_Reduce_local(const void *inbuf, void *inoutbuf, MPIX_Aint count, MPIX_D
     if (!d)
         return set_err(MPIX_REDOP_ERR_OTHER);
     rc = enqueue(inbuf, inoutbuf, (uint64_t) count, it, ext, (uint32_t) op, d->s[0]);
-    int rc2 = hip_err(hipStreamSynchronize(d->s[0]));
+    int rc2 = wait_stream(d, d->s[0]);
     return set_err(rc ? rc : rc2);
 }
 
@@ -510,7 +533,7 @@ int MPIX_Reduce_local_vector(const void *inbuf, void *inoutbuf, MPIX_Aint count,
         return set_err(MPIX_REDOP_ERR_OTHER);
     int rc = MPIX_Reduce_local_vector_async(inbuf, inoutbuf, count, blocklen, stride, basic_type,
                                             op, d->s[0]);
-    int rc2 = hip_err(hipStreamSynchronize(d->s[0]));
+    int rc2 = wait_stream(d, d->s[0]);
     return set_err(rc ? rc : rc2);
 }
 

@@ -330,8 +330,8 @@ def test_op_table_functions(R, H, oracle):
 
 
 def test_errors_on_gpu(R, H):
-    x = torch.zeros(1024, device='cuda')
-    y = torch.zeros(1024, device='cuda')
+    x = torch.zeros(1 << 16, device='cuda')
+    y = torch.zeros(1 << 16, device='cuda')
     assert R.MPI_Reduce_local(x, x, 1024, H.MPI_FLOAT, H.MPI_SUM) == H.MPI_ERR_BUFFER
     assert R.MPI_Reduce_local(-1, y, 1024, H.MPI_FLOAT, H.MPI_SUM) == H.MPI_ERR_BUFFER
     assert R.MPI_Reduce_local(x, y, 1024, H.MPI_LONG_DOUBLE, H.MPI_SUM) == H.MPI_ERR_TYPE
