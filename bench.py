@@ -301,7 +301,10 @@ def main():
     torch.cuda.empty_cache()
 
     if world > 1 or args.rsb:
-        result['reduce_scatter_block'] = rsb_bench(args, world, rank, dev)
+        try:
+            result['reduce_scatter_block'] = rsb_bench(args, world, rank, dev)
+        except Exception as e:      # secondary figure: never lose the headline line
+            result['reduce_scatter_block'] = dict(error='%s: %s' % (type(e).__name__, e))
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result['cpu_baseline'] = cpu_baseline(args.cpu_seconds, args.count)
@@ -318,6 +321,17 @@ def rsb_bench(args, world, rank, dev):
     from mpich_amd import coll
     if world == 1 or not dist.is_initialized():
         return dict(note='P=1 is a local copy (coll_api.txt:402-411); see value for the combine')
+    # parity first: redscatblk3.c:43-56 closed form (MPI_INT SUM), on device
+    rc_small = 4096 + 3
+    blk = torch.cat([torch.full((rc_small,), rank + i, dtype=torch.int32, device=dev)
+                     for i in range(world)])
+    out = torch.empty(rc_small, dtype=torch.int32, device=dev)
+    coll.reduce_scatter_block(blk, out, rc_small, H.MPI_INT, H.MPI_SUM, extent=4)
+    torch.cuda.synchronize()
+    parity = bool(torch.all(out == world * rank + world * (world - 1) // 2).item())
+    ok = torch.tensor([1 if parity else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    parity = bool(ok.item())
     total = args.rsb_bytes // 4
     recvcount = total // world
     total = recvcount * world
@@ -351,7 +365,8 @@ def rsb_bench(args, world, rank, dev):
     link_bytes = (pof2 - 1) / pof2 * total * 4
     del send, recv, ws
     torch.cuda.empty_cache()
-    return dict(P=world, bytes_per_rank=total * 4, recvcount=recvcount, ms=round(t * 1e3, 3),
+    return dict(P=world, parity_redscatblk3_all_ranks=parity,
+                bytes_per_rank=total * 4, recvcount=recvcount, ms=round(t * 1e3, 3),
                 busbw_GBs=round(busbytes / t / 1e9, 2),
                 link_GBs=round(link_bytes / t / 1e9, 2),
                 frac_of_xgmi_link=round(link_bytes / t / 1e9 / 153.0, 4),

@@ -1,0 +1,91 @@
+"""Multi-process CPU coverage of the N>1 path: the recursive-halving
+MPI_Reduce_scatter_block schedule of mpich_amd/coll.py run over the gloo
+backend with world sizes 2..8 (power-of-two and not), the oracle injected
+as the combine.  Checks (a) bit-identity with the oracle's single-process
+simulation of the reference schedule
+(reduce_scatter_block_intra_recursive_halving.c:38-260) and (b) the
+reference's own closed form (test/mpi/coll/redscatblk3.c:48-78)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, outdir, recvcount, mode):
+    import torch
+    import torch.distributed as dist
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from oracle import oracle as orc
+    from mpich_amd import coll
+    MPI_FLOAT, MPI_INT, MPI_SUM = 0x4c00040a, 0x4c000405, 0x58000003
+    if mode == 'float':
+        rng = np.random.default_rng(0x5EED0100 + rank)
+        send = rng.uniform(-1, 1, world * recvcount).astype(np.float32)
+        dt = MPI_FLOAT
+    else:   # redscatblk3.c:43-48: block i of rank r holds r + i
+        send = np.concatenate([np.full(recvcount, rank + i, np.int32) for i in range(world)])
+        dt = MPI_INT
+    sendt = torch.from_numpy(send.copy())
+    recv = torch.zeros(recvcount, dtype=sendt.dtype)
+
+    def combine(inb, inoutb, count):
+        a = inoutb.numpy()
+        b = inb.numpy()
+        assert orc.reduce_local(b, a, count, dt, MPI_SUM) == 0
+
+    coll.reduce_scatter_block(sendt, recv, recvcount, dt, MPI_SUM, combine=combine, extent=4)
+    np.save(os.path.join(outdir, 'send%d.npy' % rank), send)
+    np.save(os.path.join(outdir, 'recv%d.npy' % rank), recv.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _run(world, recvcount, mode, tmp_path):
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), recvcount, mode), nprocs=world,
+             join=True)
+    sends = [np.load(tmp_path / ('send%d.npy' % r)) for r in range(world)]
+    recvs = [np.load(tmp_path / ('recv%d.npy' % r)) for r in range(world)]
+    return sends, recvs
+
+
+@pytest.mark.parametrize('world', [2, 3, 4, 5, 8])
+def test_rsb_gloo_matches_oracle_schedule(oracle, tmp_path, world):
+    recvcount = 1001
+    sends, recvs = _run(world, recvcount, 'float', tmp_path)
+    exp = oracle.rsb_recursive_halving([s.view(np.uint8) for s in sends], recvcount, 0x4c00040a,
+                                       0x58000003)
+    for r in range(world):
+        assert recvs[r].tobytes() == exp[r].tobytes(), r
+
+
+@pytest.mark.parametrize('world', [2, 3, 4])
+def test_rsb_gloo_redscatblk3(tmp_path, world):
+    recvcount = (1024 * 1024) // world // 64
+    _, recvs = _run(world, recvcount, 'int', tmp_path)
+    for r in range(world):
+        assert np.all(recvs[r] == world * r + world * (world - 1) // 2)
+
+
+def test_plan_matches_reference_counts():
+    """step table of the schedule for P=8: halves 4,2,1 blocks."""
+    from mpich_amd import coll
+    rc = 10
+    for r in range(8):
+        p = coll.plan(r, 8, rc)
+        assert [s[2] for s in p['steps']] == [40, 20, 10]
+        assert [s[4] for s in p['steps']] == [40, 20, 10]
+        assert [s[0] for s in p['steps']] == [r ^ 4, r ^ 2, r ^ 1]
+    p = coll.plan(0, 6, rc)          # non-pof2: even rank < 2*rem sits out
+    assert p['newrank'] == -1 and p['steps'] == []
