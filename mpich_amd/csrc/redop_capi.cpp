@@ -180,6 +180,7 @@ const Entry *gpu_entry(uint32_t opi, uint32_t it)
 std::atomic<long long> g_ftrue{1}, g_ffalse{0};
 std::atomic<int> g_block{256}, g_max_grid{0};
 std::atomic<bool> g_spin{true};     // MPIX_REDOP_SYNC=block selects hipStreamSynchronize
+std::atomic<bool> g_zero_copy{true}; // MPIX_REDOP_PINNED=stage stages pinned host memory too
 std::once_flag g_env_once;
 size_t g_stage_chunk = (size_t) 64 << 20;
 
@@ -194,6 +195,8 @@ void read_env()
         g_max_grid = atoi(s) > 0 ? atoi(s) : 0;
     if (const char *s = getenv("MPIX_REDOP_SYNC"))
         g_spin = strcmp(s, "block") != 0;
+    if (const char *s = getenv("MPIX_REDOP_PINNED"))
+        g_zero_copy = strcmp(s, "stage") != 0;
     if (const char *s = getenv("MPIX_REDOP_STAGE_CHUNK")) {
         long long c = atoll(s);
         if (c >= 4096)
@@ -269,21 +272,31 @@ int wait_stream(DevState *d, hipStream_t s)
     return hip_err(e);
 }
 
-enum class Where { Device, Host };
+enum class Where { Device, Pinned, Pageable };
 
-Where classify(const void *p, int *dev)
+// Device / managed memory is used in place.  Pinned (page-locked, mapped)
+// host memory is read and written by the kernel directly over PCIe
+// ("zero-copy": one pass, both link directions busy at once) unless
+// MPIX_REDOP_PINNED=stage; pageable host memory has to be staged.
+Where classify(const void *p, int *dev, const void **devptr)
 {
     hipPointerAttribute_t a;
     hipError_t e = hipPointerGetAttributes(&a, p);
+    *devptr = p;
     if (e != hipSuccess) {
         (void) hipGetLastError();
-        return Where::Host;
+        return Where::Pageable;
     }
     if (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged) {
         *dev = a.device;
         return Where::Device;
     }
-    return Where::Host;
+    if (a.type == hipMemoryTypeHost && a.devicePointer) {
+        // devicePointer maps the start of the allocation containing p
+        *devptr = (const char *) a.devicePointer + ((const char *) p - (const char *) a.hostPointer);
+        return Where::Pinned;
+    }
+    return Where::Pageable;
 }
 
 bool overlaps(const void *a, const void *b, uint64_t bytes)
@@ -463,19 +476,24 @@ int MPIX_Reduce_local(const void *inbuf, void *inoutbuf, MPIX_Aint count, MPIX_D
     uint32_t opi = (uint32_t) op & 0xf;
     if (opi != 13 && opi != 14 && !gpu_entry(opi, it))
         return set_err(MPIX_REDOP_ERR_TYPE);
+    launch_cfg();
     int din = -1, dio = -1, cur = 0;
     (void) hipGetDevice(&cur);
-    bool in_host = classify(inbuf, &din) == Where::Host;
-    bool io_host = classify(inoutbuf, &dio) == Where::Host;
-    int dev = !io_host ? dio : (!in_host ? din : cur);
+    const void *pin, *pio;
+    Where win = classify(inbuf, &din, &pin);
+    Where wio = classify(inoutbuf, &dio, &pio);
+    bool zc = g_zero_copy.load();
+    bool in_stage = win == Where::Pageable || (win == Where::Pinned && !zc);
+    bool io_stage = wio == Where::Pageable || (wio == Where::Pinned && !zc);
+    int dev = wio == Where::Device ? dio : (win == Where::Device ? din : cur);
     DeviceGuard guard(dev);
-    if (in_host || io_host)
-        return set_err(staged(inbuf, inoutbuf, (uint64_t) count, it, ext, (uint32_t) op, in_host,
-                              io_host, dev));
+    if (in_stage || io_stage)
+        return set_err(staged(in_stage ? inbuf : pin, io_stage ? inoutbuf : (void *) pio,
+                              (uint64_t) count, it, ext, (uint32_t) op, in_stage, io_stage, dev));
     DevState *d = dev_state(dev);
     if (!d)
         return set_err(MPIX_REDOP_ERR_OTHER);
-    rc = enqueue(inbuf, inoutbuf, (uint64_t) count, it, ext, (uint32_t) op, d->s[0]);
+    rc = enqueue(pin, (void *) pio, (uint64_t) count, it, ext, (uint32_t) op, d->s[0]);
     int rc2 = wait_stream(d, d->s[0]);
     return set_err(rc ? rc : rc2);
 }
@@ -525,7 +543,8 @@ int MPIX_Reduce_local_vector(const void *inbuf, void *inoutbuf, MPIX_Aint count,
                              MPIX_Op op)
 {
     int dev = 0;
-    if (classify(inoutbuf, &dev) != Where::Device)
+    const void *dp;
+    if (classify(inoutbuf, &dev, &dp) != Where::Device)
         return set_err(MPIX_REDOP_ERR_BUFFER);
     DeviceGuard guard(dev);
     DevState *d = dev_state(dev);
