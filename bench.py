@@ -316,22 +316,13 @@ def main():
 
 
 def rsb_bench(args, world, rank, dev):
-    """BASELINE config 4: MPI_Reduce_scatter_block fp32 SUM, recursive halving,
-    fixed vector per rank (strong scaling), RCCL/xGMI chunk transport."""
+    """BASELINE config 4: MPI_Reduce_scatter_block fp32 SUM, fixed vector per
+    rank (strong scaling), RCCL/xGMI chunk transport; the reference's
+    recursive-halving schedule and the pairwise one (all links at once)."""
     from mpich_amd import coll
     if world == 1 or not dist.is_initialized():
         return dict(note='P=1 is a local copy (coll_api.txt:402-411); see value for the combine')
-    # parity first: redscatblk3.c:43-56 closed form (MPI_INT SUM), on device
-    rc_small = 4096 + 3
-    blk = torch.cat([torch.full((rc_small,), rank + i, dtype=torch.int32, device=dev)
-                     for i in range(world)])
-    out = torch.empty(rc_small, dtype=torch.int32, device=dev)
-    coll.reduce_scatter_block(blk, out, rc_small, H.MPI_INT, H.MPI_SUM, extent=4)
-    torch.cuda.synchronize()
-    parity = bool(torch.all(out == world * rank + world * (world - 1) // 2).item())
-    ok = torch.tensor([1 if parity else 0], dtype=torch.int32, device=dev)
-    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-    parity = bool(ok.item())
+    out = {}
     total = args.rsb_bytes // 4
     recvcount = total // world
     total = recvcount * world
@@ -340,37 +331,55 @@ def rsb_bench(args, world, rank, dev):
     recv = torch.empty(recvcount, dtype=torch.float32, device=dev)
     ws = (torch.empty(total * 4, dtype=torch.uint8, device=dev),
           torch.empty(total * 4, dtype=torch.uint8, device=dev))
-
-    def once():
-        coll.reduce_scatter_block(send, recv, recvcount, H.MPI_FLOAT, H.MPI_SUM, workspace=ws,
-                                  extent=4)
-    once()
-    reps = max(3, min(10, args.steps))
-    dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        once()
-    torch.cuda.synchronize()
-    dist.barrier()
-    t = (time.perf_counter() - t0) / reps
-    tt = torch.tensor([t], dtype=torch.float64, device=dev)
-    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-    t = float(tt.item())
-    busbytes = (world - 1) / world * total * 4
     pof2 = 1
     while pof2 * 2 <= world:
         pof2 *= 2
-    # bytes each rank receives over its single active link in the pof2 steps
-    link_bytes = (pof2 - 1) / pof2 * total * 4
+    for algo in ('recursive_halving', 'pairwise'):
+        fn = coll.ALGORITHMS[algo]
+        kw = dict(workspace=ws if algo == 'recursive_halving' else ws[0], extent=4)
+        # parity first: redscatblk3.c:43-56 closed form (MPI_INT SUM), on device
+        rc_small = 4096 + 3
+        blk = torch.cat([torch.full((rc_small,), rank + i, dtype=torch.int32, device=dev)
+                         for i in range(world)])
+        o = torch.empty(rc_small, dtype=torch.int32, device=dev)
+        fn(blk, o, rc_small, H.MPI_INT, H.MPI_SUM, extent=4)
+        torch.cuda.synchronize()
+        ok = torch.tensor([1 if bool(torch.all(o == world * rank + world * (world - 1) // 2))
+                           else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+
+        def once():
+            fn(send, recv, recvcount, H.MPI_FLOAT, H.MPI_SUM, **kw)
+        once()
+        reps = max(3, min(10, args.steps))
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            once()
+        torch.cuda.synchronize()
+        dist.barrier()
+        t = (time.perf_counter() - t0) / reps
+        tt = torch.tensor([t], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t = float(tt.item())
+        busbytes = (world - 1) / world * total * 4
+        if algo == 'recursive_halving':
+            # bytes a rank receives over its one active link across the steps
+            link_bytes = (pof2 - 1) / pof2 * total * 4
+            links = 1
+        else:
+            link_bytes = total * 4 / world          # one block per peer link, concurrently
+            links = world - 1
+        out[algo] = dict(parity_redscatblk3_all_ranks=bool(ok.item()), ms=round(t * 1e3, 3),
+                         busbw_GBs=round(busbytes / t / 1e9, 2),
+                         per_link_GBs=round(link_bytes / t / 1e9, 2), links_active=links,
+                         frac_of_xgmi_link=round(link_bytes / t / 1e9 / 153.0, 4))
     del send, recv, ws
     torch.cuda.empty_cache()
-    return dict(P=world, parity_redscatblk3_all_ranks=parity,
-                bytes_per_rank=total * 4, recvcount=recvcount, ms=round(t * 1e3, 3),
-                busbw_GBs=round(busbytes / t / 1e9, 2),
-                link_GBs=round(link_bytes / t / 1e9, 2),
-                frac_of_xgmi_link=round(link_bytes / t / 1e9 / 153.0, 4),
-                algorithm='recursive halving (reduce_scatter_block_intra_recursive_halving.c)')
+    out.update(P=world, bytes_per_rank=total * 4, recvcount=recvcount,
+               xgmi_link_GBs_assumed=153.0)
+    return out
 
 
 if __name__ == '__main__':

@@ -182,6 +182,16 @@ int MPIX_Reduce_local_vector(const void *inbuf, void *inoutbuf, MPIX_Aint count,
                              MPIX_Aint blocklen, MPIX_Aint stride,
                              MPIX_Datatype basic_type, MPIX_Op op);
 
+/* Multi-input form: equivalent to `ninputs` MPIX_Reduce_local calls
+ *   for k = 0 .. ninputs-1:  inoutbuf = inoutbuf OP inbufs[k]
+ * in that order (same association, same bits) but done in one pass over
+ * memory.  Used by reduce-scatter schedules whose received blocks arrive
+ * together (pairwise, reduce_scatter_block_intra_pairwise.c:86-100).
+ * 1 <= ninputs <= 16; device-accessible buffers; stream-ordered. */
+int MPIX_Reduce_local_multi_async(const void *const *inbufs, int ninputs, void *inoutbuf,
+                                  MPIX_Aint count, MPIX_Datatype datatype, MPIX_Op op,
+                                  void *stream);
+
 /* 1 if (op, datatype) runs on the GPU path, else 0.  `count` is accepted
  * for signature parity and ignored (the reference passes 0 here too,
  * reduce_local.c:66-68).  When 0, a caller keeps its own CPU op table. */

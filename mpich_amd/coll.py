@@ -1,4 +1,4 @@
-"""Recursive-halving MPI_Reduce_scatter_block over torch.distributed.
+"""MPI_Reduce_scatter_block schedules over torch.distributed.
 
 Restates MPIR_Reduce_scatter_block_intra_recursive_halving
 (src/mpi/coll/reduce_scatter_block/reduce_scatter_block_intra_recursive_halving.c:38-260)
@@ -15,10 +15,20 @@ for one process per GPU:
     MPIR_Reduce_local(tmp_recvbuf, tmp_results) -- so the fp association, and
     therefore every bit, matches the CPU schedule.
 
-The combine can be injected (`combine=`) so the schedule itself can be
+`reduce_scatter_block_pairwise` restates
+MPIR_Reduce_scatter_block_intra_pairwise (…_intra_pairwise.c:42-104),
+MPICH's large-message choice (maint/tuning/coll/mpir/generic.json:324-328),
+MI355X-first: the P-1 exchanges are posted as ONE group, so every xGMI link
+of the node carries one block at the same time (the reference runs them as
+P-1 sequential sendrecvs), and the P-1 received blocks are folded into the
+result by one multi-input kernel pass in the reference's order i = 1..P-1
+(same association as its P-1 MPIR_Reduce_local calls, so the same bits).
+
+The combine can be injected (`combine=`) so the schedules themselves can be
 exercised on CPU with the gloo backend; the default is the HIP path and
 there is no CPU fallback.
 """
+import os
 import torch
 import torch.distributed as dist
 
@@ -151,3 +161,77 @@ def reduce_scatter_block(sendbuf, recvbuf, recvcount, datatype, op, group=None, 
         else:
             _exchange(None, None, rb, g2l(rank + 1), group)
     return recvbuf
+
+
+def reduce_scatter_block_pairwise(sendbuf, recvbuf, recvcount, datatype, op, group=None,
+                                  combine=None, extent=None, workspace=None, concurrent=True):
+    """MPI_Reduce_scatter_block, pairwise exchange (reference algorithm
+    `pairwise`).  workspace: optional byte tensor of >= (P-1)*recvcount
+    elements for the received blocks."""
+    rank = dist.get_rank(group)
+    size = dist.get_world_size(group)
+    if extent is None:
+        from . import redop
+        extent = redop.datatype_extent(datatype)
+    g2l = (lambda r: dist.get_global_rank(group, r)) if group is not None else (lambda r: r)
+    sb = sendbuf.reshape(-1).view(torch.uint8)
+    rb = recvbuf.reshape(-1).view(torch.uint8)
+    blk = recvcount * extent
+
+    def block(i):
+        return slice(i * blk, (i + 1) * blk)
+
+    rb[:blk].copy_(sb[block(rank)])                                 # :60-64
+    if size == 1:
+        return recvbuf
+    nslot = size - 1 if concurrent else 1
+    if workspace is not None:
+        slots = workspace[:nslot * blk]
+    else:
+        slots = torch.empty(nslot * blk, dtype=torch.uint8, device=sb.device)
+    peers = [((rank + i) % size, (rank - i + size) % size) for i in range(1, size)]
+    if not concurrent:                                              # the reference's loop
+        for dst, src in peers:
+            _exchange(sb[block(dst)], g2l(dst), slots[:blk], g2l(src), group)
+            if combine is not None:
+                combine(slots[:blk], rb[:blk], recvcount)
+            else:
+                _default_combine(datatype, op)(slots[:blk], rb[:blk], recvcount)
+        return recvbuf
+    ops = []
+    for i, (dst, src) in enumerate(peers):
+        ops.append(dist.P2POp(dist.isend, sb[block(dst)], g2l(dst), group=group, tag=TAG))
+        ops.append(dist.P2POp(dist.irecv, slots[i * blk:(i + 1) * blk], g2l(src), group=group,
+                              tag=TAG))
+    for w in dist.batch_isend_irecv(ops):
+        w.wait()
+    ins = [slots[i * blk:(i + 1) * blk] for i in range(size - 1)]
+    if combine is not None:
+        for x in ins:                                               # :86-100, i = 1..P-1
+            combine(x, rb[:blk], recvcount)
+    else:
+        from . import redop
+        for lo in range(0, len(ins), 16):
+            redop.check(redop.reduce_local_multi_async(ins[lo:lo + 16], rb[:blk], recvcount,
+                                                       datatype, op),
+                        'MPIX_Reduce_local_multi_async')
+    return recvbuf
+
+
+ALGORITHMS = {'recursive_halving': reduce_scatter_block, 'pairwise': reduce_scatter_block_pairwise}
+
+
+def reduce_scatter_block_auto(sendbuf, recvbuf, recvcount, datatype, op, group=None, **kw):
+    """Algorithm selection mirroring MPIR_CVAR_REDUCE_SCATTER_BLOCK_INTRA_ALGORITHM
+    (cvars.txt:1712-1726): env value `recursive_halving` or `pairwise`;
+    `auto` follows generic.json:316-341 (recursive halving below 512 KiB per
+    rank, pairwise above)."""
+    algo = os.environ.get('MPIR_CVAR_REDUCE_SCATTER_BLOCK_INTRA_ALGORITHM', 'auto')
+    if algo not in ALGORITHMS:
+        ext = kw.get('extent')
+        if ext is None:
+            from . import redop
+            ext = redop.datatype_extent(datatype)
+        total = recvcount * ext * dist.get_world_size(group)
+        algo = 'recursive_halving' if total < (512 << 10) else 'pairwise'
+    return ALGORITHMS[algo](sendbuf, recvbuf, recvcount, datatype, op, group=group, **kw)

@@ -556,6 +556,35 @@ int MPIX_Reduce_local_vector(const void *inbuf, void *inoutbuf, MPIX_Aint count,
     return set_err(rc ? rc : rc2);
 }
 
+int MPIX_Reduce_local_multi_async(const void *const *inbufs, int ninputs, void *inoutbuf,
+                                  MPIX_Aint count, MPIX_Datatype datatype, MPIX_Op op,
+                                  void *stream)
+{
+    if (ninputs < 1 || ninputs > mpix::kMaxMultiInputs || !inbufs)
+        return set_err(MPIX_REDOP_ERR_ARG);
+    uint32_t it;
+    uint64_t ext;
+    for (int q = 0; q < ninputs; ++q) {
+        int rc = validate(inbufs[q], inoutbuf, count, (uint32_t) datatype, (uint32_t) op, &it,
+                          &ext);
+        if (rc != MPIX_REDOP_SUCCESS)
+            return set_err(rc);
+    }
+    if (count == 0)
+        return set_err(MPIX_REDOP_SUCCESS);
+    uint32_t opi = (uint32_t) op & 0xf;
+    if (opi == 14)
+        return set_err(MPIX_REDOP_SUCCESS);
+    if (opi == 13)      // REPLACE k times = copy of the last input
+        return set_err(hip_err(hipMemcpyAsync(inoutbuf, inbufs[ninputs - 1], (size_t) count * ext,
+                                              hipMemcpyDeviceToDevice, (hipStream_t) stream)));
+    const Entry *e = gpu_entry(opi, it);
+    if (!e)
+        return set_err(MPIX_REDOP_ERR_TYPE);
+    return set_err(hip_err(e->multi(inbufs, ninputs, inoutbuf, (uint64_t) count, params(),
+                                    launch_cfg(), (hipStream_t) stream)));
+}
+
 int MPIX_Redop_is_supported(MPIX_Op op, MPIX_Aint count, MPIX_Datatype datatype)
 {
     (void) count;

@@ -26,7 +26,11 @@ struct Entry {
                          const LaunchCfg &, hipStream_t);
     hipError_t (*vector)(const void *in, void *io, uint64_t count, uint64_t blocklen,
                          uint64_t stride, const Params &, const LaunchCfg &, hipStream_t);
+    hipError_t (*multi)(const void *const *ins, int k, void *io, uint64_t count, const Params &,
+                        const LaunchCfg &, hipStream_t);
 };
+
+constexpr int kMaxMultiInputs = 16;
 
 // Each instantiation unit resolves (raw internal type, op index) to an Entry
 // or returns nullptr.  raw = handle & 0xffffff00 for builtins; struct pair

@@ -102,6 +102,78 @@ k_contig(const typename C::unit *__restrict__ in, typename C::unit *__restrict__
     }
 }
 
+// Multi-input combine: inout = OP(...OP(OP(inout, in[0]), in[1])..., in[k-1]),
+// i.e. k back-to-back MPIR_Reduce_local calls in that order -- the same
+// association, so the same bits -- in ONE pass over HBM: (k+2) x bytes
+// instead of 3k x bytes.  Used by the pairwise reduce-scatter, whose k
+// received blocks arrive together.
+constexpr int kMaxMulti = 16;
+template <typename T> struct MultiIn {
+    const T *p[kMaxMulti];
+};
+
+template <class C, int U>
+__global__ void __launch_bounds__(1024)
+k_contig_multi(MultiIn<typename C::unit> ins, int k, typename C::unit *__restrict__ io,
+               uint64_t head, uint64_t npk, uint64_t tail_start, uint32_t ntail, Params prm)
+{
+    v4u *__restrict__ vio = reinterpret_cast<v4u *>(io + head);
+    const uint64_t nt = blockDim.x;
+    const uint64_t tile = nt * U;
+    const uint64_t stride = (uint64_t) gridDim.x * tile;
+    for (uint64_t i = (uint64_t) blockIdx.x * tile + threadIdx.x; i < npk; i += stride) {
+        v4u acc[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (i + u * nt < npk)
+                acc[u] = ld16<true>(vio + i + u * nt);
+        for (int q = 0; q < k; ++q) {
+            const v4u *__restrict__ vin = reinterpret_cast<const v4u *>(ins.p[q] + head);
+            v4u b[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (i + u * nt < npk)
+                    b[u] = ld16<true>(vin + i + u * nt);
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (i + u * nt < npk)
+                    acc[u] = combine16<C>(acc[u], b[u], prm);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (i + u * nt < npk)
+                st16<true>(vio + i + u * nt, acc[u]);
+    }
+    if (blockIdx.x == 0) {
+        for (uint64_t t = threadIdx.x; t < head; t += nt) {
+            typename C::unit a = io[t];
+            for (int q = 0; q < k; ++q)
+                a = C::apply(a, ins.p[q][t], prm);
+            io[t] = a;
+        }
+        for (uint64_t t = threadIdx.x; t < ntail; t += nt) {
+            typename C::unit a = io[tail_start + t];
+            for (int q = 0; q < k; ++q)
+                a = C::apply(a, ins.p[q][tail_start + t], prm);
+            io[tail_start + t] = a;
+        }
+    }
+}
+
+template <class C>
+__global__ void __launch_bounds__(1024)
+k_elem_multi(MultiIn<typename C::unit> ins, int k, typename C::unit *__restrict__ io, uint64_t n,
+             Params prm)
+{
+    const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        typename C::unit a = io[i];
+        for (int q = 0; q < k; ++q)
+            a = C::apply(a, ins.p[q][i], prm);
+        io[i] = a;
+    }
+}
+
 template <class C>
 __global__ void __launch_bounds__(1024)
 k_elem(const typename C::unit *__restrict__ in, typename C::unit *__restrict__ io, uint64_t n,
@@ -212,6 +284,39 @@ hipError_t launch_contig(const void *in, void *io, uint64_t count, const Params 
 }
 
 template <class C>
+hipError_t launch_multi(const void *const *ins, int k, void *io, uint64_t count, const Params &prm,
+                        const LaunchCfg &cfg, hipStream_t s)
+{
+    using T = typename C::unit;
+    constexpr uint64_t E = 16 / sizeof(T);
+    MultiIn<T> mi{};
+    uintptr_t ao = reinterpret_cast<uintptr_t>(io);
+    bool aligned = (ao % sizeof(T)) == 0;
+    for (int q = 0; q < k; ++q) {
+        mi.p[q] = static_cast<const T *>(ins[q]);
+        aligned = aligned && ((reinterpret_cast<uintptr_t>(ins[q]) & 15) == (ao & 15));
+    }
+    T *tio = static_cast<T *>(io);
+    if (aligned) {
+        uint64_t head = ((16 - (ao & 15)) & 15) / sizeof(T);
+        if (head > count)
+            head = count;
+        uint64_t npk = (count - head) / E;
+        uint64_t tail_start = head + npk * E;
+        uint32_t ntail = (uint32_t) (count - tail_start);
+        constexpr int U = 2;
+        unsigned grid = grid_for((uint64_t) cfg.block * U, npk, cfg.max_grid);
+        hipLaunchKernelGGL((k_contig_multi<C, U>), dim3(grid), dim3(cfg.block), 0, s, mi, k, tio,
+                           head, npk, tail_start, ntail, prm);
+    } else {
+        unsigned grid = grid_for((uint64_t) cfg.block * 4, count, cfg.max_grid);
+        hipLaunchKernelGGL((k_elem_multi<C>), dim3(grid), dim3(cfg.block), 0, s, mi, k, tio, count,
+                           prm);
+    }
+    return hipGetLastError();
+}
+
+template <class C>
 hipError_t launch_vector(const void *in, void *io, uint64_t count, uint64_t bl, uint64_t st,
                          const Params &prm, const LaunchCfg &cfg, hipStream_t s)
 {
@@ -234,6 +339,9 @@ hipError_t launch_vector(const void *in, void *io, uint64_t count, uint64_t bl, 
     return hipGetLastError();
 }
 
-template <class C> constexpr Entry entry() { return Entry{&launch_contig<C>, &launch_vector<C>}; }
+template <class C> constexpr Entry entry()
+{
+    return Entry{&launch_contig<C>, &launch_vector<C>, &launch_multi<C>};
+}
 
 }  // namespace mpix

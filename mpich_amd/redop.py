@@ -46,6 +46,8 @@ def lib():
             'MPIX_Reduce_local_async': ([vp, vp, aint, i32, i32, vp], i32),
             'MPIX_Reduce_local_vector': ([vp, vp, aint, aint, aint, i32, i32], i32),
             'MPIX_Reduce_local_vector_async': ([vp, vp, aint, aint, aint, i32, i32, vp], i32),
+            'MPIX_Reduce_local_multi_async': ([ctypes.POINTER(vp), i32, vp, aint, i32, i32, vp],
+                                              i32),
             'MPIX_Redop_is_supported': ([i32, aint, i32], i32),
             'MPIX_Redop_op_dt_check': ([i32, i32], i32),
             'MPIX_Redop_internal_op_dt_check': ([i32, i32], i32),
@@ -111,6 +113,14 @@ def reduce_local_vector(inbuf, inoutbuf, count, blocklen, stride, basic_type, op
     return lib().MPIX_Reduce_local_vector_async(_addr(inbuf), _addr(inoutbuf), count, blocklen,
                                                 stride, H.as_c_int(basic_type), H.as_c_int(op),
                                                 _stream_ptr(stream))
+
+
+def reduce_local_multi_async(inbufs, inoutbuf, count, datatype, op, stream=None):
+    """inoutbuf = (...((inoutbuf OP in[0]) OP in[1])...) OP in[k-1], one pass."""
+    arr = (ctypes.c_void_p * len(inbufs))(*[_addr(b) for b in inbufs])
+    return lib().MPIX_Reduce_local_multi_async(arr, len(inbufs), _addr(inoutbuf), count,
+                                               H.as_c_int(datatype), H.as_c_int(op),
+                                               _stream_ptr(stream))
 
 
 def check(rc, what='MPI_Reduce_local'):

@@ -44,6 +44,7 @@ def lib():
         L.oracle_set_fortran_booleans.restype = None
         L.oracle_rsb_recursive_halving.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(vp), il,
                                                    i32, i32, i32]
+        L.oracle_rsb_pairwise.argtypes = L.oracle_rsb_recursive_halving.argtypes
         L.oracle_wtime.restype = ctypes.c_double
         _lib = L
     return _lib
@@ -91,18 +92,24 @@ def set_fortran_booleans(t, f):
     lib().oracle_set_fortran_booleans(t, f)
 
 
-def rsb_recursive_halving(sendbufs, recvcount, datatype, op):
-    """Simulate MPI_Reduce_scatter_block (recursive halving) over P ranks in
-    one process; returns the list of per-rank result arrays."""
+def rsb_recursive_halving(sendbufs, recvcount, datatype, op, algorithm='recursive_halving'):
+    """Simulate MPI_Reduce_scatter_block (recursive halving or pairwise) over
+    P ranks in one process; returns the list of per-rank result arrays."""
     P = len(sendbufs)
     ext = extent(datatype)
     recvs = [np.zeros(recvcount * ext, np.uint8) for _ in range(P)]
     sp = (ctypes.c_void_p * P)(*[s.ctypes.data for s in sendbufs])
     rp = (ctypes.c_void_p * P)(*[r.ctypes.data for r in recvs])
-    rc = lib().oracle_rsb_recursive_halving(sp, rp, recvcount, _i32(datatype), _i32(op), P)
+    fn = lib().oracle_rsb_pairwise if algorithm == 'pairwise' else \
+        lib().oracle_rsb_recursive_halving
+    rc = fn(sp, rp, recvcount, _i32(datatype), _i32(op), P)
     if rc:
         raise RuntimeError('oracle rsb failed: %d' % rc)
     return recvs
+
+
+def rsb_pairwise(sendbufs, recvcount, datatype, op):
+    return rsb_recursive_halving(sendbufs, recvcount, datatype, op, algorithm='pairwise')
 
 
 def wtime():

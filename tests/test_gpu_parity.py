@@ -407,3 +407,40 @@ def test_full_vector_stride2_fp64(R, H, oracle):
     assert np.array_equal(dd.cpu().numpy(), dst)
     del dd, ds
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize('k', [1, 2, 7, 16])
+@pytest.mark.parametrize('dtname,opname', [('MPI_FLOAT', 'MPI_SUM'), ('MPI_DOUBLE', 'MPI_PROD'),
+                                           ('MPI_INT', 'MPI_MAX'), ('MPI_2INT', 'MPI_MINLOC'),
+                                           ('MPIX_C_FLOAT16', 'MPI_SUM'),
+                                           ('MPI_C_FLOAT_COMPLEX', 'MPI_PROD')])
+def test_multi_input_combine(R, H, oracle, k, dtname, opname):
+    """MPIX_Reduce_local_multi_async == k sequential MPI_Reduce_local calls
+    (same association, so bit-exact), incl. ragged/unaligned element paths."""
+    dt, op = getattr(H, dtname), getattr(H, opname)
+    ext = R.datatype_extent(dt)
+    for n, off in ((100003, 0), (4097, ext)):
+        rng = np.random.default_rng(k * 1000 + n)
+        if dtname in ('MPI_INT', 'MPI_2INT'):
+            mk = lambda: rng.integers(-50, 50, n * ext // 4 + 4).astype(np.int32).view(np.uint8)  # noqa
+        elif dtname == 'MPIX_C_FLOAT16':
+            mk = lambda: rng.uniform(-1, 1, n + 8).astype(np.float16).view(np.uint8)  # noqa
+        else:
+            mk = lambda: rng.uniform(-1, 1, n * ext // 4 + 4).astype(np.float32).view(np.uint8) \
+                if ext % 4 == 0 and dtname != 'MPI_DOUBLE' else \
+                rng.uniform(-1, 1, n * ext // 8 + 2).astype(np.float64).view(np.uint8)  # noqa
+        acc = mk()
+        ins = [mk() for _ in range(k)]
+        exp = acc.copy()
+        for x in ins:
+            oracle.reduce_local(x[off:off + n * ext].copy(), exp[off:], n, dt, op)
+        dacc = dev(acc)
+        dins = [dev(x) for x in ins]
+        rc = R.reduce_local_multi_async([d.data_ptr() + off for d in dins], dacc.data_ptr() + off,
+                                        n, dt, op)
+        assert rc == 0
+        got = host(dacc)
+        assert compare(got[off:off + n * ext], exp[off:off + n * ext],
+                       'fp' if 'FLOAT' in dtname or 'DOUBLE' in dtname else 'int',
+                       {'MPI_FLOAT': 4, 'MPI_DOUBLE': 8, 'MPIX_C_FLOAT16': 2}.get(dtname, 4),
+                       opname, ext) == 0

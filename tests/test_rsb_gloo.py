@@ -21,7 +21,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, outdir, recvcount, mode):
+def _worker(rank, world, port, outdir, recvcount, mode, algo='recursive_halving'):
     import torch
     import torch.distributed as dist
     os.environ['MASTER_ADDR'] = '127.0.0.1'
@@ -45,16 +45,20 @@ def _worker(rank, world, port, outdir, recvcount, mode):
         b = inb.numpy()
         assert orc.reduce_local(b, a, count, dt, MPI_SUM) == 0
 
-    coll.reduce_scatter_block(sendt, recv, recvcount, dt, MPI_SUM, combine=combine, extent=4)
+    if algo == 'recursive_halving':
+        coll.reduce_scatter_block(sendt, recv, recvcount, dt, MPI_SUM, combine=combine, extent=4)
+    else:
+        coll.reduce_scatter_block_pairwise(sendt, recv, recvcount, dt, MPI_SUM, combine=combine,
+                                           extent=4, concurrent=(algo == 'pairwise'))
     np.save(os.path.join(outdir, 'send%d.npy' % rank), send)
     np.save(os.path.join(outdir, 'recv%d.npy' % rank), recv.numpy())
     dist.barrier()
     dist.destroy_process_group()
 
 
-def _run(world, recvcount, mode, tmp_path):
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), recvcount, mode), nprocs=world,
-             join=True)
+def _run(world, recvcount, mode, tmp_path, algo='recursive_halving'):
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), recvcount, mode, algo),
+             nprocs=world, join=True)
     sends = [np.load(tmp_path / ('send%d.npy' % r)) for r in range(world)]
     recvs = [np.load(tmp_path / ('recv%d.npy' % r)) for r in range(world)]
     return sends, recvs
@@ -74,6 +78,22 @@ def test_rsb_gloo_matches_oracle_schedule(oracle, tmp_path, world):
 def test_rsb_gloo_redscatblk3(tmp_path, world):
     recvcount = (1024 * 1024) // world // 64
     _, recvs = _run(world, recvcount, 'int', tmp_path)
+    for r in range(world):
+        assert np.all(recvs[r] == world * r + world * (world - 1) // 2)
+
+
+@pytest.mark.parametrize('algo', ['pairwise', 'pairwise_sequential'])
+@pytest.mark.parametrize('world', [2, 3, 4, 7])
+def test_pairwise_gloo_matches_oracle(oracle, tmp_path, world, algo):
+    """concurrent (one group, all links) and the reference's sequential
+    exchange give the reference pairwise association bit-for-bit."""
+    recvcount = 777
+    sends, recvs = _run(world, recvcount, 'float', tmp_path, algo)
+    exp = oracle.rsb_pairwise([s.view(np.uint8) for s in sends], recvcount, 0x4c00040a,
+                              0x58000003)
+    for r in range(world):
+        assert recvs[r].tobytes() == exp[r].tobytes(), r
+    sends, recvs = _run(world, 1000, 'int', tmp_path, algo)
     for r in range(world):
         assert np.all(recvs[r] == world * r + world * (world - 1) // 2)
 

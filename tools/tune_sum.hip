@@ -73,13 +73,24 @@ int main(int argc, char **argv)
     hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, a, n, 1u);
     hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, b, n, 2u);
     CK(hipDeviceSynchronize());
+    bool focus = argc > 4 && std::string(argv[4]) == "focus";
     std::vector<Var> v;
-    for (int block : {256, 512, 1024}) {
-        for (int mg : {0, 2048, 4096}) {
-            add_all<1>(v, block, mg);
-            add_all<2>(v, block, mg);
-            add_all<4>(v, block, mg);
-            add_all<8>(v, block, mg);
+    if (focus) {        // NT/NT, one tile per block: the winners of the full sweep
+        for (int block : {256, 512, 1024}) {
+            add<1, true, true>(v, block, 0);
+            add<2, true, true>(v, block, 0);
+            add<4, true, true>(v, block, 0);
+            add<8, true, true>(v, block, 0);
+            add<16, true, true>(v, block, 0);
+        }
+    } else {
+        for (int block : {256, 512, 1024}) {
+            for (int mg : {0, 2048, 4096}) {
+                add_all<1>(v, block, mg);
+                add_all<2>(v, block, mg);
+                add_all<4>(v, block, mg);
+                add_all<8>(v, block, mg);
+            }
         }
     }
     hipStream_t s;
@@ -111,5 +122,9 @@ int main(int argc, char **argv)
     std::sort(res.begin(), res.end());
     for (auto &r : res)
         printf("%8.1f GB/s  %s\n", r.first, r.second.c_str());
+    for (auto &x : v) {     // spread per variant (min / median / max of all launches)
+        printf("# %-40s min %.4f med %.4f max %.4f ms (n=%zu)\n", x.name.c_str(), x.ms.front(),
+               x.ms[x.ms.size() / 2], x.ms.back(), x.ms.size());
+    }
     return 0;
 }
