@@ -440,7 +440,8 @@ def test_multi_input_combine(R, H, oracle, k, dtname, opname):
                                         n, dt, op)
         assert rc == 0
         got = host(dacc)
-        assert compare(got[off:off + n * ext], exp[off:off + n * ext],
-                       'fp' if 'FLOAT' in dtname or 'DOUBLE' in dtname else 'int',
+        kind = 'cplx' if 'COMPLEX' in dtname else \
+            ('fp' if 'FLOAT' in dtname or 'DOUBLE' in dtname else 'int')
+        assert compare(got[off:off + n * ext], exp[off:off + n * ext], kind,
                        {'MPI_FLOAT': 4, 'MPI_DOUBLE': 8, 'MPIX_C_FLOAT16': 2}.get(dtname, 4),
                        opname, ext) == 0
