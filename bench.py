@@ -305,6 +305,10 @@ def main():
             result['reduce_scatter_block'] = rsb_bench(args, world, rank, dev)
         except Exception as e:      # secondary figure: never lose the headline line
             result['reduce_scatter_block'] = dict(error='%s: %s' % (type(e).__name__, e))
+        try:
+            result['allreduce'] = allreduce_bench(args, world, rank, dev)
+        except Exception as e:
+            result['allreduce'] = dict(error='%s: %s' % (type(e).__name__, e))
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result['cpu_baseline'] = cpu_baseline(args.cpu_seconds, args.count)
@@ -380,6 +384,53 @@ def rsb_bench(args, world, rank, dev):
     out.update(P=world, bytes_per_rank=total * 4, recvcount=recvcount,
                xgmi_link_GBs_assumed=153.0)
     return out
+
+
+def allreduce_bench(args, world, rank, dev):
+    """MPI_Allreduce fp32 SUM, 1 GiB per rank: the reference's
+    reduce-scatter + allgather schedule on RCCL point-to-point + the HIP
+    combine (bit-identical to the reference association), next to RCCL's own
+    all_reduce (torch.distributed, ncclAllReduce -- the reference's
+    MPIR_Allreduce_intra_ccl route, rccl.c:223) as the comparator."""
+    from mpich_amd import coll
+    if world == 1 or not dist.is_initialized():
+        return dict(note='P=1 is a local copy')
+    # parity: allred.c sum_test_1 closed form (in = i, sol = i*P), on device
+    m = 100003
+    x = torch.arange(m, dtype=torch.int32, device=dev)
+    y = torch.empty_like(x)
+    coll.allreduce(x, y, m, H.MPI_INT, H.MPI_SUM, extent=4)
+    torch.cuda.synchronize()
+    ok = torch.tensor([1 if bool(torch.all(y == x * world)) else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    n = (1 << 30) // 4
+    send = torch.empty(n, dtype=torch.float32, device=dev)
+    fill_uniform(send, 0x5EED0200 + rank)
+    recv = torch.empty_like(send)
+    ws = torch.empty(n * 4, dtype=torch.uint8, device=dev)
+    res = dict(parity_allred_sum_test_1_all_ranks=bool(ok.item()), bytes_per_rank=n * 4, P=world)
+    for name, fn in (('mpich_schedule_hip_combine',
+                      lambda: coll.allreduce(send, recv, n, H.MPI_FLOAT, H.MPI_SUM, extent=4,
+                                             workspace=ws)),
+                     ('rccl_all_reduce', lambda: (recv.copy_(send), dist.all_reduce(recv)))):
+        fn()
+        reps = max(3, min(10, args.steps))
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        dist.barrier()
+        t = (time.perf_counter() - t0) / reps
+        tt = torch.tensor([t], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t = float(tt.item())
+        res[name] = dict(ms=round(t * 1e3, 3),
+                         busbw_GBs=round(2 * (world - 1) / world * n * 4 / t / 1e9, 2))
+    del send, recv, ws
+    torch.cuda.empty_cache()
+    return res
 
 
 if __name__ == '__main__':

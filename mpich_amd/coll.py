@@ -235,3 +235,97 @@ def reduce_scatter_block_auto(sendbuf, recvbuf, recvcount, datatype, op, group=N
         total = recvcount * ext * dist.get_world_size(group)
         algo = 'recursive_halving' if total < (512 << 10) else 'pairwise'
     return ALGORITHMS[algo](sendbuf, recvbuf, recvcount, datatype, op, group=group, **kw)
+
+
+def allreduce(sendbuf, recvbuf, count, datatype, op, group=None, combine=None, extent=None,
+              workspace=None):
+    """MPI_Allreduce by reduce-scatter + allgather (Rabenseifner):
+    MPIR_Allreduce_intra_reduce_scatter_allgather
+    (src/mpi/coll/allreduce/allreduce_intra_reduce_scatter_allgather.c:41-277),
+    MPICH's choice for builtin ops with count >= pof2 (generic.json:99-135).
+    Device buffers; RCCL point-to-point transport; every partial is combined
+    by the HIP kernel in the reference's order, so results are bit-identical
+    to the reference schedule -- unlike ncclAllReduce (rccl.c:223), whose
+    association is RCCL's own and whose op set stops at SUM/PROD/MIN/MAX.
+    sendbuf=None means MPI_IN_PLACE (recvbuf holds the input)."""
+    rank = dist.get_rank(group)
+    size = dist.get_world_size(group)
+    if extent is None:
+        from . import redop
+        extent = redop.datatype_extent(datatype)
+    if combine is None:
+        combine = _default_combine(datatype, op)
+    g2l = (lambda r: dist.get_global_rank(group, r)) if group is not None else (lambda r: r)
+    rb = recvbuf.reshape(-1).view(torch.uint8)
+    if sendbuf is not None:
+        rb[:count * extent].copy_(sendbuf.reshape(-1).view(torch.uint8)[:count * extent])
+    if size == 1 or count == 0:
+        return recvbuf
+    pof2 = _pof2(size)
+    rem = size - pof2
+    if count < pof2:
+        raise ValueError('reduce_scatter_allgather allreduce needs count >= pof2 (:127); '
+                         'the reference uses recursive doubling below that')
+    tmp = workspace[:count * extent] if workspace is not None else \
+        torch.empty(count * extent, dtype=torch.uint8, device=rb.device)
+
+    def el(off, cnt):
+        return slice(off * extent, (off + cnt) * extent)
+
+    if rank < 2 * rem:                                              # :85-112
+        if rank % 2 == 0:
+            _exchange(rb[:count * extent], g2l(rank + 1), None, None, group)
+            newrank = -1
+        else:
+            _exchange(None, None, tmp, g2l(rank - 1), group)
+            combine(tmp, rb[:count * extent], count)
+            newrank = rank // 2
+    else:
+        newrank = rank - rem
+    if newrank != -1:
+        cnts = [count // pof2 + (1 if i < count % pof2 else 0) for i in range(pof2)]
+        disps = [0] * pof2
+        for i in range(1, pof2):
+            disps[i] = disps[i - 1] + cnts[i - 1]
+
+        def real(nr):
+            return nr * 2 + 1 if nr < rem else nr + rem
+        mask, send_idx, recv_idx, last_idx = 1, 0, 0, pof2
+        while mask < pof2:                                          # :138-189
+            newdst = newrank ^ mask
+            if newrank < newdst:
+                send_idx = recv_idx + pof2 // (mask * 2)
+                send_cnt, recv_cnt = sum(cnts[send_idx:last_idx]), sum(cnts[recv_idx:send_idx])
+            else:
+                recv_idx = send_idx + pof2 // (mask * 2)
+                send_cnt, recv_cnt = sum(cnts[send_idx:recv_idx]), sum(cnts[recv_idx:last_idx])
+            _exchange(rb[el(disps[send_idx], send_cnt)], g2l(real(newdst)),
+                      tmp[el(disps[recv_idx], recv_cnt)], g2l(real(newdst)), group)
+            combine(tmp[el(disps[recv_idx], recv_cnt)], rb[el(disps[recv_idx], recv_cnt)],
+                    recv_cnt)
+            send_idx = recv_idx
+            mask <<= 1
+            if mask < pof2:
+                last_idx = recv_idx + pof2 // mask
+        mask >>= 1
+        while mask > 0:                                             # :191-226
+            newdst = newrank ^ mask
+            if newrank < newdst:
+                if mask != pof2 // 2:
+                    last_idx = last_idx + pof2 // (mask * 2)
+                recv_idx = send_idx + pof2 // (mask * 2)
+                send_cnt, recv_cnt = sum(cnts[send_idx:recv_idx]), sum(cnts[recv_idx:last_idx])
+            else:
+                recv_idx = send_idx - pof2 // (mask * 2)
+                send_cnt, recv_cnt = sum(cnts[send_idx:last_idx]), sum(cnts[recv_idx:send_idx])
+            _exchange(rb[el(disps[send_idx], send_cnt)], g2l(real(newdst)),
+                      rb[el(disps[recv_idx], recv_cnt)], g2l(real(newdst)), group)
+            if newrank > newdst:
+                send_idx = recv_idx
+            mask >>= 1
+    if rank < 2 * rem:                                              # :229-238
+        if rank % 2:
+            _exchange(rb[:count * extent], g2l(rank - 1), None, None, group)
+        else:
+            _exchange(None, None, rb[:count * extent], g2l(rank + 1), group)
+    return recvbuf
