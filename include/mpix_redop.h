@@ -192,6 +192,18 @@ int MPIX_Reduce_local_multi_async(const void *const *inbufs, int ninputs, void *
                                   MPIX_Aint count, MPIX_Datatype datatype, MPIX_Op op,
                                   void *stream);
 
+/* ---- peer memory for the fused pull + combine ----
+ * The reference maps peer GPU buffers with hipIpc* in its shm/ipc path
+ * (src/mpl/src/gpu/mpl_gpu_hip.c:174-204).  Here a rank exports the
+ * allocation holding `devptr` (handle: MPIX_IPC_HANDLE_BYTES opaque bytes,
+ * plus the byte offset of devptr inside it); peers open it and pass the
+ * mapped addresses straight to MPIX_Reduce_local_multi_async, so the combine
+ * kernel reads the peers' blocks over xGMI with no intermediate copy. */
+#define MPIX_IPC_HANDLE_BYTES 64
+int MPIX_Ipc_export(const void *devptr, void *handle_out, MPIX_Aint *offset_out);
+int MPIX_Ipc_open(const void *handle, void **base_out);
+int MPIX_Ipc_close(void *base);
+
 /* 1 if (op, datatype) runs on the GPU path, else 0.  `count` is accepted
  * for signature parity and ignored (the reference passes 0 here too,
  * reduce_local.c:66-68).  When 0, a caller keeps its own CPU op table. */

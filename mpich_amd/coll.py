@@ -329,3 +329,67 @@ def allreduce(sendbuf, recvbuf, count, datatype, op, group=None, combine=None, e
         else:
             _exchange(None, None, rb[:count * extent], g2l(rank + 1), group)
     return recvbuf
+
+
+_ipc_cache = {}
+
+
+def ipc_cache_clear():
+    """Unmap every cached peer allocation (call before peers free buffers
+    that were used with reduce_scatter_block_pull)."""
+    from . import redop
+    for base in _ipc_cache.values():
+        redop.ipc_close(base)
+    _ipc_cache.clear()
+
+
+def _sync_barrier(group):
+    torch.cuda.synchronize()
+    dist.barrier(group=group)
+
+
+def reduce_scatter_block_pull(sendbuf, recvbuf, recvcount, datatype, op, group=None,
+                              extent=None):
+    """MPI_Reduce_scatter_block as ONE fused pull + combine kernel
+    (SURVEY.md §8(f)2): every rank maps its peers' send buffers
+    (hipIpc*, as MPICH's ipc/gpu shm path does, mpl_gpu_hip.c:174-204) and a
+    single multi-input kernel reads block `rank` of all P-1 peers directly
+    over xGMI -- all links at once, no receive buffer, no copy -- folding them
+    into the result in the pairwise order i = 1..P-1
+    (…_intra_pairwise.c:86-100), i.e. bit-identical to the reference pairwise
+    schedule.  Peer mappings are cached (ipc_cache_clear() drops them).
+    Costs two barriers per call: peers' inputs must be complete before the
+    pull and must stay untouched until every rank has pulled."""
+    from . import redop
+    rank = dist.get_rank(group)
+    size = dist.get_world_size(group)
+    if extent is None:
+        extent = redop.datatype_extent(datatype)
+    sb = sendbuf.reshape(-1).view(torch.uint8)
+    rb = recvbuf.reshape(-1).view(torch.uint8)
+    blk = recvcount * extent
+    rb[:blk].copy_(sb[rank * blk:(rank + 1) * blk])
+    if size == 1:
+        return recvbuf
+    handle, off = redop.ipc_export(sb)
+    infos = [None] * size
+    dist.all_gather_object(infos, (handle, off), group=group)
+    bases = []
+    for r, (h, o) in enumerate(infos):
+        if r == rank:
+            bases.append(sb.data_ptr())
+            continue
+        key = (r, h)
+        if key not in _ipc_cache:
+            _ipc_cache[key] = redop.ipc_open(h)
+        bases.append(_ipc_cache[key] + o)
+    _sync_barrier(group)                        # every peer's sendbuf is complete
+    ins = [bases[(rank - i + size) % size] + rank * blk for i in range(1, size)]
+    for lo in range(0, len(ins), 16):
+        redop.check(redop.reduce_local_multi_async(ins[lo:lo + 16], rb[:blk], recvcount,
+                                                   datatype, op), 'MPIX_Reduce_local_multi_async')
+    _sync_barrier(group)                        # nobody reuses sendbuf while peers read it
+    return recvbuf
+
+
+ALGORITHMS['pull'] = reduce_scatter_block_pull

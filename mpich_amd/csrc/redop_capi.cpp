@@ -585,6 +585,38 @@ int MPIX_Reduce_local_multi_async(const void *const *inbufs, int ninputs, void *
                                     launch_cfg(), (hipStream_t) stream)));
 }
 
+int MPIX_Ipc_export(const void *devptr, void *handle_out, MPIX_Aint *offset_out)
+{
+    if (!devptr || !handle_out || !offset_out)
+        return set_err(MPIX_REDOP_ERR_ARG);
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    hipError_t e = hipMemGetAddressRange(&base, &size, (hipDeviceptr_t) devptr);
+    if (e != hipSuccess)
+        return set_err(hip_err(e));
+    hipIpcMemHandle_t h;
+    e = hipIpcGetMemHandle(&h, (void *) base);
+    if (e != hipSuccess)
+        return set_err(hip_err(e));
+    memcpy(handle_out, &h, sizeof(h));
+    *offset_out = (MPIX_Aint) ((const char *) devptr - (const char *) base);
+    return set_err(MPIX_REDOP_SUCCESS);
+}
+
+int MPIX_Ipc_open(const void *handle, void **base_out)
+{
+    if (!handle || !base_out)
+        return set_err(MPIX_REDOP_ERR_ARG);
+    hipIpcMemHandle_t h;
+    memcpy(&h, handle, sizeof(h));
+    return set_err(hip_err(hipIpcOpenMemHandle(base_out, h, hipIpcMemLazyEnablePeerAccess)));
+}
+
+int MPIX_Ipc_close(void *base)
+{
+    return set_err(hip_err(hipIpcCloseMemHandle(base)));
+}
+
 int MPIX_Redop_is_supported(MPIX_Op op, MPIX_Aint count, MPIX_Datatype datatype)
 {
     (void) count;

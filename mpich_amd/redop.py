@@ -49,6 +49,9 @@ def lib():
             'MPIX_Reduce_local_multi_async': ([ctypes.POINTER(vp), i32, vp, aint, i32, i32, vp],
                                               i32),
             'MPIX_Redop_is_supported': ([i32, aint, i32], i32),
+            'MPIX_Ipc_export': ([vp, vp, ctypes.POINTER(aint)], i32),
+            'MPIX_Ipc_open': ([vp, ctypes.POINTER(vp)], i32),
+            'MPIX_Ipc_close': ([vp], i32),
             'MPIX_Redop_op_dt_check': ([i32, i32], i32),
             'MPIX_Redop_internal_op_dt_check': ([i32, i32], i32),
             'MPIX_Datatype_internal': ([i32], i32),
@@ -121,6 +124,28 @@ def reduce_local_multi_async(inbufs, inoutbuf, count, datatype, op, stream=None)
     return lib().MPIX_Reduce_local_multi_async(arr, len(inbufs), _addr(inoutbuf), count,
                                                H.as_c_int(datatype), H.as_c_int(op),
                                                _stream_ptr(stream))
+
+
+IPC_HANDLE_BYTES = 64
+
+
+def ipc_export(buf):
+    """(handle bytes, byte offset of buf inside its allocation)"""
+    h = ctypes.create_string_buffer(IPC_HANDLE_BYTES)
+    off = ctypes.c_ssize_t()
+    check(lib().MPIX_Ipc_export(_addr(buf), h, ctypes.byref(off)), 'MPIX_Ipc_export')
+    return h.raw, off.value
+
+
+def ipc_open(handle):
+    """map a peer allocation; returns its base address in this process"""
+    p = ctypes.c_void_p()
+    check(lib().MPIX_Ipc_open(handle, ctypes.byref(p)), 'MPIX_Ipc_open')
+    return p.value
+
+
+def ipc_close(base):
+    return lib().MPIX_Ipc_close(base)
 
 
 def check(rc, what='MPI_Reduce_local'):
