@@ -321,8 +321,9 @@ def main():
 
 def rsb_bench(args, world, rank, dev):
     """BASELINE config 4: MPI_Reduce_scatter_block fp32 SUM, fixed vector per
-    rank (strong scaling), RCCL/xGMI chunk transport; the reference's
-    recursive-halving schedule and the pairwise one (all links at once)."""
+    rank (strong scaling): the reference's recursive-halving schedule and
+    the pairwise one over RCCL/xGMI (all links at once), and the fused
+    pull + combine kernel over hipIpc-mapped peer buffers."""
     from mpich_amd import coll
     if world == 1 or not dist.is_initialized():
         return dict(note='P=1 is a local copy (coll_api.txt:402-411); see value for the combine')
@@ -338,9 +339,11 @@ def rsb_bench(args, world, rank, dev):
     pof2 = 1
     while pof2 * 2 <= world:
         pof2 *= 2
-    for algo in ('recursive_halving', 'pairwise'):
+    for algo in ('recursive_halving', 'pairwise', 'pull'):
         fn = coll.ALGORITHMS[algo]
-        kw = dict(workspace=ws if algo == 'recursive_halving' else ws[0], extent=4)
+        kw = dict(extent=4)
+        if algo != 'pull':
+            kw['workspace'] = ws if algo == 'recursive_halving' else ws[0]
         # parity first: redscatblk3.c:43-56 closed form (MPI_INT SUM), on device
         rc_small = 4096 + 3
         blk = torch.cat([torch.full((rc_small,), rank + i, dtype=torch.int32, device=dev)
@@ -372,8 +375,8 @@ def rsb_bench(args, world, rank, dev):
             # bytes a rank receives over its one active link across the steps
             link_bytes = (pof2 - 1) / pof2 * total * 4
             links = 1
-        else:
-            link_bytes = total * 4 / world          # one block per peer link, concurrently
+        else:                                       # pairwise / pull: all links at once
+            link_bytes = total * 4 / world          # one block per peer link
             links = world - 1
         out[algo] = dict(parity_redscatblk3_all_ranks=bool(ok.item()), ms=round(t * 1e3, 3),
                          busbw_GBs=round(busbytes / t / 1e9, 2),
