@@ -354,7 +354,11 @@ def rsb_bench(args, world, rank, dev):
     pof2 = 1
     while pof2 * 2 <= world:
         pof2 *= 2
+    p2p_ok = dist.get_backend() == 'nccl'     # the gloo rehearsal cannot move device tensors
     for algo in ('recursive_halving', 'pairwise', 'pull'):
+        if algo != 'pull' and not p2p_ok:
+            out[algo] = dict(skipped='needs the nccl (RCCL) backend')
+            continue
         try:
             fn = coll.ALGORITHMS[algo]
             kw = dict(extent=4)
@@ -414,6 +418,8 @@ def allreduce_bench(args, world, rank, dev):
     from mpich_amd import coll
     if world == 1 or not dist.is_initialized():
         return dict(note='P=1 is a local copy')
+    if dist.get_backend() != 'nccl':
+        return dict(skipped='needs the nccl (RCCL) backend')
     # parity: allred.c sum_test_1 closed form (in = i, sol = i*P), on device
     m = 100003
     x = torch.arange(m, dtype=torch.int32, device=dev)
