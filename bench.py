@@ -283,8 +283,8 @@ def main():
         te = (time.perf_counter() - t0) / reps
         result['end_to_end_host'] = dict(gibs=round(3 * hn * 4 / GIB / te, 2),
                                          ms_per_call=round(te * 1e3, 2),
-                                         note='pinned host buffers, chunked H2D/kernel/D2H '
-                                              'staging inside MPIX_Reduce_local; never `value`')
+                                         note='pinned host buffers: the kernel reads and writes '
+                                              'them over PCIe (zero-copy); never `value`')
         del hin, hio
 
     if args.sweep and rank == 0:

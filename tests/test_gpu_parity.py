@@ -445,3 +445,42 @@ def test_multi_input_combine(R, H, oracle, k, dtname, opname):
         assert compare(got[off:off + n * ext], exp[off:off + n * ext], kind,
                        {'MPI_FLOAT': 4, 'MPI_DOUBLE': 8, 'MPIX_C_FLOAT16': 2}.get(dtname, 4),
                        opname, ext) == 0
+
+
+def test_concurrent_callers(R, H, oracle):
+    """MPIR_Reduce_local is reentrant (called with the global CS held by
+    different threads under MPI_THREAD_MULTIPLE): per-thread streams, no
+    shared state on the data path."""
+    import threading
+    n = (1 << 20) + 11
+    rng = np.random.default_rng(99)
+    jobs = []
+    for t in range(8):
+        a = rng.uniform(-1, 1, n).astype(np.float32)
+        b = rng.uniform(-1, 1, n).astype(np.float32)
+        exp = a.copy()
+        for _ in range(5):
+            oracle.reduce_local(b, exp, n, H.MPI_FLOAT, H.MPI_SUM)
+        jobs.append((dev(a), dev(b), exp))
+    errs = []
+
+    def work(da, db):
+        torch.cuda.set_device(0)
+        for _ in range(5):
+            rc = R.MPI_Reduce_local(db, da, n, H.MPI_FLOAT, H.MPI_SUM)
+            if rc:
+                errs.append(rc)
+        R.finalize()        # per-thread streams released; later calls re-create them
+
+    th = [threading.Thread(target=work, args=(da, db)) for da, db, _ in jobs]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs
+    for da, _, exp in jobs:
+        assert np.array_equal(host(da).view(np.float32), exp)
+    # library still usable from this thread after other threads finalized theirs
+    x, y = dev(np.ones(1000, np.float32)), dev(np.ones(1000, np.float32))
+    assert R.MPI_Reduce_local(x, y, 1000, H.MPI_FLOAT, H.MPI_SUM) == 0
+    assert np.all(host(y).view(np.float32) == 2)
