@@ -182,6 +182,17 @@ int MPIX_Reduce_local_vector(const void *inbuf, void *inoutbuf, MPIX_Aint count,
                              MPIX_Aint blocklen, MPIX_Aint stride,
                              MPIX_Datatype basic_type, MPIX_Op op);
 
+/* General derived target given as its flattened iov, packed source --
+ * typerep_op_fallback (typerep_op.c:100-150) for a basic (non-pair) type:
+ * for s < nseg, in segment order, seg_counts[s] elements at byte offset
+ * seg_offsets[s] of inoutbuf are combined with the next seg_counts[s]
+ * elements of inbuf.  Offsets must be multiples of the type's extent and
+ * segments must not overlap (MPI accumulate targets).  The two tables are
+ * host arrays, read before the call returns.  Device buffers. */
+int MPIX_Reduce_local_iov_async(const void *inbuf, void *inoutbuf, MPIX_Aint nseg,
+                                const MPIX_Aint *seg_offsets, const MPIX_Aint *seg_counts,
+                                MPIX_Datatype basic_type, MPIX_Op op, void *stream);
+
 /* Multi-input form: equivalent to `ninputs` MPIX_Reduce_local calls
  *   for k = 0 .. ninputs-1:  inoutbuf = inoutbuf OP inbufs[k]
  * in that order (same association, same bits) but done in one pass over

@@ -12,7 +12,7 @@ const Entry *int_ops(int opi)
     // SUM/PROD/bitwise/logical are sign-agnostic bit patterns: share the
     // unsigned instantiation; only MAX/MIN depend on signedness.
     static const Entry tab[11] = {
-        Entry{nullptr, nullptr, nullptr},
+        Entry{nullptr, nullptr, nullptr, nullptr},
         entry<IMax<S>>(), entry<IMin<S>>(), entry<ISum<U>>(), entry<IProd<U>>(),
         entry<ILand<U>>(), entry<IBand<U>>(), entry<ILor<U>>(), entry<IBor<U>>(),
         entry<ILxor<U>>(), entry<IBxor<U>>(),

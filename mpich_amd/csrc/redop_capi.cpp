@@ -213,6 +213,8 @@ struct DevState {
     hipEvent_t done = nullptr;          // completion marker for the spin wait
     void *scratch = nullptr;    // 2 slots x (in chunk + inout chunk)
     size_t scratch_bytes = 0;
+    int64_t *iov_tab = nullptr; // device copy of an iov segment table (offsets + prefix)
+    size_t iov_cap = 0;         // entries per half
 };
 thread_local DevState *t_dev = nullptr;   // array of kMaxDev, never freed implicitly
 
@@ -446,6 +448,8 @@ int MPIX_Redop_finalize(void)
             (void) hipEventDestroy(d.done);
         if (d.scratch)
             (void) hipFree(d.scratch);
+        if (d.iov_tab)
+            (void) hipFree(d.iov_tab);
         d = DevState();
     }
     delete[] t_dev;
@@ -554,6 +558,93 @@ int MPIX_Reduce_local_vector(const void *inbuf, void *inoutbuf, MPIX_Aint count,
                                             op, d->s[0]);
     int rc2 = wait_stream(d, d->s[0]);
     return set_err(rc ? rc : rc2);
+}
+
+int MPIX_Reduce_local_iov_async(const void *inbuf, void *inoutbuf, MPIX_Aint nseg,
+                                const MPIX_Aint *seg_offsets, const MPIX_Aint *seg_counts,
+                                MPIX_Datatype basic_type, MPIX_Op op, void *stream)
+{
+    if (nseg < 0)
+        return set_err(MPIX_REDOP_ERR_COUNT);
+    uint32_t it;
+    uint64_t ext;
+    int rc = validate(inbuf, inoutbuf, 0, (uint32_t) basic_type, (uint32_t) op, &it, &ext);
+    if (rc != MPIX_REDOP_SUCCESS)
+        return set_err(rc);
+    if (nseg == 0)
+        return set_err(MPIX_REDOP_SUCCESS);
+    if (!seg_offsets || !seg_counts || !inbuf || !inoutbuf || inbuf == (const void *) -1 ||
+        inoutbuf == (void *) -1)
+        return set_err(MPIX_REDOP_ERR_BUFFER);
+    if (is_pairtype(it))
+        return set_err(MPIX_REDOP_ERR_TYPE);    // pair targets split across segments: not here
+    // host-side tables: element offsets + prefix counts (2*nseg + 1 entries)
+    int64_t *tab = (int64_t *) malloc(sizeof(int64_t) * (2 * (size_t) nseg + 1));
+    if (!tab)
+        return set_err(MPIX_REDOP_ERR_OTHER);
+    int64_t total = 0;
+    for (MPIX_Aint s = 0; s < nseg; ++s) {
+        if (seg_counts[s] < 0 || seg_offsets[s] % (MPIX_Aint) ext) {
+            free(tab);
+            return set_err(seg_counts[s] < 0 ? MPIX_REDOP_ERR_COUNT : MPIX_REDOP_ERR_ARG);
+        }
+        tab[s] = seg_offsets[s] / (int64_t) ext;
+        tab[nseg + s] = total;
+        total += seg_counts[s];
+    }
+    tab[2 * nseg] = total;
+    uint32_t opi = (uint32_t) op & 0xf;
+    if (opi == 14 || total == 0) {
+        free(tab);
+        return set_err(MPIX_REDOP_SUCCESS);
+    }
+    const Entry *e = opi == 13 ? nullptr : gpu_entry(opi, it);
+    if (!e && opi != 13) {
+        free(tab);
+        return set_err(MPIX_REDOP_ERR_TYPE);
+    }
+    if (opi == 13) {    // REPLACE: one copy per segment
+        for (MPIX_Aint s2 = 0; s2 < nseg && rc == MPIX_REDOP_SUCCESS; ++s2)
+            rc = hip_err(hipMemcpyAsync((char *) inoutbuf + seg_offsets[s2],
+                                        (const char *) inbuf + tab[nseg + s2] * ext,
+                                        (size_t) seg_counts[s2] * ext, hipMemcpyDeviceToDevice,
+                                        (hipStream_t) stream));
+        free(tab);
+        return set_err(rc);
+    }
+    int dev = 0;
+    (void) hipGetDevice(&dev);
+    DevState *d = dev_state(dev);
+    if (!d) {
+        free(tab);
+        return set_err(MPIX_REDOP_ERR_OTHER);
+    }
+    size_t need = 2 * (size_t) nseg + 1;
+    if (d->iov_cap < need) {
+        // the previous table may still be read by work queued on this stream
+        (void) hipStreamSynchronize((hipStream_t) stream);
+        if (d->iov_tab)
+            (void) hipFree(d->iov_tab);
+        d->iov_tab = nullptr;
+        d->iov_cap = 0;
+        if (hipMalloc((void **) &d->iov_tab, need * sizeof(int64_t)) != hipSuccess) {
+            free(tab);
+            return set_err(MPIX_REDOP_ERR_OTHER);
+        }
+        d->iov_cap = need;
+    }
+    // pageable source: the copy is complete (staged) when the call returns,
+    // and stream order keeps it behind earlier kernels that read the table
+    rc = hip_err(hipMemcpyAsync(d->iov_tab, tab, need * sizeof(int64_t), hipMemcpyHostToDevice,
+                                (hipStream_t) stream));
+    if (rc == MPIX_REDOP_SUCCESS)
+        rc = hip_err(hipStreamSynchronize((hipStream_t) stream));
+    free(tab);
+    if (rc != MPIX_REDOP_SUCCESS)
+        return set_err(rc);
+    return set_err(hip_err(e->iov(inbuf, inoutbuf, d->iov_tab, d->iov_tab + nseg, (int64_t) nseg,
+                                  (uint64_t) total, params(), launch_cfg(),
+                                  (hipStream_t) stream)));
 }
 
 int MPIX_Reduce_local_multi_async(const void *const *inbufs, int ninputs, void *inoutbuf,

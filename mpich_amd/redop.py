@@ -48,6 +48,8 @@ def lib():
             'MPIX_Reduce_local_vector_async': ([vp, vp, aint, aint, aint, i32, i32, vp], i32),
             'MPIX_Reduce_local_multi_async': ([ctypes.POINTER(vp), i32, vp, aint, i32, i32, vp],
                                               i32),
+            'MPIX_Reduce_local_iov_async': ([vp, vp, aint, ctypes.POINTER(aint),
+                                             ctypes.POINTER(aint), i32, i32, vp], i32),
             'MPIX_Redop_is_supported': ([i32, aint, i32], i32),
             'MPIX_Ipc_export': ([vp, vp, ctypes.POINTER(aint)], i32),
             'MPIX_Ipc_open': ([vp, ctypes.POINTER(vp)], i32),
@@ -116,6 +118,17 @@ def reduce_local_vector(inbuf, inoutbuf, count, blocklen, stride, basic_type, op
     return lib().MPIX_Reduce_local_vector_async(_addr(inbuf), _addr(inoutbuf), count, blocklen,
                                                 stride, H.as_c_int(basic_type), H.as_c_int(op),
                                                 _stream_ptr(stream))
+
+
+def reduce_local_iov_async(inbuf, inoutbuf, seg_offsets, seg_counts, basic_type, op,
+                           stream=None):
+    """derived target given as its flattened iov (byte offsets, element counts)"""
+    n = len(seg_offsets)
+    offs = (ctypes.c_ssize_t * n)(*seg_offsets)
+    cnts = (ctypes.c_ssize_t * n)(*seg_counts)
+    return lib().MPIX_Reduce_local_iov_async(_addr(inbuf), _addr(inoutbuf), n, offs, cnts,
+                                             H.as_c_int(basic_type), H.as_c_int(op),
+                                             _stream_ptr(stream))
 
 
 def reduce_local_multi_async(inbufs, inoutbuf, count, datatype, op, stream=None):

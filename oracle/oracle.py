@@ -35,6 +35,8 @@ def lib():
         L.oracle_reduce_local.argtypes = [vp, vp, il, i32, i32]
         L.oracle_reduce_local_mt.argtypes = [vp, vp, il, i32, i32, i32]
         L.oracle_reduce_local_vector.argtypes = [vp, vp, il, il, il, i32, i32]
+        L.oracle_reduce_local_iov.argtypes = [vp, vp, il, ctypes.POINTER(il), ctypes.POINTER(il),
+                                              i32, i32]
         L.oracle_internal.argtypes = [i32]
         L.oracle_extent.argtypes = [i32]
         L.oracle_extent.restype = il
@@ -71,6 +73,14 @@ def reduce_local(inbuf, inoutbuf, count, datatype, op, nthreads=1):
 def reduce_local_vector(inbuf, inoutbuf, count, blocklen, stride, datatype, op):
     return lib().oracle_reduce_local_vector(_ptr(inbuf), _ptr(inoutbuf), count, blocklen, stride,
                                             _i32(datatype), _i32(op))
+
+
+def reduce_local_iov(inbuf, inoutbuf, seg_offsets, seg_counts, datatype, op):
+    n = len(seg_offsets)
+    return lib().oracle_reduce_local_iov(_ptr(inbuf), _ptr(inoutbuf), n,
+                                         (ctypes.c_long * n)(*seg_offsets),
+                                         (ctypes.c_long * n)(*seg_counts), _i32(datatype),
+                                         _i32(op))
 
 
 def internal(datatype):

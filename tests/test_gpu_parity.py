@@ -484,3 +484,37 @@ def test_concurrent_callers(R, H, oracle):
     x, y = dev(np.ones(1000, np.float32)), dev(np.ones(1000, np.float32))
     assert R.MPI_Reduce_local(x, y, 1000, H.MPI_FLOAT, H.MPI_SUM) == 0
     assert np.all(host(y).view(np.float32) == 2)
+
+
+@pytest.mark.parametrize('dtname,opname', [('MPI_DOUBLE', 'MPI_SUM'), ('MPI_INT', 'MPI_BXOR'),
+                                           ('MPI_C_FLOAT_COMPLEX', 'MPI_PROD'),
+                                           ('MPI_SHORT', 'MPI_MIN')])
+def test_iov_target(R, H, oracle, dtname, opname):
+    """general derived target via its flattened iov (MPI_Type_indexed-like,
+    ragged segments incl. empty ones) against the oracle."""
+    dt, op = getattr(H, dtname), getattr(H, opname)
+    ext = R.datatype_extent(dt)
+    rng = np.random.default_rng(ext * 17)
+    nseg = 20000
+    cnts = rng.integers(0, 9, nseg)
+    gaps = rng.integers(0, 5, nseg)
+    offs, pos = [], 0
+    for c, g in zip(cnts, gaps):
+        pos += int(g)
+        offs.append(pos * ext)
+        pos += int(c)
+    total = int(cnts.sum())
+    if ext >= 4:
+        src = rng.uniform(-1, 1, total * ext // 4).astype(np.float32).view(np.uint8)
+        dst = rng.uniform(-1, 1, pos * ext // 4 + 4).astype(np.float32).view(np.uint8)
+    else:
+        src = rng.integers(-30000, 30000, total).astype(np.int16).view(np.uint8)
+        dst = rng.integers(-30000, 30000, pos + 8).astype(np.int16).view(np.uint8)
+    if dtname == 'MPI_DOUBLE':
+        src = rng.uniform(-1, 1, total).view(np.uint8)
+        dst = rng.uniform(-1, 1, pos + 1).view(np.uint8)
+    dd, ds = dev(dst), dev(src)
+    assert R.reduce_local_iov_async(ds, dd, offs, [int(c) for c in cnts], dt, op) == 0
+    exp = dst.copy()
+    assert oracle.reduce_local_iov(src, exp, offs, [int(c) for c in cnts], dt, op) == 0
+    assert np.array_equal(host(dd), exp)
