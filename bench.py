@@ -310,7 +310,31 @@ def main():
             torch.cuda.synchronize()
             tt = time.perf_counter() - t0
             chunks.append(dict(chunk_bytes=ck, calls=nch, GiBs=round(nbytes_alg / tt / GIB, 1)))
-        result['sweep'] = dict(size_kernel=sweep, chunked_1gib_async=chunks)
+        # the same chunked sweep replayed from a HIP graph (torch.cuda.graph):
+        # the launch-bound small chunks lose the per-call host launch cost
+        graphed = []
+        gs = torch.cuda.Stream()
+        for ck in (64 << 10, 256 << 10, 1 << 20, 4 << 20):
+            m = ck // 4
+            nch = min(n // m, 4096)
+            g = torch.cuda.CUDAGraph()
+            gs.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(gs):
+                with torch.cuda.graph(g, stream=gs):
+                    for k in range(nch):
+                        redop.check(redop.reduce_local_async(inb[k * m:], inout[k * m:], m,
+                                                             H.MPI_FLOAT, H.MPI_SUM, gs))
+            torch.cuda.synchronize()
+            g.replay()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            g.replay()
+            torch.cuda.synchronize()
+            tt = time.perf_counter() - t0
+            graphed.append(dict(chunk_bytes=ck, calls=nch, GiBs=round(3 * m * 4 * nch / tt / GIB, 1)))
+            del g
+        result['sweep'] = dict(size_kernel=sweep, chunked_1gib_async=chunks,
+                               chunked_hipgraph_replay=graphed)
 
     del inout, inb
     torch.cuda.empty_cache()
