@@ -393,3 +393,68 @@ def reduce_scatter_block_pull(sendbuf, recvbuf, recvcount, datatype, op, group=N
 
 
 ALGORITHMS['pull'] = reduce_scatter_block_pull
+
+
+def allreduce_recursive_doubling(sendbuf, recvbuf, count, datatype, op, group=None, combine=None,
+                                 extent=None, workspace=None):
+    """MPIR_Allreduce_intra_recursive_doubling
+    (src/mpi/coll/allreduce/allreduce_intra_recursive_doubling.c:24-150) for
+    the predefined (commutative) ops: log2(P) full-vector exchanges, each
+    folded in with MPIR_Reduce_local(tmp_buf, recvbuf).  Used below pof2
+    elements, where the reduce-scatter schedule cannot split the vector."""
+    rank = dist.get_rank(group)
+    size = dist.get_world_size(group)
+    if extent is None:
+        from . import redop
+        extent = redop.datatype_extent(datatype)
+    if combine is None:
+        combine = _default_combine(datatype, op)
+    g2l = (lambda r: dist.get_global_rank(group, r)) if group is not None else (lambda r: r)
+    rb = recvbuf.reshape(-1).view(torch.uint8)
+    nb = count * extent
+    if sendbuf is not None:
+        rb[:nb].copy_(sendbuf.reshape(-1).view(torch.uint8)[:nb])
+    if size == 1 or count == 0:
+        return recvbuf
+    pof2 = _pof2(size)
+    rem = size - pof2
+    tmp = workspace[:nb] if workspace is not None else \
+        torch.empty(nb, dtype=torch.uint8, device=rb.device)
+    if rank < 2 * rem:                                              # :59-86
+        if rank % 2 == 0:
+            _exchange(rb[:nb], g2l(rank + 1), None, None, group)
+            newrank = -1
+        else:
+            _exchange(None, None, tmp, g2l(rank - 1), group)
+            combine(tmp, rb[:nb], count)
+            newrank = rank // 2
+    else:
+        newrank = rank - rem
+    if newrank != -1:
+        mask = 1
+        while mask < pof2:                                          # :97-129
+            newdst = newrank ^ mask
+            dst = newdst * 2 + 1 if newdst < rem else newdst + rem
+            _exchange(rb[:nb], g2l(dst), tmp, g2l(dst), group)
+            combine(tmp, rb[:nb], count)
+            mask <<= 1
+    if rank < 2 * rem:                                              # :131-141
+        if rank % 2:
+            _exchange(rb[:nb], g2l(rank - 1), None, None, group)
+        else:
+            _exchange(None, None, rb[:nb], g2l(rank + 1), group)
+    return recvbuf
+
+
+def allreduce_auto(sendbuf, recvbuf, count, datatype, op, group=None, **kw):
+    """MPI_Allreduce algorithm choice: MPIR_CVAR_ALLREDUCE_INTRA_ALGORITHM
+    (`recursive_doubling` | `reduce_scatter_allgather`) or, by default, the
+    reduce-scatter + allgather schedule whenever count >= pof2 (the
+    condition the reference asserts for it, :127) and recursive doubling
+    below."""
+    algo = os.environ.get('MPIR_CVAR_ALLREDUCE_INTRA_ALGORITHM', 'auto')
+    if algo not in ('recursive_doubling', 'reduce_scatter_allgather'):
+        algo = 'reduce_scatter_allgather' if count >= _pof2(dist.get_world_size(group)) \
+            else 'recursive_doubling'
+    fn = allreduce if algo == 'reduce_scatter_allgather' else allreduce_recursive_doubling
+    return fn(sendbuf, recvbuf, count, datatype, op, group=group, **kw)

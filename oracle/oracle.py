@@ -48,6 +48,7 @@ def lib():
                                                    i32, i32, i32]
         L.oracle_rsb_pairwise.argtypes = L.oracle_rsb_recursive_halving.argtypes
         L.oracle_allreduce_rabenseifner.argtypes = L.oracle_rsb_recursive_halving.argtypes
+        L.oracle_allreduce_recursive_doubling.argtypes = L.oracle_rsb_recursive_halving.argtypes
         L.oracle_wtime.restype = ctypes.c_double
         _lib = L
     return _lib
@@ -123,14 +124,18 @@ def rsb_pairwise(sendbufs, recvcount, datatype, op):
     return rsb_recursive_halving(sendbufs, recvcount, datatype, op, algorithm='pairwise')
 
 
-def allreduce_rabenseifner(sendbufs, count, datatype, op):
-    """Simulate MPIR_Allreduce_intra_reduce_scatter_allgather over P ranks."""
+def allreduce_rabenseifner(sendbufs, count, datatype, op, algorithm='reduce_scatter_allgather'):
+    """Simulate MPIR_Allreduce_intra_reduce_scatter_allgather (or, with
+    algorithm='recursive_doubling', MPIR_Allreduce_intra_recursive_doubling)
+    over P ranks."""
     P = len(sendbufs)
     ext = extent(datatype)
     recvs = [np.zeros(count * ext, np.uint8) for _ in range(P)]
     sp = (ctypes.c_void_p * P)(*[s.ctypes.data for s in sendbufs])
     rp = (ctypes.c_void_p * P)(*[r.ctypes.data for r in recvs])
-    rc = lib().oracle_allreduce_rabenseifner(sp, rp, count, _i32(datatype), _i32(op), P)
+    fn = lib().oracle_allreduce_recursive_doubling if algorithm == 'recursive_doubling' else \
+        lib().oracle_allreduce_rabenseifner
+    rc = fn(sp, rp, count, _i32(datatype), _i32(op), P)
     if rc:
         raise RuntimeError('oracle allreduce failed: %d' % rc)
     return recvs

@@ -111,7 +111,7 @@ def test_plan_matches_reference_counts():
     assert p['newrank'] == -1 and p['steps'] == []
 
 
-def _ar_worker(rank, world, port, outdir, count):
+def _ar_worker(rank, world, port, outdir, count, algo='reduce_scatter_allgather'):
     import torch
     import torch.distributed as dist
     os.environ['MASTER_ADDR'] = '127.0.0.1'
@@ -129,21 +129,23 @@ def _ar_worker(rank, world, port, outdir, count):
         def combine(inb, inoutb, n):
             assert orc.reduce_local(inb.numpy(), inoutb.numpy(), n, dt, op) == 0
         return combine
-    coll.allreduce(torch.from_numpy(send.copy()), recv, count, MPI_FLOAT, MPI_SUM,
-                   combine=mk_combine(MPI_FLOAT, MPI_SUM), extent=4)
+    fn = coll.allreduce if algo == 'reduce_scatter_allgather' else \
+        coll.allreduce_recursive_doubling
+    fn(torch.from_numpy(send.copy()), recv, count, MPI_FLOAT, MPI_SUM,
+       combine=mk_combine(MPI_FLOAT, MPI_SUM), extent=4)
     np.save(os.path.join(outdir, 'send%d.npy' % rank), send)
     np.save(os.path.join(outdir, 'recv%d.npy' % rank), recv.numpy())
     # the allred.c KATs that were generated for this world size, end to end
     bad = []
     for c in gu.load_cases():
         if c['nranks'] != world or not c['name'].startswith('allred ') or \
-                c['count'] < (1 << (world.bit_length() - 1)):
+                (algo == 'reduce_scatter_allgather' and
+                 c['count'] < (1 << (world.bit_length() - 1))):
             continue
         ext = len(c['expected']) // c['count']
         out = torch.zeros(c['count'] * ext, dtype=torch.uint8)
-        coll.allreduce(torch.from_numpy(c['inputs'][rank].copy()), out, c['count'],
-                       c['datatype'], c['op'], combine=mk_combine(c['datatype'], c['op']),
-                       extent=ext)
+        fn(torch.from_numpy(c['inputs'][rank].copy()), out, c['count'], c['datatype'], c['op'],
+           combine=mk_combine(c['datatype'], c['op']), extent=ext)
         if gu.mismatches(c, out.numpy()):
             bad.append(c['id'])
     with open(os.path.join(outdir, 'bad%d.txt' % rank), 'w') as f:
@@ -152,17 +154,18 @@ def _ar_worker(rank, world, port, outdir, count):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize('algo', ['reduce_scatter_allgather', 'recursive_doubling'])
 @pytest.mark.parametrize('world', [2, 3, 4, 7])
-def test_allreduce_gloo(oracle, tmp_path, world):
+def test_allreduce_gloo(oracle, tmp_path, world, algo):
     """Rabenseifner allreduce over gloo: bit-identical on every rank to the
     oracle's simulation of the reference schedule, and all allred.c KATs
     generated for this world size pass end to end."""
     count = 1037
-    mp.spawn(_ar_worker, args=(world, _free_port(), str(tmp_path), count), nprocs=world,
+    mp.spawn(_ar_worker, args=(world, _free_port(), str(tmp_path), count, algo), nprocs=world,
              join=True)
     sends = [np.load(tmp_path / ('send%d.npy' % r)) for r in range(world)]
     exp = oracle.allreduce_rabenseifner([s.view(np.uint8) for s in sends], count, 0x4c00040a,
-                                        0x58000003)
+                                        0x58000003, algorithm=algo)
     for r in range(world):
         assert np.load(tmp_path / ('recv%d.npy' % r)).tobytes() == exp[r].tobytes(), r
         assert open(tmp_path / ('bad%d.txt' % r)).read() == '', r
