@@ -166,8 +166,8 @@ def reduce_scatter_block(sendbuf, recvbuf, recvcount, datatype, op, group=None, 
 def reduce_scatter_block_pairwise(sendbuf, recvbuf, recvcount, datatype, op, group=None,
                                   combine=None, extent=None, workspace=None, concurrent=True):
     """MPI_Reduce_scatter_block, pairwise exchange (reference algorithm
-    `pairwise`).  workspace: optional byte tensor of >= (P-1)*recvcount
-    elements for the received blocks."""
+    `pairwise`).  workspace: optional byte tensor of >= (P-1) * (block bytes
+    rounded up to 256) for the received blocks."""
     rank = dist.get_rank(group)
     size = dist.get_world_size(group)
     if extent is None:
@@ -185,27 +185,32 @@ def reduce_scatter_block_pairwise(sendbuf, recvbuf, recvcount, datatype, op, gro
     if size == 1:
         return recvbuf
     nslot = size - 1 if concurrent else 1
+    # slots start on 256-byte boundaries so every received block has the same
+    # 16-byte phase as the result and takes the packet kernel
+    sstride = (blk + 255) // 256 * 256
     if workspace is not None:
-        slots = workspace[:nslot * blk]
+        slots = workspace[:nslot * sstride]
     else:
-        slots = torch.empty(nslot * blk, dtype=torch.uint8, device=sb.device)
+        slots = torch.empty(nslot * sstride, dtype=torch.uint8, device=sb.device)
+
+    def slot(i):
+        return slots[i * sstride:i * sstride + blk]
     peers = [((rank + i) % size, (rank - i + size) % size) for i in range(1, size)]
     if not concurrent:                                              # the reference's loop
         for dst, src in peers:
-            _exchange(sb[block(dst)], g2l(dst), slots[:blk], g2l(src), group)
+            _exchange(sb[block(dst)], g2l(dst), slot(0), g2l(src), group)
             if combine is not None:
-                combine(slots[:blk], rb[:blk], recvcount)
+                combine(slot(0), rb[:blk], recvcount)
             else:
-                _default_combine(datatype, op)(slots[:blk], rb[:blk], recvcount)
+                _default_combine(datatype, op)(slot(0), rb[:blk], recvcount)
         return recvbuf
     ops = []
     for i, (dst, src) in enumerate(peers):
         ops.append(dist.P2POp(dist.isend, sb[block(dst)], g2l(dst), group=group, tag=TAG))
-        ops.append(dist.P2POp(dist.irecv, slots[i * blk:(i + 1) * blk], g2l(src), group=group,
-                              tag=TAG))
+        ops.append(dist.P2POp(dist.irecv, slot(i), g2l(src), group=group, tag=TAG))
     for w in dist.batch_isend_irecv(ops):
         w.wait()
-    ins = [slots[i * blk:(i + 1) * blk] for i in range(size - 1)]
+    ins = [slot(i) for i in range(size - 1)]
     if combine is not None:
         for x in ins:                                               # :86-100, i = 1..P-1
             combine(x, rb[:blk], recvcount)

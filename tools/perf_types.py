@@ -46,6 +46,14 @@ def main():
                 lambda: redop.check(redop.reduce_local_async(b, a, n, dt, op, s)), 10, s)
             out.append(dict(type=tn, op=on, bytes=n * ext, ms=round(avg, 4),
                             GBs=round(3 * n * ext / (avg * 1e-3) / 1e9, 1)))
+    # relatively misaligned operands (in at +4 bytes): the element-wise kernel
+    n = nbytes // 4 - 4
+    redop.check(redop.reduce_local_async(b.data_ptr() + 4, a, n, H.MPI_FLOAT, H.MPI_SUM, s))
+    avg, med, mn = event_time_per_launch(
+        lambda: redop.check(redop.reduce_local_async(b.data_ptr() + 4, a, n, H.MPI_FLOAT,
+                                                     H.MPI_SUM, s)), 10, s)
+    misaligned = dict(case='fp32 SUM, in at +4 B relative to inout (k_elem path)',
+                      ms=round(avg, 4), GBs=round(12 * n / (avg * 1e-3) / 1e9, 1))
     del a, b
     torch.cuda.empty_cache()
     # config 5: vector(67108864, 1, 2, MPI_DOUBLE), 512 MiB payload, 1 GiB span
@@ -60,7 +68,8 @@ def main():
     vec = dict(config='vector(67108864,1,2,MPI_DOUBLE) SUM', ms=round(avg, 4),
                GBs_algorithmic=round(3 * cnt * 8 / (avg * 1e-3) / 1e9, 1),
                frac_of_8TBs=round(3 * cnt * 8 / (avg * 1e-3) / 8e12, 4))
-    print(json.dumps(dict(per_type=out, vector=vec, build=redop.build_info())))
+    print(json.dumps(dict(per_type=out, vector=vec, misaligned=misaligned,
+                          build=redop.build_info())))
 
 
 if __name__ == '__main__':
