@@ -301,6 +301,16 @@ Where classify(const void *p, int *dev, const void **devptr)
     return Where::Pageable;
 }
 
+// The stream-ordered entry points take device-accessible pointers only: a
+// pageable host pointer handed to a kernel would fault the GPU, so it is
+// refused with MPI_ERR_BUFFER; pinned host memory is translated to its
+// device mapping.
+bool device_accessible(const void *p, const void **devptr)
+{
+    int dev = 0;
+    return classify(p, &dev, devptr) != Where::Pageable;
+}
+
 bool overlaps(const void *a, const void *b, uint64_t bytes)
 {
     uintptr_t x = (uintptr_t) a, y = (uintptr_t) b;
@@ -465,7 +475,10 @@ int MPIX_Reduce_local_async(const void *inbuf, void *inoutbuf, MPIX_Aint count,
     int rc = validate(inbuf, inoutbuf, count, (uint32_t) datatype, (uint32_t) op, &it, &ext);
     if (rc != MPIX_REDOP_SUCCESS || count == 0)
         return set_err(rc);
-    return set_err(enqueue(inbuf, inoutbuf, (uint64_t) count, it, ext, (uint32_t) op,
+    const void *pin, *pio;
+    if (!device_accessible(inbuf, &pin) || !device_accessible(inoutbuf, &pio))
+        return set_err(MPIX_REDOP_ERR_BUFFER);
+    return set_err(enqueue(pin, (void *) pio, (uint64_t) count, it, ext, (uint32_t) op,
                            (hipStream_t) stream));
 }
 
@@ -524,6 +537,13 @@ int MPIX_Reduce_local_vector_async(const void *inbuf, void *inoutbuf, MPIX_Aint 
     uintptr_t x = (uintptr_t) inbuf, y = (uintptr_t) inoutbuf;
     if (x < y + span && y < x + n * ext)
         return set_err(MPIX_REDOP_ERR_BUFFER);
+    {
+        const void *pin, *pio;
+        if (!device_accessible(inbuf, &pin) || !device_accessible(inoutbuf, &pio))
+            return set_err(MPIX_REDOP_ERR_BUFFER);
+        inbuf = pin;
+        inoutbuf = (void *) pio;
+    }
     uint32_t opi = (uint32_t) op & 0xf;
     if (opi == 14)
         return set_err(MPIX_REDOP_SUCCESS);
@@ -578,6 +598,13 @@ int MPIX_Reduce_local_iov_async(const void *inbuf, void *inoutbuf, MPIX_Aint nse
         return set_err(MPIX_REDOP_ERR_BUFFER);
     if (is_pairtype(it))
         return set_err(MPIX_REDOP_ERR_TYPE);    // pair targets split across segments: not here
+    {
+        const void *pin, *pio;
+        if (!device_accessible(inbuf, &pin) || !device_accessible(inoutbuf, &pio))
+            return set_err(MPIX_REDOP_ERR_BUFFER);
+        inbuf = pin;
+        inoutbuf = (void *) pio;
+    }
     // host-side tables: element offsets + prefix counts (2*nseg + 1 entries)
     int64_t *tab = (int64_t *) malloc(sizeof(int64_t) * (2 * (size_t) nseg + 1));
     if (!tab)
@@ -663,6 +690,15 @@ int MPIX_Reduce_local_multi_async(const void *const *inbufs, int ninputs, void *
     }
     if (count == 0)
         return set_err(MPIX_REDOP_SUCCESS);
+    const void *dins[mpix::kMaxMultiInputs];
+    const void *pio;
+    if (!device_accessible(inoutbuf, &pio))
+        return set_err(MPIX_REDOP_ERR_BUFFER);
+    for (int q = 0; q < ninputs; ++q)
+        if (!device_accessible(inbufs[q], &dins[q]))
+            return set_err(MPIX_REDOP_ERR_BUFFER);
+    inbufs = dins;
+    inoutbuf = (void *) pio;
     uint32_t opi = (uint32_t) op & 0xf;
     if (opi == 14)
         return set_err(MPIX_REDOP_SUCCESS);

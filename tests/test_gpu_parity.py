@@ -549,3 +549,18 @@ def test_async_is_graph_capturable(R, H, oracle):
     for _ in range(3):
         oracle.reduce_local(b, exp, n * chunks, H.MPI_FLOAT, H.MPI_SUM)
     assert np.array_equal(host(da).view(np.float32), exp)
+
+
+def test_async_refuses_pageable_host(R, H):
+    """a pageable host pointer in a stream-ordered call must be refused
+    (a kernel touching it would fault the GPU), pinned host is accepted."""
+    a = np.ones(4096, np.float32)
+    b = np.ones(4096, np.float32)
+    assert R.reduce_local_async(b, a, 4096, H.MPI_FLOAT, H.MPI_SUM) == H.MPI_ERR_BUFFER
+    pa = torch.ones(4096).pin_memory()
+    pb = torch.ones(4096).pin_memory()
+    assert R.reduce_local_async(pb, pa, 4096, H.MPI_FLOAT, H.MPI_SUM) == 0
+    torch.cuda.synchronize()
+    assert torch.all(pa == 2)
+    assert R.reduce_local_multi_async([b], torch.zeros(4096, device='cuda'), 4096, H.MPI_FLOAT,
+                                      H.MPI_SUM) == H.MPI_ERR_BUFFER

@@ -61,5 +61,22 @@ int main()
         hipEventRecord(ev, s);
         while (hipEventQuery(ev) == hipErrorNotReady) {}
     }));
+    // completion through a value written to pinned host memory by the stream
+    volatile uint32_t *flag = nullptr;
+    hipHostMalloc((void **) &flag, 64, hipHostMallocCoherent);
+    *flag = 0;
+    uint32_t seq = 0;
+    printf("launch + hipStreamWriteValue32    %8.0f ns\n", med_ns([&] {
+        ++seq;
+        MPIX_Reduce_local_async(b, a, 1, MPIX_MPI_FLOAT, MPIX_SUM, s);
+        hipStreamWriteValue32(s, (void *) flag, seq, 0);
+        while (*flag != seq) {}
+    }));
+    printf("empty hipStreamWriteValue32+spin  %8.0f ns\n", med_ns([&] {
+        ++seq;
+        hipStreamWriteValue32(s, (void *) flag, seq, 0);
+        while (*flag != seq) {}
+    }));
+    hipStreamSynchronize(s);
     return 0;
 }
