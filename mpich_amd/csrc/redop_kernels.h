@@ -10,8 +10,10 @@
 //   * each packet holds 16/sizeof(unit) elements, combined in registers;
 //   * elements before the first 16-byte boundary of inout (head) and after
 //     the last full packet (tail) are done element-wise by block 0;
-//   * if in and inout disagree modulo 16 bytes, an element-wise grid-stride
-//     kernel is used instead (still coalesced for >= 4-byte units).
+//   * if in and inout disagree modulo 16 bytes, `in` is read with unaligned
+//     16-byte loads (gfx950 global loads take element-aligned addresses);
+//     only buffers that are not even element-aligned fall back to an
+//     element-wise grid-stride kernel.
 // Launch geometry: one tile of blockDim*U packets per block, grid =
 // ceil(npk / tile) (optionally capped, then grid-stride).
 #pragma once
@@ -51,6 +53,15 @@ template <bool NT> __device__ __forceinline__ void st16(v4u *p, v4u v)
         *p = v;
 }
 
+// 16-byte load from an address that is only element-aligned: gfx950 global
+// loads accept unaligned addresses, so this is still one global_load_dwordx4.
+__device__ __forceinline__ v4u ld16u(const char *p)
+{
+    v4u v;
+    __builtin_memcpy(&v, p, 16);
+    return v;
+}
+
 template <class C> __device__ __forceinline__ v4u combine16(v4u a, v4u b, const Params &prm)
 {
     using T = typename C::unit;
@@ -65,23 +76,33 @@ template <class C> __device__ __forceinline__ v4u combine16(v4u a, v4u b, const 
     return __builtin_bit_cast(v4u, pa);
 }
 
-template <class C, int U, bool NTL, bool NTS>
+// AIN: `in` has the same 16-byte phase as `io` (packet loads); otherwise it
+// is only element-aligned and its packets are read with unaligned loads
+// (still one dwordx4 per lane; the lines are shared with the neighbours').
+template <class C, int U, bool NTL, bool NTS, bool AIN = true>
 __global__ void __launch_bounds__(1024)
 k_contig(const typename C::unit *__restrict__ in, typename C::unit *__restrict__ io,
          uint64_t head, uint64_t npk, uint64_t tail_start, uint32_t ntail, Params prm)
 {
     const v4u *__restrict__ vin = reinterpret_cast<const v4u *>(in + head);
+    const char *__restrict__ cin = reinterpret_cast<const char *>(in + head);
     v4u *__restrict__ vio = reinterpret_cast<v4u *>(io + head);
     const uint64_t nt = blockDim.x;
     const uint64_t tile = nt * U;
     const uint64_t stride = (uint64_t) gridDim.x * tile;
+    auto ldin = [&](uint64_t k) -> v4u {
+        if constexpr (AIN)
+            return ld16<NTL>(vin + k);
+        else
+            return ld16u(cin + 16 * k);
+    };
     for (uint64_t i = (uint64_t) blockIdx.x * tile + threadIdx.x; i < npk; i += stride) {
         if (i + (U - 1) * nt < npk) {
             v4u a[U], b[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 a[u] = ld16<NTL>(vio + i + u * nt);
-                b[u] = ld16<NTL>(vin + i + u * nt);
+                b[u] = ldin(i + u * nt);
             }
 #pragma unroll
             for (int u = 0; u < U; ++u)
@@ -90,7 +111,7 @@ k_contig(const typename C::unit *__restrict__ in, typename C::unit *__restrict__
             for (int u = 0; u < U; ++u) {
                 uint64_t k = i + u * nt;
                 if (k < npk)
-                    st16<NTS>(vio + k, combine16<C>(ld16<NTL>(vio + k), ld16<NTL>(vin + k), prm));
+                    st16<NTS>(vio + k, combine16<C>(ld16<NTL>(vio + k), ldin(k), prm));
             }
         }
     }
@@ -290,7 +311,7 @@ hipError_t launch_contig(const void *in, void *io, uint64_t count, const Params 
     const T *tin = static_cast<const T *>(in);
     T *tio = static_cast<T *>(io);
     uintptr_t ai = reinterpret_cast<uintptr_t>(in), ao = reinterpret_cast<uintptr_t>(io);
-    if ((ai & 15) == (ao & 15) && (ao % sizeof(T)) == 0) {
+    if ((ao % sizeof(T)) == 0 && (ai % sizeof(T)) == 0) {
         uint64_t head = ((16 - (ao & 15)) & 15) / sizeof(T);
         if (head > count)
             head = count;
@@ -299,9 +320,14 @@ hipError_t launch_contig(const void *in, void *io, uint64_t count, const Params 
         uint32_t ntail = (uint32_t) (count - tail_start);
         const uint64_t tile = (uint64_t) cfg.block * MPIX_REDOP_UNROLL;
         unsigned grid = grid_for(tile, npk, cfg.max_grid);
-        hipLaunchKernelGGL((k_contig<C, MPIX_REDOP_UNROLL, MPIX_REDOP_NT_LOAD, MPIX_REDOP_NT_STORE>),
-                           dim3(grid), dim3(cfg.block), 0, s, tin, tio, head, npk, tail_start,
-                           ntail, prm);
+        if ((ai & 15) == (ao & 15))
+            hipLaunchKernelGGL(
+                (k_contig<C, MPIX_REDOP_UNROLL, MPIX_REDOP_NT_LOAD, MPIX_REDOP_NT_STORE, true>),
+                dim3(grid), dim3(cfg.block), 0, s, tin, tio, head, npk, tail_start, ntail, prm);
+        else
+            hipLaunchKernelGGL(
+                (k_contig<C, MPIX_REDOP_UNROLL, MPIX_REDOP_NT_LOAD, MPIX_REDOP_NT_STORE, false>),
+                dim3(grid), dim3(cfg.block), 0, s, tin, tio, head, npk, tail_start, ntail, prm);
     } else {
         unsigned grid = grid_for((uint64_t) cfg.block * 4, count, cfg.max_grid);
         hipLaunchKernelGGL((k_elem<C>), dim3(grid), dim3(cfg.block), 0, s, tin, tio, count, prm);
