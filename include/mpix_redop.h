@@ -255,6 +255,8 @@ void MPIX_MINLOC_fn(void *invec, void *inoutvec, MPIX_Aint *len, MPIX_Datatype *
 void MPIX_MAXLOC_fn(void *invec, void *inoutvec, MPIX_Aint *len, MPIX_Datatype *type);
 void MPIX_REPLACE_fn(void *invec, void *inoutvec, MPIX_Aint *len, MPIX_Datatype *type);
 void MPIX_NO_OP_fn(void *invec, void *inoutvec, MPIX_Aint *len, MPIX_Datatype *type);
+/* MPIX_EQUAL (opequal.c:20-35): MPI_BYTE, 8-byte is_equal header + payload */
+void MPIX_EQUAL_fn(void *invec, void *inoutvec, MPIX_Aint *len, MPIX_Datatype *type);
 
 int MPIX_Redop_last_error(void);
 const char *MPIX_Redop_error_string(int code);

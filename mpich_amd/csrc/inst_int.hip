@@ -41,6 +41,47 @@ const Entry *flog_ops(int opi)
 
 }  // namespace
 
+// MPIX_EQUAL (src/mpi/coll/op/opequal.c:20-35): MPI_BYTE buffers whose first
+// 8 bytes are an is_equal flag; inout's flag becomes 0 if either flag is not
+// 1 or the payloads differ.  Not element-wise: a byte compare whose only
+// effect is zeroing one word, so every wave that sees a difference stores the
+// zero (idempotent, no atomics needed).
+__global__ void __launch_bounds__(256)
+k_equal(const unsigned char *__restrict__ in, unsigned char *__restrict__ io, uint64_t n)
+{
+    uint64_t hin, hio;
+    __builtin_memcpy(&hin, in, 8);
+    __builtin_memcpy(&hio, io, 8);
+    const uint64_t zero = 0;
+    if (hin != 1 || hio != 1) {
+        if (blockIdx.x == 0 && threadIdx.x == 0)
+            __builtin_memcpy(io, &zero, 8);
+        return;
+    }
+    const uint64_t data = n - 8, npk = data / 16;
+    const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
+    bool diff = false;
+    for (uint64_t k = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x; k < npk; k += stride) {
+        v4u a = ld16u(reinterpret_cast<const char *>(io) + 8 + 16 * k);
+        v4u b = ld16u(reinterpret_cast<const char *>(in) + 8 + 16 * k);
+        diff |= (a.x != b.x) | (a.y != b.y) | (a.z != b.z) | (a.w != b.w);
+    }
+    if (blockIdx.x == 0)
+        for (uint64_t t = 8 + npk * 16 + threadIdx.x; t < n; t += blockDim.x)
+            diff |= in[t] != io[t];
+    if (diff)
+        __builtin_memcpy(io, &zero, 8);
+}
+
+hipError_t launch_equal(const void *in, void *io, uint64_t n, hipStream_t s)
+{
+    uint64_t npk = (n - 8) / 16;
+    unsigned grid = grid_for(256ull * 4, npk, 0);
+    hipLaunchKernelGGL(k_equal, dim3(grid), dim3(256), 0, s,
+                       static_cast<const unsigned char *>(in), static_cast<unsigned char *>(io), n);
+    return hipGetLastError();
+}
+
 const Entry *lookup_int(int raw, int opi)
 {
     switch ((unsigned) raw) {

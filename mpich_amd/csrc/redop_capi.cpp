@@ -354,6 +354,9 @@ int enqueue(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext,
         return MPIX_REDOP_SUCCESS;
     if (opi == 13)      // MPI_REPLACE = MPIR_Localcopy (op_fns.c:445-457)
         return hip_err(hipMemcpyAsync(io, in, count * ext, hipMemcpyDeviceToDevice, s));
+    if (opi == 15)      // MPIX_EQUAL, MPI_BYTE only (opequal.c:22-23)
+        return ((it & 0xffffff00u) == U8 && count >= 8)
+            ? hip_err(mpix::launch_equal(in, io, count, s)) : MPIX_REDOP_ERR_TYPE;
     const Entry *e = gpu_entry(opi, it);
     if (!e)
         return MPIX_REDOP_ERR_TYPE;
@@ -491,7 +494,8 @@ int MPIX_Reduce_local(const void *inbuf, void *inoutbuf, MPIX_Aint count, MPIX_D
     if (rc != MPIX_REDOP_SUCCESS || count == 0)
         return set_err(rc);
     uint32_t opi = (uint32_t) op & 0xf;
-    if (opi != 13 && opi != 14 && !gpu_entry(opi, it))
+    if (opi == 15 ? ((it & 0xffffff00u) != U8 || count < 8)
+                  : (opi != 13 && opi != 14 && !gpu_entry(opi, it)))
         return set_err(MPIX_REDOP_ERR_TYPE);
     launch_cfg();
     int din = -1, dio = -1, cur = 0;
@@ -753,6 +757,8 @@ int MPIX_Redop_is_supported(MPIX_Op op, MPIX_Aint count, MPIX_Datatype datatype)
     uint32_t opi = (uint32_t) op & 0xf;
     if (opi == 13 || opi == 14)
         return 1;
+    if (opi == 15)
+        return (it & 0xffffff00u) == U8;
     return gpu_entry(opi, it) ? 1 : 0;
 }
 
@@ -848,13 +854,14 @@ MPIX_OPFN(MPIX_MINLOC_fn, MPIX_MINLOC)
 MPIX_OPFN(MPIX_MAXLOC_fn, MPIX_MAXLOC)
 MPIX_OPFN(MPIX_REPLACE_fn, MPIX_REPLACE)
 MPIX_OPFN(MPIX_NO_OP_fn, MPIX_NO_OP)
+MPIX_OPFN(MPIX_EQUAL_fn, MPIX_EQUAL)
 #undef MPIX_OPFN
 
 // order of src/mpi/coll/op/oputil.c:10-27 / mpi.h.in:297-311
 MPIX_op_function *const MPIX_Op_table[16] = {
     nullptr, MPIX_MAXF, MPIX_MINF, MPIX_SUM_fn, MPIX_PROD_fn, MPIX_LAND_fn, MPIX_BAND_fn,
     MPIX_LOR_fn, MPIX_BOR_fn, MPIX_LXOR_fn, MPIX_BXOR_fn, MPIX_MINLOC_fn, MPIX_MAXLOC_fn,
-    MPIX_REPLACE_fn, MPIX_NO_OP_fn, nullptr,
+    MPIX_REPLACE_fn, MPIX_NO_OP_fn, MPIX_EQUAL_fn,
 };
 
 }  // extern "C"

@@ -42,6 +42,9 @@ const Entry *lookup_int(int raw, int opi);
 const Entry *lookup_fp(int raw, int opi);
 const Entry *lookup_pair(int raw, int opi);
 
+// MPIX_EQUAL on an MPI_BYTE buffer of n >= 8 bytes (opequal.c:20-35)
+hipError_t launch_equal(const void *in, void *io, uint64_t n, hipStream_t s);
+
 // compile-time unroll of the packet kernel (packets per lane per operand)
 int unroll();
 

@@ -28,7 +28,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 OPS = dict(MAX=0x58000001, MIN=0x58000002, SUM=0x58000003, PROD=0x58000004,
            LAND=0x58000005, BAND=0x58000006, LOR=0x58000007, BOR=0x58000008,
            LXOR=0x58000009, BXOR=0x5800000a, MINLOC=0x5800000b,
-           MAXLOC=0x5800000c, REPLACE=0x5800000d, NO_OP=0x5800000e)
+           MAXLOC=0x5800000c, REPLACE=0x5800000d, NO_OP=0x5800000e, EQUAL=0x5800000f)
 
 DT = dict(
     MPI_CHAR=0x4c000101, MPI_UNSIGNED_CHAR=0x4c000102, MPI_SHORT=0x4c000203,
@@ -511,6 +511,26 @@ ra = np.arange(8, dtype='<i4')
 rb = np.arange(100, 108, dtype='<i4')
 add('edge REPLACE int', 'MPI_INT', 'REPLACE', [ra, rb], rb, 'op_fns.c:445-457', 'inout = in')
 add('edge NO_OP int', 'MPI_INT', 'NO_OP', [ra, rb], ra, 'op_fns.c:439-443', 'inout unchanged')
+
+# MPIX_EQUAL (src/mpi/coll/op/opequal.c:20-35): MPI_BYTE buffers led by a
+# uint64 is_equal flag; inout's flag drops to 0 unless both flags are 1 and
+# the payloads match byte for byte.  (Reached only through
+# MPIR_Reduce_equal / MPIR_Allreduce_equal, opequal.c:37-102.)
+def eq_buf(flag, payload):
+    return np.concatenate([np.array([flag], '<u8').view(np.uint8), np.array(payload, np.uint8)])
+
+
+for nm, a_, b_, e_ in (
+        ('equal payloads', eq_buf(1, [1, 2, 3, 4, 5]), eq_buf(1, [1, 2, 3, 4, 5]), 1),
+        ('one byte differs', eq_buf(1, [1, 2, 3, 4, 5]), eq_buf(1, [1, 2, 3, 9, 5]), 0),
+        ('in flag 0', eq_buf(1, [7] * 20), eq_buf(0, [7] * 20), 0),
+        ('inout flag 0', eq_buf(0, [7] * 20), eq_buf(1, [7] * 20), 0),
+        ('flag 2 is not 1', eq_buf(1, [7] * 3), eq_buf(2, [7] * 3), 0),
+        ('header only', eq_buf(1, []), eq_buf(1, []), 1)):
+    exp = a_.copy()
+    exp[:8] = np.array([e_], '<u8').view(np.uint8)
+    add('edge EQUAL %s' % nm, 'MPI_BYTE', 'EQUAL', [a_, b_], exp, 'src/mpi/coll/op/opequal.c:20-35',
+        'is_equal = (in.flag == 1 && inout.flag == 1 && payloads equal) ? inout.flag : 0')
 
 # ---------------------------------------------------------------------------
 # Rule-based KATs too large to store as bytes: the tests build the arrays

@@ -40,10 +40,11 @@ def test_op_table_layout(R):
     L = R.lib()
     tab = (ctypes.c_void_p * 16).in_dll(L, 'MPIX_Op_table')
     # oputil.c:10-27 order: NULL, MAX, MIN, SUM, PROD, LAND, BAND, LOR, BOR,
-    # LXOR, BXOR, MINLOC, MAXLOC, REPLACE, NO_OP, (EQUAL not provided)
+    # LXOR, BXOR, MINLOC, MAXLOC, REPLACE, NO_OP, EQUAL
     names = [None, 'MPIX_MAXF', 'MPIX_MINF', 'MPIX_SUM_fn', 'MPIX_PROD_fn', 'MPIX_LAND_fn',
              'MPIX_BAND_fn', 'MPIX_LOR_fn', 'MPIX_BOR_fn', 'MPIX_LXOR_fn', 'MPIX_BXOR_fn',
-             'MPIX_MINLOC_fn', 'MPIX_MAXLOC_fn', 'MPIX_REPLACE_fn', 'MPIX_NO_OP_fn', None]
+             'MPIX_MINLOC_fn', 'MPIX_MAXLOC_fn', 'MPIX_REPLACE_fn', 'MPIX_NO_OP_fn',
+             'MPIX_EQUAL_fn']
     for i, n in enumerate(names):
         if n is None:
             assert not tab[i]

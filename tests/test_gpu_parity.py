@@ -564,3 +564,27 @@ def test_async_refuses_pageable_host(R, H):
     assert torch.all(pa == 2)
     assert R.reduce_local_multi_async([b], torch.zeros(4096, device='cuda'), 4096, H.MPI_FLOAT,
                                       H.MPI_SUM) == H.MPI_ERR_BUFFER
+
+
+@pytest.mark.parametrize('nbytes', [8, 9, 24, 4099, (1 << 20) + 13])
+def test_equal_op(R, H, oracle, nbytes):
+    """MPIX_EQUAL (opequal.c:20-35) on the GPU against the oracle."""
+    rng = np.random.default_rng(nbytes)
+    base = rng.integers(0, 256, nbytes, dtype=np.uint8)
+    base[:8] = np.array([1], '<u8').view(np.uint8)
+    variants = [base.copy()]
+    if nbytes > 8:
+        v = base.copy()
+        v[int(rng.integers(8, nbytes))] ^= 0x40
+        variants.append(v)
+    v = base.copy()
+    v[:8] = 0
+    variants.append(v)
+    for other in variants:
+        for a, b in ((base, other), (other, base)):
+            da, db = dev(a), dev(b)
+            assert R.MPI_Reduce_local(db, da, nbytes, H.MPI_BYTE, 0x5800000f) == 0
+            exp = a.copy()
+            assert oracle.reduce_local(b.copy(), exp, nbytes, H.MPI_BYTE, 0x5800000f) == 0
+            assert np.array_equal(host(da), exp)
+    assert R.MPI_Reduce_local(dev(base), dev(base), nbytes, H.MPI_INT, 0x5800000f) != 0
