@@ -54,6 +54,28 @@ def main():
                                                      H.MPI_SUM, s)), 10, s)
     misaligned = dict(case='fp32 SUM, in at +4 B relative to inout (k_elem path)',
                       ms=round(avg, 4), GBs=round(12 * n / (avg * 1e-3) / 1e9, 1))
+    # fused multi-input combine (pairwise reduce-scatter epilogue): 7 received
+    # 64 MiB blocks folded into the result in one pass vs 7 sequential calls
+    blk = 64 << 20
+    m = blk // 4
+    ins = [torch.empty(m, dtype=torch.float32, device=dev).uniform_(-1, 1) for _ in range(7)]
+    acc = torch.empty(m, dtype=torch.float32, device=dev).uniform_(-1, 1)
+    torch.cuda.synchronize()
+    redop.check(redop.reduce_local_multi_async(ins, acc, m, H.MPI_FLOAT, H.MPI_SUM, s))
+    t_multi, _, _ = event_time_per_launch(
+        lambda: redop.check(redop.reduce_local_multi_async(ins, acc, m, H.MPI_FLOAT, H.MPI_SUM,
+                                                           s)), 10, s)
+
+    def seq():
+        for x in ins:
+            redop.check(redop.reduce_local_async(x, acc, m, H.MPI_FLOAT, H.MPI_SUM, s))
+    t_seq, _, _ = event_time_per_launch(seq, 10, s)
+    multi = dict(case='7 x 64 MiB fp32 blocks folded into a 64 MiB result',
+                 fused_ms=round(t_multi, 4), sequential_ms=round(t_seq, 4),
+                 fused_GBs=round(8 * blk / (t_multi * 1e-3) / 1e9, 1),
+                 sequential_GBs_algorithmic=round(21 * blk / (t_seq * 1e-3) / 1e9, 1),
+                 speedup=round(t_seq / t_multi, 2))
+    del ins, acc
     del a, b
     torch.cuda.empty_cache()
     # config 5: vector(67108864, 1, 2, MPI_DOUBLE), 512 MiB payload, 1 GiB span
@@ -68,7 +90,7 @@ def main():
     vec = dict(config='vector(67108864,1,2,MPI_DOUBLE) SUM', ms=round(avg, 4),
                GBs_algorithmic=round(3 * cnt * 8 / (avg * 1e-3) / 1e9, 1),
                frac_of_8TBs=round(3 * cnt * 8 / (avg * 1e-3) / 8e12, 4))
-    print(json.dumps(dict(per_type=out, vector=vec, misaligned=misaligned,
+    print(json.dumps(dict(per_type=out, vector=vec, misaligned=misaligned, multi=multi,
                           build=redop.build_info())))
 
 
