@@ -72,7 +72,7 @@ def main():
     t_seq, _, _ = event_time_per_launch(seq, 10, s)
     multi = dict(case='7 x 64 MiB fp32 blocks folded into a 64 MiB result',
                  fused_ms=round(t_multi, 4), sequential_ms=round(t_seq, 4),
-                 fused_GBs=round(8 * blk / (t_multi * 1e-3) / 1e9, 1),
+                 fused_GBs=round(9 * blk / (t_multi * 1e-3) / 1e9, 1),
                  sequential_GBs_algorithmic=round(21 * blk / (t_seq * 1e-3) / 1e9, 1),
                  speedup=round(t_seq / t_multi, 2))
     del ins, acc
