@@ -179,7 +179,10 @@ const Entry *gpu_entry(uint32_t opi, uint32_t it)
 // ---------------------------------------------------------------- state
 std::atomic<long long> g_ftrue{1}, g_ffalse{0};
 std::atomic<int> g_block{256}, g_max_grid{0};
-std::atomic<bool> g_spin{true};     // MPIX_REDOP_SYNC=block selects hipStreamSynchronize
+// completion wait of the synchronous calls: 0 block (hipStreamSynchronize),
+// 1 spin on an event (default), 2 spin on a host word the stream writes
+// (hipStreamWriteValue32) -- MPIX_REDOP_SYNC=block|event|flag
+std::atomic<int> g_sync{1};
 std::atomic<bool> g_zero_copy{true}; // MPIX_REDOP_PINNED=stage stages pinned host memory too
 std::once_flag g_env_once;
 size_t g_stage_chunk = (size_t) 64 << 20;
@@ -194,7 +197,7 @@ void read_env()
     if (const char *s = getenv("MPIX_REDOP_MAXGRID"))
         g_max_grid = atoi(s) > 0 ? atoi(s) : 0;
     if (const char *s = getenv("MPIX_REDOP_SYNC"))
-        g_spin = strcmp(s, "block") != 0;
+        g_sync = strcmp(s, "block") == 0 ? 0 : (strcmp(s, "flag") == 0 ? 2 : 1);
     if (const char *s = getenv("MPIX_REDOP_PINNED"))
         g_zero_copy = strcmp(s, "stage") != 0;
     if (const char *s = getenv("MPIX_REDOP_STAGE_CHUNK")) {
@@ -211,6 +214,8 @@ struct DevState {
     bool init = false;
     hipStream_t s[2] = {nullptr, nullptr};
     hipEvent_t done = nullptr;          // completion marker for the spin wait
+    volatile uint32_t *flag = nullptr;  // pinned host word for MPIX_REDOP_SYNC=flag
+    uint32_t seq = 0;
     void *scratch = nullptr;    // 2 slots x (in chunk + inout chunk)
     size_t scratch_bytes = 0;
     int64_t *iov_tab = nullptr; // device copy of an iov segment table (offsets + prefix)
@@ -246,6 +251,11 @@ DevState *dev_state(int dev)
                 return nullptr;
         if (hipEventCreateWithFlags(&d.done, hipEventDisableTiming) != hipSuccess)
             return nullptr;
+        void *f = nullptr;
+        if (hipHostMalloc(&f, 64, hipHostMallocCoherent) == hipSuccess) {
+            d.flag = (volatile uint32_t *) f;
+            *d.flag = 0;
+        }
         d.init = true;
     }
     return &d;
@@ -264,9 +274,20 @@ Params params() { return Params{g_ftrue.load(), g_ffalse.load()}; }
 // wake-up latency per call, so by default completion is polled on an event.
 int wait_stream(DevState *d, hipStream_t s)
 {
-    if (!g_spin.load())
+    int mode = g_sync.load();
+    if (mode == 0)
         return hip_err(hipStreamSynchronize(s));
-    hipError_t e = hipEventRecord(d->done, s);
+    hipError_t e;
+    if (mode == 2 && d->flag) {
+        uint32_t seq = ++d->seq;
+        e = hipStreamWriteValue32(s, (void *) d->flag, seq, 0);
+        if (e != hipSuccess)
+            return hip_err(e);
+        while (__atomic_load_n(d->flag, __ATOMIC_ACQUIRE) != seq) {
+        }
+        return MPIX_REDOP_SUCCESS;
+    }
+    e = hipEventRecord(d->done, s);
     if (e != hipSuccess)
         return hip_err(e);
     while ((e = hipEventQuery(d->done)) == hipErrorNotReady) {
@@ -459,6 +480,8 @@ int MPIX_Redop_finalize(void)
                 (void) hipStreamDestroy(d.s[k]);
         if (d.done)
             (void) hipEventDestroy(d.done);
+        if (d.flag)
+            (void) hipHostFree((void *) d.flag);
         if (d.scratch)
             (void) hipFree(d.scratch);
         if (d.iov_tab)

@@ -5,6 +5,7 @@
 //        -Wl,-rpath,$PWD/mpich_amd -Wl,-rpath,/opt/rocm/lib -o /tmp/lat_probe
 #include <hip/hip_runtime_api.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <algorithm>
 #include <chrono>
 #include <functional>
@@ -55,6 +56,7 @@ int main()
         MPIX_Reduce_local_async(b, a, 1, MPIX_MPI_FLOAT, MPIX_SUM, s);
         hipStreamSynchronize(s);
     }));
+    printf("MPIX_Reduce_local count=1 (%s)   %8.0f ns\n", getenv("MPIX_REDOP_SYNC") ? getenv("MPIX_REDOP_SYNC") : "event", med_ns([&] { MPIX_Reduce_local(b, a, 1, MPIX_MPI_FLOAT, MPIX_SUM); }));
     printf("MPIX_Reduce_local count=1         %8.0f ns\n", med_ns([&] { MPIX_Reduce_local(b, a, 1, MPIX_MPI_FLOAT, MPIX_SUM); }));
     printf("MPIX_Reduce_local count=1M/4      %8.0f ns\n", med_ns([&] { MPIX_Reduce_local(b, a, 1 << 18, MPIX_MPI_FLOAT, MPIX_SUM); }, 500));
     printf("empty event record+spin           %8.0f ns\n", med_ns([&] {
