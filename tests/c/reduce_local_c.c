@@ -13,7 +13,7 @@
 
 #include "mpix_redop.h"
 
-#define MAX_BUF_ELEMENTS 65000
+#define NMAX 32768     /* largest count of the reference test's doubling sweep */
 
 static int check_2i(const int *io, int count, const char *what)
 {
@@ -30,19 +30,21 @@ static int check_2i(const int *io, int count, const char *what)
 int main(void)
 {
     int errs = 0;
-    int *in = malloc(sizeof(int) * MAX_BUF_ELEMENTS);
-    int *io = malloc(sizeof(int) * MAX_BUF_ELEMENTS);
+    int *in = malloc(sizeof(int) * NMAX);
+    int *io = malloc(sizeof(int) * NMAX);
     int *d_in, *d_io;
-    if (hipMalloc((void **) &d_in, sizeof(int) * MAX_BUF_ELEMENTS) != hipSuccess ||
-        hipMalloc((void **) &d_io, sizeof(int) * MAX_BUF_ELEMENTS) != hipSuccess) {
+    if (hipMalloc((void **) &d_in, sizeof(int) * NMAX) != hipSuccess ||
+        hipMalloc((void **) &d_io, sizeof(int) * NMAX) != hipSuccess) {
         fprintf(stderr, "hipMalloc failed\n");
         return 1;
     }
     if (MPIX_Redop_init() != MPIX_REDOP_SUCCESS)
         return 1;
-    for (int count = 0; count < MAX_BUF_ELEMENTS; count > 0 ? count *= 2 : count++) {
-        for (int i = 0; i < count; ++i)
-            in[i] = io[i] = i;
+    for (int count = 0; count <= NMAX; count = count ? 2 * count : 1) {
+        for (int k = 0; k < count; ++k) {
+            in[k] = k;
+            io[k] = k;
+        }
         /* host buffers */
         if (MPIX_Reduce_local(in, io, count, MPIX_MPI_INT, MPIX_SUM) != MPIX_REDOP_SUCCESS)
             ++errs;
