@@ -180,9 +180,10 @@ const Entry *gpu_entry(uint32_t opi, uint32_t it)
 std::atomic<long long> g_ftrue{1}, g_ffalse{0};
 std::atomic<int> g_block{256}, g_max_grid{0};
 // completion wait of the synchronous calls: 0 block (hipStreamSynchronize),
-// 1 spin on an event (default), 2 spin on a host word the stream writes
-// (hipStreamWriteValue32) -- MPIX_REDOP_SYNC=block|event|flag
-std::atomic<int> g_sync{1};
+// 1 spin on an event, 2 spin on a pinned host word the stream writes after the
+// kernel (hipStreamWriteValue32; default: 10.1 vs 13.2 us for a 1-element
+// call, profiles/r01_lat_probe.txt) -- MPIX_REDOP_SYNC=block|event|flag
+std::atomic<int> g_sync{2};
 std::atomic<bool> g_zero_copy{true}; // MPIX_REDOP_PINNED=stage stages pinned host memory too
 std::once_flag g_env_once;
 size_t g_stage_chunk = (size_t) 64 << 20;
@@ -270,8 +271,10 @@ LaunchCfg launch_cfg()
 Params params() { return Params{g_ftrue.load(), g_ffalse.load()}; }
 
 // Completion wait of the synchronous entry points.  MPI progress engines
-// poll; a blocking hipStreamSynchronize costs ~tens of microseconds of
-// wake-up latency per call, so by default completion is polled on an event.
+// poll; a blocking hipStreamSynchronize costs wake-up latency per call, and an
+// event query goes through the runtime's signal path, so by default the
+// stream writes a sequence number into pinned host memory after the kernel and
+// the caller spins on that word.
 int wait_stream(DevState *d, hipStream_t s)
 {
     int mode = g_sync.load();
