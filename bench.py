@@ -423,6 +423,13 @@ def rsb_bench(args, world, rank, dev):
                              busbw_GBs=round(busbytes / t / 1e9, 2),
                              per_link_GBs=round(link_bytes / t / 1e9, 2), links_active=links,
                              frac_of_xgmi_link=round(link_bytes / t / 1e9 / 153.0, 4))
+            if algo == 'recursive_halving':
+                # per-step breakdown, rank 0's stream
+                tl = []
+                dist.barrier()
+                fn(send, recv, recvcount, H.MPI_FLOAT, H.MPI_SUM, timer=tl, **kw)
+                torch.cuda.synchronize()
+                out[algo]['steps_rank0'] = tl[0].result()
 
         except Exception as e:          # keep the other algorithms' figures
             out[algo] = dict(error='%s: %s' % (type(e).__name__, e))
@@ -460,6 +467,9 @@ def allreduce_bench(args, world, rank, dev):
     for name, fn in (('mpich_schedule_hip_combine',
                       lambda: coll.allreduce(send, recv, n, H.MPI_FLOAT, H.MPI_SUM, extent=4,
                                              workspace=ws)),
+                     ('mpich_schedule_rd_allgather',
+                      lambda: coll.allreduce(send, recv, n, H.MPI_FLOAT, H.MPI_SUM, extent=4,
+                                             workspace=ws, allgather='recursive_doubling')),
                      ('rccl_all_reduce', lambda: (recv.copy_(send), dist.all_reduce(recv)))):
         fn()
         reps = max(3, min(10, args.steps))

@@ -104,14 +104,39 @@ def plan(rank, comm_size, recvcount):
     return dict(pof2=pof2, rem=rem, newrank=newrank, steps=steps)
 
 
+class _StepTimer:
+    """Per-step breakdown of a schedule: device events on
+    the current stream around each exchange (the stream waits for the
+    receive) and each combine; read with `.result()` after a synchronize."""
+
+    def __init__(self, on_device):
+        self.on = on_device
+        self.marks = []
+
+    def mark(self, tag):
+        if self.on:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            self.marks.append((tag, e))
+
+    def result(self):
+        out = []
+        for (t0, e0), (t1, e1) in zip(self.marks, self.marks[1:]):
+            out.append(dict(phase=t1, ms=round(e0.elapsed_time(e1), 4)))
+        return out
+
+
 def reduce_scatter_block(sendbuf, recvbuf, recvcount, datatype, op, group=None, combine=None,
-                         extent=None, workspace=None):
+                         extent=None, workspace=None, timer=None):
     """MPI_Reduce_scatter_block(sendbuf, recvbuf, recvcount, datatype, op, comm).
 
     sendbuf: tensor holding comm_size*recvcount elements (any torch dtype;
     it is addressed as bytes); recvbuf: tensor of recvcount elements.  The
     op must be commutative (all predefined ops are; :62-67).
     workspace: optional (tmp_results, tmp_recvbuf) byte tensors to reuse.
+    timer: optional list; a step timer is appended whose .result() is the
+    per-step breakdown [{'phase': 'exchange k' | 'combine k' | ..., 'ms': t}]
+    (device tensors only; read it after a torch.cuda.synchronize()).
     """
     rank = dist.get_rank(group)
     size = dist.get_world_size(group)
@@ -134,7 +159,10 @@ def reduce_scatter_block(sendbuf, recvbuf, recvcount, datatype, op, group=None, 
     else:
         tmp_results = torch.empty(total * extent, dtype=torch.uint8, device=sb.device)
         tmp_recvbuf = torch.empty_like(tmp_results)
+    tm = _StepTimer(timer is not None and sb.is_cuda)
+    tm.mark('start')
     tmp_results.copy_(sb[:total * extent])                          # :91-96
+    tm.mark('local copy')
 
     def el(off, cnt):
         return slice(off * extent, (off + cnt) * extent)
@@ -147,11 +175,14 @@ def reduce_scatter_block(sendbuf, recvbuf, recvcount, datatype, op, group=None, 
         else:
             _exchange(None, None, tmp_recvbuf, g2l(rank - 1), group)
             combine(tmp_recvbuf, tmp_results, total)
-    for dst, soff, scnt, roff, rcnt in p['steps']:                  # :164-229
+        tm.mark('prologue')
+    for k, (dst, soff, scnt, roff, rcnt) in enumerate(p['steps']):  # :164-229
         _exchange(tmp_results[el(soff, scnt)] if scnt else None, g2l(dst),
                   tmp_recvbuf[el(roff, rcnt)] if rcnt else None, g2l(dst), group)
+        tm.mark('exchange %d' % k)
         if rcnt:
             combine(tmp_recvbuf[el(roff, rcnt)], tmp_results[el(roff, rcnt)], rcnt)
+        tm.mark('combine %d' % k)
     if p['newrank'] != -1:                                          # :232-234
         rb.copy_(tmp_results[el(rank * recvcount, recvcount)])
     if rank < 2 * rem:                                              # :241-253
@@ -160,6 +191,9 @@ def reduce_scatter_block(sendbuf, recvbuf, recvcount, datatype, op, group=None, 
                       None, None, group)
         else:
             _exchange(None, None, rb, g2l(rank + 1), group)
+    tm.mark('epilogue')
+    if timer is not None:
+        timer.append(tm)
     return recvbuf
 
 
@@ -242,8 +276,20 @@ def reduce_scatter_block_auto(sendbuf, recvbuf, recvcount, datatype, op, group=N
     return ALGORITHMS[algo](sendbuf, recvbuf, recvcount, datatype, op, group=group, **kw)
 
 
+def _bitrev(r, pof2):
+    """Block a rank owns after the distance-doubling reduce-scatter of
+    MPIR_Allreduce_intra_reduce_scatter_allgather (:138-189): recv_idx ends at
+    the bit reversal of newrank over log2(pof2) bits."""
+    out, b = 0, pof2 >> 1
+    while b:
+        out = (out << 1) | (r & 1)
+        r >>= 1
+        b >>= 1
+    return out
+
+
 def allreduce(sendbuf, recvbuf, count, datatype, op, group=None, combine=None, extent=None,
-              workspace=None):
+              workspace=None, allgather='direct'):
     """MPI_Allreduce by reduce-scatter + allgather (Rabenseifner):
     MPIR_Allreduce_intra_reduce_scatter_allgather
     (src/mpi/coll/allreduce/allreduce_intra_reduce_scatter_allgather.c:41-277),
@@ -252,7 +298,15 @@ def allreduce(sendbuf, recvbuf, count, datatype, op, group=None, combine=None, e
     by the HIP kernel in the reference's order, so results are bit-identical
     to the reference schedule -- unlike ncclAllReduce (rccl.c:223), whose
     association is RCCL's own and whose op set stops at SUM/PROD/MIN/MAX.
-    sendbuf=None means MPI_IN_PLACE (recvbuf holds the input)."""
+    sendbuf=None means MPI_IN_PLACE (recvbuf holds the input).
+
+    allgather: 'recursive_doubling' is the reference's second phase
+    (:191-226, log2(P) sequential exchanges, one link busy per step);
+    'direct' (default) posts the same final blocks as ONE group of P-1 sends
+    and P-1 receives, so every xGMI link carries one block at once.  The
+    allgather only moves finished bytes, so both give the same bits."""
+    if allgather not in ('direct', 'recursive_doubling'):
+        raise ValueError('allgather must be direct or recursive_doubling')
     rank = dist.get_rank(group)
     size = dist.get_world_size(group)
     if extent is None:
@@ -313,6 +367,20 @@ def allreduce(sendbuf, recvbuf, count, datatype, op, group=None, combine=None, e
             if mask < pof2:
                 last_idx = recv_idx + pof2 // mask
         mask >>= 1
+        if allgather == 'direct':
+            mine = _bitrev(newrank, pof2)
+            ops = []
+            for q in range(pof2):
+                if q == newrank:
+                    continue
+                b = _bitrev(q, pof2)
+                ops.append(dist.P2POp(dist.isend, rb[el(disps[mine], cnts[mine])],
+                                      g2l(real(q)), group=group, tag=TAG))
+                ops.append(dist.P2POp(dist.irecv, rb[el(disps[b], cnts[b])], g2l(real(q)),
+                                      group=group, tag=TAG))
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+            mask = 0
         while mask > 0:                                             # :191-226
             newdst = newrank ^ mask
             if newrank < newdst:

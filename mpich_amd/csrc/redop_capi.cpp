@@ -187,6 +187,11 @@ std::atomic<int> g_sync{2};
 std::atomic<bool> g_zero_copy{true}; // MPIX_REDOP_PINNED=stage stages pinned host memory too
 std::once_flag g_env_once;
 size_t g_stage_chunk = (size_t) 64 << 20;
+// pageable operands up to this many bytes are copied (host memcpy) into a
+// pinned bounce buffer the kernel reads and writes over PCIe, instead of three
+// pageable hipMemcpy calls (each a driver-side bounce of its own);
+// MPIX_REDOP_BOUNCE_BYTES, 0 disables
+size_t g_bounce_bytes = (size_t) 64 << 10;
 
 void read_env()
 {
@@ -206,6 +211,11 @@ void read_env()
         if (c >= 4096)
             g_stage_chunk = (size_t) c;
     }
+    if (const char *s = getenv("MPIX_REDOP_BOUNCE_BYTES")) {
+        long long c = atoll(s);
+        if (c >= 0 && c <= (64ll << 20))
+            g_bounce_bytes = (size_t) c;
+    }
 }
 
 thread_local int t_last_error = 0;
@@ -221,6 +231,9 @@ struct DevState {
     size_t scratch_bytes = 0;
     int64_t *iov_tab = nullptr; // device copy of an iov segment table (offsets + prefix)
     size_t iov_cap = 0;         // entries per half
+    char *bounce = nullptr;     // pinned host: in half + inout half, bounce_half bytes each
+    char *bounce_dev = nullptr; // its device mapping
+    size_t bounce_half = 0;
 };
 thread_local DevState *t_dev = nullptr;   // array of kMaxDev, never freed implicitly
 
@@ -440,6 +453,48 @@ int staged(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext, 
     return rc ? rc : (rc2 ? rc2 : rc3);
 }
 
+// Small pageable operand(s): memcpy into the pinned bounce buffer, one
+// zero-copy kernel over it, memcpy the result back (a staged 1-element call
+// costs ~42 us in three pageable hipMemcpy calls).  Returns -1 when the bounce buffer cannot be had (caller stages).
+int bounced(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext, uint32_t op,
+            bool in_host, bool io_host, int dev)
+{
+    DevState *d = dev_state(dev);
+    if (!d)
+        return MPIX_REDOP_ERR_OTHER;
+    size_t bytes = (size_t) (count * ext);
+    if (!d->bounce) {
+        void *h = nullptr, *hd = nullptr;
+        size_t half = (g_bounce_bytes + 255) & ~(size_t) 255;
+        if (hipHostMalloc(&h, 2 * half, hipHostMallocDefault) != hipSuccess)
+            return -1;
+        if (hipHostGetDevicePointer(&hd, h, 0) != hipSuccess) {
+            (void) hipHostFree(h);
+            return -1;
+        }
+        d->bounce = (char *) h;
+        d->bounce_dev = (char *) hd;
+        d->bounce_half = half;
+    }
+    if (bytes > d->bounce_half)
+        return -1;
+    const void *kin = in;
+    void *kio = io;
+    if (in_host) {
+        memcpy(d->bounce, in, bytes);
+        kin = d->bounce_dev;
+    }
+    if (io_host) {
+        memcpy(d->bounce + d->bounce_half, io, bytes);
+        kio = d->bounce_dev + d->bounce_half;
+    }
+    int rc = enqueue(kin, kio, count, it, ext, op, d->s[0]);
+    int rc2 = wait_stream(d, d->s[0]);
+    if (rc == MPIX_REDOP_SUCCESS && rc2 == MPIX_REDOP_SUCCESS && io_host)
+        memcpy(io, d->bounce + d->bounce_half, bytes);
+    return rc ? rc : rc2;
+}
+
 struct DeviceGuard {
     int prev = -1;
     explicit DeviceGuard(int dev)
@@ -489,6 +544,8 @@ int MPIX_Redop_finalize(void)
             (void) hipFree(d.scratch);
         if (d.iov_tab)
             (void) hipFree(d.iov_tab);
+        if (d.bounce)
+            (void) hipHostFree(d.bounce);
         d = DevState();
     }
     delete[] t_dev;
@@ -534,6 +591,15 @@ int MPIX_Reduce_local(const void *inbuf, void *inoutbuf, MPIX_Aint count, MPIX_D
     bool io_stage = wio == Where::Pageable || (wio == Where::Pinned && !zc);
     int dev = wio == Where::Device ? dio : (win == Where::Device ? din : cur);
     DeviceGuard guard(dev);
+    bool pageable = win == Where::Pageable || wio == Where::Pageable;
+    if (pageable && (uint64_t) count * ext <= g_bounce_bytes) {
+        // only pageable operands bounce; pinned ones are used through their mapping
+        rc = bounced(win == Where::Pageable ? inbuf : pin,
+                     wio == Where::Pageable ? inoutbuf : (void *) pio, (uint64_t) count, it, ext,
+                     (uint32_t) op, win == Where::Pageable, wio == Where::Pageable, dev);
+        if (rc >= 0)
+            return set_err(rc);
+    }
     if (in_stage || io_stage)
         return set_err(staged(in_stage ? inbuf : pin, io_stage ? inoutbuf : (void *) pio,
                               (uint64_t) count, it, ext, (uint32_t) op, in_stage, io_stage, dev));

@@ -290,6 +290,41 @@ def test_host_buffers_are_staged(R, H, oracle):
     assert np.array_equal(pa.numpy(), exp)
 
 
+@pytest.mark.parametrize('nbytes', [1, 8, 4096, 65535, 65536, 65537, 1 << 18])
+@pytest.mark.parametrize('place', ['both_host', 'host_in', 'host_inout', 'pinned_in'])
+def test_small_pageable_bounce(R, H, oracle, nbytes, place):
+    """pageable operands up to MPIX_REDOP_BOUNCE_BYTES (64 KiB) go through the
+    pinned bounce buffer, larger ones through the staged path; results must
+    not depend on the route.  MAXLOC on MPI_2INT and int8 SUM as well."""
+    rng = np.random.default_rng(nbytes)
+    for dt, op, T in ((H.MPI_FLOAT, H.MPI_SUM, np.float32), (H.MPI_INT8_T, H.MPI_SUM, np.int8),
+                      (H.MPI_2INT, H.MPI_MAXLOC, np.int32)):
+        ext = R.datatype_extent(dt)
+        n = max(1, nbytes // ext)
+        w = n * ext // np.dtype(T).itemsize
+        if T == np.float32:
+            a = rng.uniform(-1, 1, w).astype(T)
+            b = rng.uniform(-1, 1, w).astype(T)
+        else:
+            a = rng.integers(-8, 8, w).astype(T)
+            b = rng.integers(-8, 8, w).astype(T)
+        exp = a.copy()
+        oracle.reduce_local(b.copy(), exp, n, dt, op)
+        got = a.copy()
+        if place == 'both_host':
+            assert R.MPI_Reduce_local(b, got, n, dt, op) == 0
+        elif place == 'host_in':
+            dgot = dev(got)
+            assert R.MPI_Reduce_local(b, dgot, n, dt, op) == 0
+            got = host(dgot).view(T)
+        elif place == 'host_inout':
+            assert R.MPI_Reduce_local(dev(b), got, n, dt, op) == 0
+        else:
+            pb = torch.from_numpy(b.copy()).pin_memory()
+            assert R.MPI_Reduce_local(pb, got, n, dt, op) == 0
+        assert np.array_equal(got.view(np.uint8), exp.view(np.uint8)), (dt, place)
+
+
 def test_async_on_torch_stream(R, H, oracle):
     rng = np.random.default_rng(11)
     n = 1 << 22

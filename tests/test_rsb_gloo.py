@@ -46,7 +46,10 @@ def _worker(rank, world, port, outdir, recvcount, mode, algo='recursive_halving'
         assert orc.reduce_local(b, a, count, dt, MPI_SUM) == 0
 
     if algo == 'recursive_halving':
-        coll.reduce_scatter_block(sendt, recv, recvcount, dt, MPI_SUM, combine=combine, extent=4)
+        tl = []     # the per-step timer is inert on host tensors
+        coll.reduce_scatter_block(sendt, recv, recvcount, dt, MPI_SUM, combine=combine, extent=4,
+                                  timer=tl)
+        assert len(tl) == 1 and tl[0].result() == []
     else:
         coll.reduce_scatter_block_pairwise(sendt, recv, recvcount, dt, MPI_SUM, combine=combine,
                                            extent=4, concurrent=(algo == 'pairwise'))
@@ -129,8 +132,13 @@ def _ar_worker(rank, world, port, outdir, count, algo='reduce_scatter_allgather'
         def combine(inb, inoutb, n):
             assert orc.reduce_local(inb.numpy(), inoutb.numpy(), n, dt, op) == 0
         return combine
-    fn = coll.allreduce if algo == 'reduce_scatter_allgather' else \
-        coll.allreduce_recursive_doubling
+    if algo == 'recursive_doubling':
+        fn = coll.allreduce_recursive_doubling
+    else:   # second phase: one group of direct sends, or the reference's exchanges
+        ag = 'recursive_doubling' if algo == 'rsag_rd_allgather' else 'direct'
+
+        def fn(*a, **k):
+            return coll.allreduce(*a, allgather=ag, **k)
     fn(torch.from_numpy(send.copy()), recv, count, MPI_FLOAT, MPI_SUM,
        combine=mk_combine(MPI_FLOAT, MPI_SUM), extent=4)
     np.save(os.path.join(outdir, 'send%d.npy' % rank), send)
@@ -139,7 +147,7 @@ def _ar_worker(rank, world, port, outdir, count, algo='reduce_scatter_allgather'
     bad = []
     for c in gu.load_cases():
         if c['nranks'] != world or not c['name'].startswith('allred ') or \
-                (algo == 'reduce_scatter_allgather' and
+                (algo != 'recursive_doubling' and
                  c['count'] < (1 << (world.bit_length() - 1))):
             continue
         ext = len(c['expected']) // c['count']
@@ -154,10 +162,12 @@ def _ar_worker(rank, world, port, outdir, count, algo='reduce_scatter_allgather'
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('algo', ['reduce_scatter_allgather', 'recursive_doubling'])
-@pytest.mark.parametrize('world', [2, 3, 4, 7])
+@pytest.mark.parametrize('algo', ['reduce_scatter_allgather', 'rsag_rd_allgather',
+                                  'recursive_doubling'])
+@pytest.mark.parametrize('world', [2, 3, 4, 7, 8])
 def test_allreduce_gloo(oracle, tmp_path, world, algo):
-    """Rabenseifner allreduce over gloo: bit-identical on every rank to the
+    """Rabenseifner allreduce over gloo (direct or the reference's
+    recursive-doubling allgather): bit-identical on every rank to the
     oracle's simulation of the reference schedule, and all allred.c KATs
     generated for this world size pass end to end."""
     count = 1037
@@ -165,7 +175,9 @@ def test_allreduce_gloo(oracle, tmp_path, world, algo):
              join=True)
     sends = [np.load(tmp_path / ('send%d.npy' % r)) for r in range(world)]
     exp = oracle.allreduce_rabenseifner([s.view(np.uint8) for s in sends], count, 0x4c00040a,
-                                        0x58000003, algorithm=algo)
+                                        0x58000003,
+                                        algorithm='recursive_doubling' if algo == 'recursive_doubling'
+                                        else 'reduce_scatter_allgather')
     for r in range(world):
         assert np.load(tmp_path / ('recv%d.npy' % r)).tobytes() == exp[r].tobytes(), r
         assert open(tmp_path / ('bad%d.txt' % r)).read() == '', r

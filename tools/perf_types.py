@@ -46,14 +46,32 @@ def main():
                 lambda: redop.check(redop.reduce_local_async(b, a, n, dt, op, s)), 10, s)
             out.append(dict(type=tn, op=on, bytes=n * ext, ms=round(avg, 4),
                             GBs=round(3 * n * ext / (avg * 1e-3) / 1e9, 1)))
-    # relatively misaligned operands (in at +4 bytes): the element-wise kernel
-    n = nbytes // 4 - 4
-    redop.check(redop.reduce_local_async(b.data_ptr() + 4, a, n, H.MPI_FLOAT, H.MPI_SUM, s))
-    avg, med, mn = event_time_per_launch(
-        lambda: redop.check(redop.reduce_local_async(b.data_ptr() + 4, a, n, H.MPI_FLOAT,
-                                                     H.MPI_SUM, s)), 10, s)
-    misaligned = dict(case='fp32 SUM, in at +4 B relative to inout (k_elem path)',
-                      ms=round(avg, 4), GBs=round(12 * n / (avg * 1e-3) / 1e9, 1))
+    # relatively misaligned operands (in at +4 bytes: packet kernel with
+    # unaligned loads of `in`, default cache policy for them), next to the
+    # aligned launch, both at 256 MiB and at 1 GiB per operand -- at 256 MiB
+    # the default-policy `in` stream can stay in the 256 MB MALL across
+    # back-to-back launches of the same buffers, at 1 GiB it cannot
+    misaligned = []
+    for mb in (nbytes, 1 << 30):
+        if mb == nbytes:
+            x, y = a, b
+        else:
+            x = torch.empty(mb, dtype=torch.uint8, device=dev)
+            y = torch.empty(mb, dtype=torch.uint8, device=dev)
+            x.view(torch.int8).random_(0, 3)
+            y.view(torch.int8).random_(0, 3)
+        n = mb // 4 - 4
+        row = dict(bytes=mb)
+        for tag, shift in (('aligned', 0), ('in_plus_4B', 4)):
+            redop.check(redop.reduce_local_async(y.data_ptr() + shift, x, n, H.MPI_FLOAT,
+                                                 H.MPI_SUM, s))
+            avg, med, mn = event_time_per_launch(
+                lambda: redop.check(redop.reduce_local_async(y.data_ptr() + shift, x, n,
+                                                             H.MPI_FLOAT, H.MPI_SUM, s)), 10, s)
+            row[tag] = dict(ms=round(avg, 4), GBs=round(12 * n / (avg * 1e-3) / 1e9, 1))
+        misaligned.append(row)
+        if mb != nbytes:
+            del x, y
     # fused multi-input combine (pairwise reduce-scatter epilogue): 7 received
     # 64 MiB blocks folded into the result in one pass vs 7 sequential calls
     blk = 64 << 20
