@@ -191,7 +191,7 @@ size_t g_stage_chunk = (size_t) 64 << 20;
 // pinned bounce buffer the kernel reads and writes over PCIe, instead of three
 // pageable hipMemcpy calls (each a driver-side bounce of its own);
 // MPIX_REDOP_BOUNCE_BYTES, 0 disables
-size_t g_bounce_bytes = (size_t) 64 << 10;
+size_t g_bounce_bytes = (size_t) 1 << 20;
 
 void read_env()
 {
@@ -400,6 +400,18 @@ int enqueue(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext,
     return hip_err(e->contig(in, io, count, params(), launch_cfg(), s));
 }
 
+// Synchronous combine of device-accessible operands on the library stream.
+// (A one-workgroup kernel that writes the completion word itself was
+// measured no faster than the stream write -- 10.9 vs 9.9 us per 1-element
+// call, profiles/r01_latency_small_kernel.json -- the floor is the dispatch.)
+int run_sync(DevState *d, const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext,
+             uint32_t op)
+{
+    int rc = enqueue(in, io, count, it, ext, op, d->s[0]);
+    int rc2 = wait_stream(d, d->s[0]);
+    return rc ? rc : rc2;
+}
+
 // Host-resident operand(s): stream them through device scratch in chunks,
 // alternating two streams so chunk k+1's copies overlap chunk k's kernel.
 int staged(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext, uint32_t op,
@@ -488,11 +500,10 @@ int bounced(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext,
         memcpy(d->bounce + d->bounce_half, io, bytes);
         kio = d->bounce_dev + d->bounce_half;
     }
-    int rc = enqueue(kin, kio, count, it, ext, op, d->s[0]);
-    int rc2 = wait_stream(d, d->s[0]);
-    if (rc == MPIX_REDOP_SUCCESS && rc2 == MPIX_REDOP_SUCCESS && io_host)
+    int rc = run_sync(d, kin, kio, count, it, ext, op);
+    if (rc == MPIX_REDOP_SUCCESS && io_host)
         memcpy(io, d->bounce + d->bounce_half, bytes);
-    return rc ? rc : rc2;
+    return rc;
 }
 
 struct DeviceGuard {
@@ -606,9 +617,7 @@ int MPIX_Reduce_local(const void *inbuf, void *inoutbuf, MPIX_Aint count, MPIX_D
     DevState *d = dev_state(dev);
     if (!d)
         return set_err(MPIX_REDOP_ERR_OTHER);
-    rc = enqueue(pin, (void *) pio, (uint64_t) count, it, ext, (uint32_t) op, d->s[0]);
-    int rc2 = wait_stream(d, d->s[0]);
-    return set_err(rc ? rc : rc2);
+    return set_err(run_sync(d, pin, (void *) pio, (uint64_t) count, it, ext, (uint32_t) op));
 }
 
 int MPIX_Reduce_local_vector_async(const void *inbuf, void *inoutbuf, MPIX_Aint count,

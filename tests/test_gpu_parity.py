@@ -229,6 +229,48 @@ def test_golden_on_gpu(R, case):
     assert gu.mismatches(case, acc) == 0
 
 
+@pytest.mark.parametrize('case', gu.load_cases(), ids=lambda c: c['id'] + ' ' + c['name'])
+def test_golden_on_gpu_async(R, case):
+    """the same golden cases through the stream-ordered entry (caller's
+    stream, no library wait) -- same bits as the synchronous calls."""
+    if not R.is_supported(case['op'], case['datatype']):
+        return
+    s = torch.cuda.current_stream()
+
+    def fn(inb, inoutb, count, dt, op):
+        di, dio = dev(inb), dev(inoutb)
+        rc = R.reduce_local_async(di, dio, count, dt, op, s)
+        inoutb[:] = host(dio)
+        return rc
+    rc, acc = gu.fold(case, fn)
+    assert rc == 0
+    assert gu.mismatches(case, acc) == 0
+
+
+@pytest.mark.parametrize('tname', ['MPI_INT8_T', 'MPIX_C_FLOAT16', 'MPI_FLOAT', 'MPI_DOUBLE',
+                                   'MPI_C_DOUBLE_COMPLEX', 'MPI_2INT', 'MPI_DOUBLE_INT'])
+@pytest.mark.parametrize('delta', [-1, 0, 1])
+@pytest.mark.parametrize('offs', [(0, 0), (0, 2), (6, 0)])
+def test_small_kernel_boundary(R, H, oracle, tname, delta, offs):
+    """counts around 16 KiB per operand for 1- to 16-byte elements, with
+    byte-offset operands (head/tail, unaligned-load and element paths)."""
+    dt = getattr(H, tname)
+    ext = R.datatype_extent(dt)
+    op = H.MPI_MAXLOC if 'INT' in tname and tname.startswith('MPI_2') or tname == 'MPI_DOUBLE_INT' \
+        else H.MPI_SUM
+    count = (16384 // ext) + delta
+    nb = count * ext + 16
+    rng = np.random.default_rng(count * 7 + offs[1])
+    a = rng.integers(0, 4, nb).astype(np.uint8)
+    b = rng.integers(0, 4, nb).astype(np.uint8)
+    da, db = dev(a), dev(b)
+    oa, ob = offs
+    assert R.MPI_Reduce_local(db.data_ptr() + ob, da.data_ptr() + oa, count, dt, op) == 0
+    exp = a.copy()
+    oracle.reduce_local(b[ob:ob + count * ext].copy(), exp[oa:], count, dt, op)
+    assert np.array_equal(host(da), exp)
+
+
 @pytest.mark.parametrize('count', [0, 1, 2, 3, 4, 5, 15, 16, 17, 63, 64, 65, 1023, 4099,
                                    (1 << 20) + 3])
 @pytest.mark.parametrize('offs', [(0, 0), (4, 4), (8, 8), (12, 12), (0, 4), (4, 0), (8, 12)])
@@ -290,10 +332,11 @@ def test_host_buffers_are_staged(R, H, oracle):
     assert np.array_equal(pa.numpy(), exp)
 
 
-@pytest.mark.parametrize('nbytes', [1, 8, 4096, 65535, 65536, 65537, 1 << 18])
+@pytest.mark.parametrize('nbytes', [1, 8, 4096, 65536, (1 << 20) - 8, 1 << 20, (1 << 20) + 8,
+                                    1 << 21])
 @pytest.mark.parametrize('place', ['both_host', 'host_in', 'host_inout', 'pinned_in'])
 def test_small_pageable_bounce(R, H, oracle, nbytes, place):
-    """pageable operands up to MPIX_REDOP_BOUNCE_BYTES (64 KiB) go through the
+    """pageable operands up to MPIX_REDOP_BOUNCE_BYTES (1 MiB) go through the
     pinned bounce buffer, larger ones through the staged path; results must
     not depend on the route.  MAXLOC on MPI_2INT and int8 SUM as well."""
     rng = np.random.default_rng(nbytes)

@@ -31,7 +31,12 @@ def main():
     dev = torch.device('cuda', 0)
     out = dict(device=[], pinned=[], pageable=[], chunk=os.environ.get('MPIX_REDOP_STAGE_CHUNK'),
                sync=os.environ.get('MPIX_REDOP_SYNC', 'spin'))
-    for n in (1, 16, 256, 4096, 65536, 1 << 20, 1 << 24, 1 << 28):
+    counts = os.environ.get('PERF_COUNTS')
+    counts = [int(x) for x in counts.split(',')] if counts else \
+        (1, 16, 256, 4096, 4097, 16384, 65536, 262144, 1 << 20, 1 << 24, 1 << 28)
+    out.update(small_bytes=os.environ.get('MPIX_REDOP_SMALL_BYTES'),
+               bounce_bytes=os.environ.get('MPIX_REDOP_BOUNCE_BYTES'))
+    for n in counts:
         a = torch.zeros(n, dtype=torch.float32, device=dev)
         b = torch.zeros(n, dtype=torch.float32, device=dev)
         torch.cuda.synchronize()
