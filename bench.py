@@ -11,14 +11,16 @@ write inout) / wall time.
 N > 1 (torchrun, one rank per GPU): every rank reduces its own 1 GiB shard
 (no data-path collective: the path is element-wise), value = all ranks'
 bytes / max-over-ranks time ("weak" scaling).  Those runs also time the
-recursive-halving MPI_Reduce_scatter_block (BASELINE config 4) as a
-secondary figure.
+MPI_Reduce_scatter_block schedules (BASELINE config 4: recursive halving
+with a per-step breakdown, pairwise, fused IPC pull) and the allreduce as
+secondary figures.
 
 Also reported (not `value`): kernel-only rate from HIP events on the launch
 stream -> `roofline`; a measured STREAM triad on the same GPU; the
-host-resident end-to-end rate (pinned H2D + kernel + D2H); and the
-`cpu_baseline` -- the oracle (clean-room C restatement of MPICH's op loop)
-timed on this host's cores on BASELINE config 1 (16 MiB fp32 SUM).
+host-resident end-to-end rate (pinned host operands, the kernel reads and
+writes them over PCIe); and the `cpu_baseline` -- the oracle (clean-room C
+restatement of MPICH's op loop) timed on this host's cores on a bounded
+sample of the same 1 GiB workload, plus BASELINE config 1 (16 MiB) beside it.
 """
 import argparse
 import ctypes
@@ -289,7 +291,7 @@ def main():
 
     if args.sweep and rank == 0:
         sweep = []
-        for mib in (16, 64, 256, 1024):
+        for mib in (16, 32, 64, 128, 256, 512, 1024):
             m = mib * (1 << 20) // 4
             if m > n:
                 break

@@ -52,6 +52,40 @@ void add_all(std::vector<Var> &v, int block, int maxgrid)
     add<U, true, true>(v, block, maxgrid);
 }
 
+// XCD-aware variant: with round-robin placement, block b runs on XCD b % 8;
+// remap so each XCD walks one contiguous eighth of the buffer.
+template <int U>
+__global__ void __launch_bounds__(1024) k_xcd(const float *__restrict__ in, float *__restrict__ io,
+                                              uint64_t npk)
+{
+    const v4u *vin = reinterpret_cast<const v4u *>(in);
+    v4u *vio = reinterpret_cast<v4u *>(io);
+    const uint64_t nt = blockDim.x, G = gridDim.x;
+    const uint64_t b = blockIdx.x;
+    const uint64_t per = G / 8;
+    const uint64_t lb = (b < per * 8) ? (b % 8) * per + b / 8 : b;
+    uint64_t i = lb * nt * U + threadIdx.x;
+    v4u a[U], c[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        if (i + u * nt < npk) {
+            a[u] = __builtin_nontemporal_load(vio + i + u * nt);
+            c[u] = __builtin_nontemporal_load(vin + i + u * nt);
+        }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        if (i + u * nt < npk)
+            __builtin_nontemporal_store(combine16<C>(a[u], c[u], Params{1, 0}), vio + i + u * nt);
+}
+
+template <int U>
+void launch_x(const float *in, float *io, uint64_t n, int block, int, hipStream_t s)
+{
+    uint64_t npk = n / 4;
+    unsigned grid = grid_for((uint64_t) block * U, npk, 0);
+    hipLaunchKernelGGL((k_xcd<U>), dim3(grid), dim3(block), 0, s, in, io, npk);
+}
+
 __global__ void fill(float *p, uint64_t n, uint32_t seed)
 {
     for (uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; i < n;
@@ -75,7 +109,17 @@ int main(int argc, char **argv)
     CK(hipDeviceSynchronize());
     bool focus = argc > 4 && std::string(argv[4]) == "focus";
     std::vector<Var> v;
-    if (focus) {        // NT/NT, one tile per block: the winners of the full sweep
+    if (argc > 4 && std::string(argv[4]) == "xcd") {   // shipped geometry vs XCD remap
+        for (int block : {256, 512}) {
+            add<4, true, true>(v, block, 0);
+            add<1, true, true>(v, block, 0);
+            char nm[64];
+            snprintf(nm, sizeof nm, "XCD-remap U=4 block=%d", block);
+            v.push_back(Var{nm, &launch_x<4>, block, 0, {}});
+            snprintf(nm, sizeof nm, "XCD-remap U=1 block=%d", block);
+            v.push_back(Var{nm, &launch_x<1>, block, 0, {}});
+        }
+    } else if (focus) { // NT/NT, one tile per block: the winners of the full sweep
         for (int block : {256, 512, 1024}) {
             add<1, true, true>(v, block, 0);
             add<2, true, true>(v, block, 0);

@@ -3,6 +3,9 @@
 // V0 = product k_vector1 (8-B target loads at 16-B stride);
 // V1<U,NT> = 16-B target packets (payload + gap) loaded whole, U per lane,
 //            8-B payload stores (gaps never written);
+// V2<NTS>  = two adjacent pairs per lane: 32 B of target (2 x 16-B loads),
+//            one 16-B source packet (non-temporal if NTS), two 8-B stores;
+// V3<B>    = V1 U=1 with the source read non-temporally, block size B;
 // Interleaved rounds in one process; median GB/s (algorithmic 3 x 512 MiB).
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -54,6 +57,33 @@ __global__ void __launch_bounds__(256) k_v1(const double *__restrict__ in, doubl
     }
 }
 
+template <bool NTS>
+__global__ void __launch_bounds__(256) k_v2(const double *__restrict__ in, double *__restrict__ io,
+                                            uint64_t n2)
+{
+    uint64_t i = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x;     // pair-of-pairs index
+    if (i >= n2)
+        return;
+    const d2 *t = reinterpret_cast<const d2 *>(io) + 2 * i;
+    d2 a = t[0], b = t[1];
+    d2 x = NTS ? __builtin_nontemporal_load(reinterpret_cast<const d2 *>(in) + i)
+               : reinterpret_cast<const d2 *>(in)[i];
+    io[4 * i] = a.x + x.x;
+    io[4 * i + 2] = b.x + x.y;
+}
+
+template <int B>
+__global__ void __launch_bounds__(1024) k_v3(const double *__restrict__ in, double *__restrict__ io,
+                                             uint64_t n)
+{
+    uint64_t k = (uint64_t) blockIdx.x * B + threadIdx.x;
+    if (k >= n)
+        return;
+    d2 t = reinterpret_cast<const d2 *>(io)[k];
+    double x = __builtin_nontemporal_load(in + k);
+    io[2 * k] = t.x + x;
+}
+
 struct Var {
     std::string name;
     void (*launch)(const double *, double *, uint64_t, hipStream_t);
@@ -73,6 +103,20 @@ void v1(const double *in, double *io, uint64_t n, hipStream_t s)
     hipLaunchKernelGGL((k_v1<U, NT>), dim3(grid), dim3(256), 0, s, in, io, n);
 }
 
+template <bool NTS>
+void v2(const double *in, double *io, uint64_t n, hipStream_t s)
+{
+    uint64_t n2 = n / 2;
+    hipLaunchKernelGGL((k_v2<NTS>), dim3((unsigned) ((n2 + 255) / 256)), dim3(256), 0, s, in, io,
+                       n2);
+}
+
+template <int B>
+void v3(const double *in, double *io, uint64_t n, hipStream_t s)
+{
+    hipLaunchKernelGGL((k_v3<B>), dim3((unsigned) ((n + B - 1) / B)), dim3(B), 0, s, in, io, n);
+}
+
 int main()
 {
     uint64_t n = 67108864;
@@ -85,7 +129,10 @@ int main()
                           {"V1 U=1 nt=0", v1<1, false>, {}}, {"V1 U=1 nt=1", v1<1, true>, {}},
                           {"V1 U=2 nt=0", v1<2, false>, {}}, {"V1 U=2 nt=1", v1<2, true>, {}},
                           {"V1 U=4 nt=0", v1<4, false>, {}}, {"V1 U=4 nt=1", v1<4, true>, {}},
-                          {"V1 U=8 nt=1", v1<8, true>, {}}};
+                          {"V1 U=8 nt=1", v1<8, true>, {}},
+                          {"V2 nts=0", v2<false>, {}}, {"V2 nts=1", v2<true>, {}},
+                          {"V3 block=256", v3<256>, {}}, {"V3 block=512", v3<512>, {}},
+                          {"V3 block=1024", v3<1024>, {}}};
     hipStream_t s;
     CK(hipStreamCreate(&s));
     hipEvent_t e0, e1;
