@@ -454,6 +454,38 @@ def test_vector_target(R, H, oracle, blocklen, stride):
     assert np.array_equal(host(dd).view(np.float64), exp)
 
 
+def test_acc_pairtype_on_gpu(R, H):
+    """test/mpi/rma/acc_pairtype.c's check (MAXLOC of {1.0, 1} pairs into a
+    zeroed vector(10, 3, 5) target; MPI_DOUBLE_INT for the x87 pair)."""
+    from tests.test_oracle_golden import _acc_pairtype_case
+    src, tgt, exp = _acc_pairtype_case()
+    dt = dev(tgt.view(np.uint8))
+    assert R.reduce_local_vector(dev(src.view(np.uint8)), dt, 10, 3, 5, H.MPI_DOUBLE_INT,
+                                 H.MPI_MAXLOC, sync=True) == 0
+    assert host(dt).tobytes() == exp.view(np.uint8).tobytes()
+
+
+@pytest.mark.parametrize('tname', ['MPI_2INT', 'MPI_FLOAT_INT', 'MPI_DOUBLE_INT', 'MPI_LONG_INT',
+                                   'MPI_SHORT_INT', 'MPI_2DOUBLE_PRECISION'])
+@pytest.mark.parametrize('blocklen,stride', [(1, 2), (3, 5)])
+def test_vector_target_pairs(R, H, oracle, tname, blocklen, stride):
+    """MAXLOC / MINLOC through the vector target for every pair layout
+    (ties and random padding included) against the oracle."""
+    dt = getattr(H, tname)
+    ext = R.datatype_extent(dt)
+    rng = np.random.default_rng(ext * 31 + stride)
+    count = 20011
+    for op in (H.MPI_MAXLOC, H.MPI_MINLOC):
+        src = rng.integers(0, 3, count * blocklen * ext).astype(np.uint8)
+        dst = rng.integers(0, 3, count * stride * ext).astype(np.uint8)
+        dd = dev(dst)
+        assert R.reduce_local_vector(dev(src), dd, count, blocklen, stride, dt, op,
+                                     sync=True) == 0
+        exp = dst.copy()
+        assert oracle.reduce_local_vector(src, exp, count, blocklen, stride, dt, op) == 0
+        assert np.array_equal(host(dd), exp), (tname, op)
+
+
 def test_full_1gib_fp32_sum(R, H, oracle):
     """BASELINE config 2 at its largest size: 1 GiB per operand, checked
     element-for-element against the oracle (8 host threads)."""
