@@ -1,0 +1,131 @@
+/*
+ * mpix_coll.h -- C-ABI of the reduce-scatter / allreduce schedules that feed
+ * the MI355X local reduction (libmpix_coll.so, built from mpich_amd/csrc/).
+ *
+ * These are host-side C restatements of MPICH's collective schedules whose
+ * every combine step is MPIR_Reduce_local -- here MPIX_Reduce_local_async
+ * (include/mpix_redop.h) on the HIP stream the collective is enqueued on --
+ * and whose point-to-point steps go through a transport:
+ *
+ *   MPIX_Reduce_scatter_block  <- MPIR_Reduce_scatter_block_intra_recursive_halving
+ *                                  src/mpi/coll/reduce_scatter_block/
+ *                                  reduce_scatter_block_intra_recursive_halving.c:38-260
+ *                                 and ..._intra_pairwise.c:42-104 (MPICH's large-message
+ *                                  choice, maint/tuning/coll/mpir/generic.json:316-341)
+ *   MPIX_Allreduce             <- MPIR_Allreduce_intra_reduce_scatter_allgather
+ *                                  src/mpi/coll/allreduce/
+ *                                  allreduce_intra_reduce_scatter_allgather.c:41-277
+ *                                 and MPIR_Allreduce_intra_recursive_doubling
+ *                                  allreduce_intra_recursive_doubling.c:24-150
+ *   MPIX_Comm_create_ccl       <- MPIR_RCCLcomm_init  src/util/ccl/rccl.c:21-52
+ *                                 (ncclCommInitRank with a unique id the caller
+ *                                  broadcasts, as rccl.c:36 does with MPIR_Bcast)
+ *   MPIX_Comm_free             <- MPIR_RCCLcomm_free  src/util/ccl/rccl.c:237
+ *
+ * Same pairing, same operand order (MPIR_Reduce_local(tmp_recvbuf,
+ * tmp_results)), same association as the reference schedules, hence the same
+ * bits.  Transports:
+ *   - RCCL (one process per GPU; every exchange step is one
+ *     ncclGroupStart / ncclSend+ncclRecv / ncclGroupEnd on the stream, over
+ *     xGMI between MI355X GPUs);
+ *   - local: the ranks are threads of ONE process (one device each, or all on
+ *     one device), an exchange is a stream-ordered device-to-device copy with
+ *     event hand-offs -- the shared-memory analogue, also how the schedules
+ *     are tested with several ranks on a single GPU;
+ *   - host-local: the same with host memory and host memcpy (schedule tests on
+ *     a machine without a GPU; needs a combine installed with
+ *     MPIX_Comm_set_combine, since the product has no CPU compute path);
+ *   - custom: a caller-supplied exchange function.
+ *
+ * Blocking entry points wait for their stream before returning; the _async
+ * forms only enqueue (local and custom transports may block the host inside an
+ * exchange until the peer rank reaches the matching step).  Return values are
+ * the MPI error classes of mpix_redop.h.
+ */
+#ifndef MPIX_COLL_H_INCLUDED
+#define MPIX_COLL_H_INCLUDED
+
+#include <stddef.h>
+
+#include "mpix_redop.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct MPIX_Comm_s *MPIX_Comm;
+
+/* one point-to-point operation of an exchange step */
+typedef struct {
+    int peer;           /* rank in the communicator */
+    int is_recv;        /* 0 send, 1 receive */
+    void *buf;
+    size_t bytes;
+} MPIX_P2p_op;
+
+/* transport hook: post all `nops` operations as one group; stream-ordered on
+ * `stream` (ignored by host transports).  0 on success. */
+typedef int (*MPIX_Exchange_fn)(void *ctx, int rank, const MPIX_P2p_op *ops, int nops,
+                                void *stream);
+/* combine hook, MPIX_Reduce_local_async's signature */
+typedef int (*MPIX_Combine_fn)(const void *inbuf, void *inoutbuf, MPIX_Aint count,
+                               MPIX_Datatype datatype, MPIX_Op op, void *stream);
+
+/* ---- communicators ---- */
+#define MPIX_CCL_UNIQUE_ID_BYTES 128
+int MPIX_Ccl_get_unique_id(void *id_out);
+/* collective over `size` processes; call with the HIP device already set */
+int MPIX_Comm_create_ccl(int rank, int size, const void *id, MPIX_Comm *comm);
+/* `size` in-process ranks; devices[r] is rank r's HIP device, or devices ==
+ * NULL for the host-memory transport.  comms[r] is rank r's handle; each rank
+ * must be driven by its own thread. */
+int MPIX_Comm_create_local(int size, const int *devices, MPIX_Comm *comms);
+int MPIX_Comm_create_custom(int rank, int size, MPIX_Exchange_fn fn, void *ctx, int host_memory,
+                            MPIX_Comm *comm);
+/* replace the combine (NULL restores MPIX_Reduce_local_async) */
+int MPIX_Comm_set_combine(MPIX_Comm comm, MPIX_Combine_fn fn);
+int MPIX_Comm_rank(MPIX_Comm comm, int *rank);
+int MPIX_Comm_size(MPIX_Comm comm, int *size);
+/* frees the handle; for local communicators, after every rank has freed its
+ * handle the shared mailbox goes too */
+int MPIX_Comm_free(MPIX_Comm comm);
+
+/* ---- MPI_Reduce_scatter_block(sendbuf, recvbuf, recvcount, datatype, op) ----
+ * sendbuf holds size*recvcount elements; recvbuf recvcount.  workspace: NULL
+ * (the communicator keeps a grow-only scratch) or at least
+ * MPIX_Reduce_scatter_block_workspace() bytes of the buffers' memory kind. */
+#define MPIX_RSB_AUTO               0   /* generic.json: recursive halving < 512 KiB, else pairwise */
+#define MPIX_RSB_RECURSIVE_HALVING  1
+#define MPIX_RSB_PAIRWISE           2   /* the P-1 exchanges in ONE group + one multi-input combine */
+#define MPIX_RSB_PAIRWISE_SEQUENTIAL 3  /* the reference's loop: P-1 sendrecv + combine steps */
+size_t MPIX_Reduce_scatter_block_workspace(MPIX_Aint recvcount, MPIX_Datatype datatype,
+                                           MPIX_Comm comm, int algorithm);
+int MPIX_Reduce_scatter_block(const void *sendbuf, void *recvbuf, MPIX_Aint recvcount,
+                              MPIX_Datatype datatype, MPIX_Op op, MPIX_Comm comm, int algorithm,
+                              void *workspace, size_t workspace_bytes);
+int MPIX_Reduce_scatter_block_async(const void *sendbuf, void *recvbuf, MPIX_Aint recvcount,
+                                    MPIX_Datatype datatype, MPIX_Op op, MPIX_Comm comm,
+                                    int algorithm, void *workspace, size_t workspace_bytes,
+                                    void *stream);
+
+/* ---- MPI_Allreduce(sendbuf, recvbuf, count, datatype, op) ----
+ * sendbuf NULL = MPI_IN_PLACE (recvbuf holds the input). */
+#define MPIX_ALLREDUCE_AUTO                 0   /* reduce-scatter+allgather if count >= pof2 */
+#define MPIX_ALLREDUCE_RECURSIVE_DOUBLING   1
+#define MPIX_ALLREDUCE_REDUCE_SCATTER_ALLGATHER 2  /* allgather as ONE group of direct exchanges */
+#define MPIX_ALLREDUCE_RSAG_RD_ALLGATHER    3   /* the reference's log2(P) allgather steps */
+size_t MPIX_Allreduce_workspace(MPIX_Aint count, MPIX_Datatype datatype, MPIX_Comm comm);
+int MPIX_Allreduce(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Datatype datatype,
+                   MPIX_Op op, MPIX_Comm comm, int algorithm, void *workspace,
+                   size_t workspace_bytes);
+int MPIX_Allreduce_async(const void *sendbuf, void *recvbuf, MPIX_Aint count,
+                         MPIX_Datatype datatype, MPIX_Op op, MPIX_Comm comm, int algorithm,
+                         void *workspace, size_t workspace_bytes, void *stream);
+
+/* stream the blocking forms use: the communicator's own (NULL) by default */
+int MPIX_Comm_set_stream(MPIX_Comm comm, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPIX_COLL_H_INCLUDED */

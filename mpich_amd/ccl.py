@@ -1,0 +1,173 @@
+"""Host-side binding of libmpix_coll.so (include/mpix_coll.h): the
+reduce-scatter / allreduce schedules of MPICH in C++ host code, combining
+through the HIP kernels of libmpix_redop.so, over RCCL (one process per GPU)
+or the in-process transports (ranks as threads of one process).
+
+Mirrors the reference interface: MPI_Reduce_scatter_block(sendbuf, recvbuf,
+recvcount, datatype, op, comm) and MPI_Allreduce(sendbuf, recvbuf, count,
+datatype, op, comm) with MPI error classes as return values; `comm` is a
+`Comm` created here.  Like redop.py this module computes nothing itself and
+fails loudly if the library is missing.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (one HIP runtime per process: torch's)
+
+from . import handles as H
+from . import redop
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libmpix_coll.so')
+UNIQUE_ID_BYTES = 128
+
+RSB_AUTO, RSB_RECURSIVE_HALVING, RSB_PAIRWISE, RSB_PAIRWISE_SEQUENTIAL = 0, 1, 2, 3
+RSB_ALGORITHMS = {'auto': RSB_AUTO, 'recursive_halving': RSB_RECURSIVE_HALVING,
+                  'pairwise': RSB_PAIRWISE, 'pairwise_sequential': RSB_PAIRWISE_SEQUENTIAL}
+AR_AUTO, AR_RECURSIVE_DOUBLING, AR_RSAG, AR_RSAG_RD = 0, 1, 2, 3
+AR_ALGORITHMS = {'auto': AR_AUTO, 'recursive_doubling': AR_RECURSIVE_DOUBLING,
+                 'reduce_scatter_allgather': AR_RSAG, 'rsag_rd_allgather': AR_RSAG_RD}
+
+_lib = None
+
+COMBINE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ssize_t,
+                              ctypes.c_int, ctypes.c_int, ctypes.c_void_p)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        redop.lib()                     # libmpix_redop.so first (RTLD_GLOBAL)
+        if not os.path.exists(LIB_PATH):
+            raise ImportError('libmpix_coll.so is not built (%s); run `make -C mpich_amd/csrc`'
+                              % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        vp, i32, aint, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_ssize_t, ctypes.c_size_t
+        sig = {
+            'MPIX_Ccl_get_unique_id': ([vp], i32),
+            'MPIX_Comm_create_ccl': ([i32, i32, vp, ctypes.POINTER(vp)], i32),
+            'MPIX_Comm_create_local': ([i32, ctypes.POINTER(i32), ctypes.POINTER(vp)], i32),
+            'MPIX_Comm_create_custom': ([i32, i32, vp, vp, i32, ctypes.POINTER(vp)], i32),
+            'MPIX_Comm_set_combine': ([vp, vp], i32),
+            'MPIX_Comm_set_stream': ([vp, vp], i32),
+            'MPIX_Comm_rank': ([vp, ctypes.POINTER(i32)], i32),
+            'MPIX_Comm_size': ([vp, ctypes.POINTER(i32)], i32),
+            'MPIX_Comm_free': ([vp], i32),
+            'MPIX_Reduce_scatter_block_workspace': ([aint, i32, vp, i32], sz),
+            'MPIX_Reduce_scatter_block': ([vp, vp, aint, i32, i32, vp, i32, vp, sz], i32),
+            'MPIX_Reduce_scatter_block_async': ([vp, vp, aint, i32, i32, vp, i32, vp, sz, vp],
+                                                i32),
+            'MPIX_Allreduce_workspace': ([aint, i32, vp], sz),
+            'MPIX_Allreduce': ([vp, vp, aint, i32, i32, vp, i32, vp, sz], i32),
+            'MPIX_Allreduce_async': ([vp, vp, aint, i32, i32, vp, i32, vp, sz, vp], i32),
+        }
+        for name, (args, res) in sig.items():
+            f = getattr(L, name)
+            f.argtypes = args
+            f.restype = res
+        _lib = L
+    return _lib
+
+
+def _addr(buf):
+    return redop._addr(buf)
+
+
+class Comm:
+    """One rank's handle of a libmpix_coll communicator."""
+
+    def __init__(self, handle):
+        self.h = ctypes.c_void_p(handle)
+        r, s = ctypes.c_int(), ctypes.c_int()
+        lib().MPIX_Comm_rank(self.h, ctypes.byref(r))
+        lib().MPIX_Comm_size(self.h, ctypes.byref(s))
+        self.rank, self.size = r.value, s.value
+        self._keep = []
+
+    def set_combine(self, fn):
+        """install a combine function pointer (an int address, e.g. a C
+        symbol of the test oracle) or None for the HIP kernel"""
+        redop.check(lib().MPIX_Comm_set_combine(self.h, fn), 'MPIX_Comm_set_combine')
+
+    def set_stream(self, stream):
+        redop.check(lib().MPIX_Comm_set_stream(self.h, None if stream is None else
+                                               redop._stream_ptr(stream)), 'MPIX_Comm_set_stream')
+
+    def free(self):
+        if self.h:
+            rc = lib().MPIX_Comm_free(self.h)
+            self.h = None
+            return rc
+        return 0
+
+
+def get_unique_id():
+    b = ctypes.create_string_buffer(UNIQUE_ID_BYTES)
+    redop.check(lib().MPIX_Ccl_get_unique_id(b), 'MPIX_Ccl_get_unique_id')
+    return b.raw
+
+
+def comm_create_ccl(rank, size, unique_id):
+    """RCCL communicator (MPIR_RCCLcomm_init, rccl.c:21-52): rank 0's
+    get_unique_id() must reach every rank first (the reference bcasts it)."""
+    h = ctypes.c_void_p()
+    redop.check(lib().MPIX_Comm_create_ccl(rank, size, unique_id, ctypes.byref(h)),
+                'MPIX_Comm_create_ccl')
+    return Comm(h.value)
+
+
+def comm_create_ccl_from_process_group(group=None):
+    """convenience: bootstrap the RCCL communicator over an initialised
+    torch.distributed process group (the role MPIR_Bcast plays in rccl.c:36)"""
+    import torch.distributed as dist
+    rank, size = dist.get_rank(group), dist.get_world_size(group)
+    obj = [get_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=dist.get_global_rank(group, 0) if group else 0,
+                               group=group)
+    return comm_create_ccl(rank, size, obj[0])
+
+
+def comm_create_local(size, devices=None):
+    """`size` in-process ranks (drive each from its own thread); devices=None
+    is the host-memory transport (needs set_combine: no CPU compute path)."""
+    hs = (ctypes.c_void_p * size)()
+    devs = None if devices is None else (ctypes.c_int * size)(*devices)
+    redop.check(lib().MPIX_Comm_create_local(size, devs, hs), 'MPIX_Comm_create_local')
+    return [Comm(hs[r]) for r in range(size)]
+
+
+def reduce_scatter_block(sendbuf, recvbuf, recvcount, datatype, op, comm, algorithm='auto',
+                         workspace=None, stream=None, blocking=True):
+    """MPI_Reduce_scatter_block; returns the MPI error class."""
+    a = RSB_ALGORITHMS[algorithm] if isinstance(algorithm, str) else algorithm
+    ws, wsb = (None, 0) if workspace is None else (_addr(workspace), workspace.numel() *
+                                                    workspace.element_size())
+    if blocking:
+        return lib().MPIX_Reduce_scatter_block(_addr(sendbuf), _addr(recvbuf), recvcount,
+                                               H.as_c_int(datatype), H.as_c_int(op), comm.h, a,
+                                               ws, wsb)
+    return lib().MPIX_Reduce_scatter_block_async(_addr(sendbuf), _addr(recvbuf), recvcount,
+                                                 H.as_c_int(datatype), H.as_c_int(op), comm.h, a,
+                                                 ws, wsb, redop._stream_ptr(stream))
+
+
+def allreduce(sendbuf, recvbuf, count, datatype, op, comm, algorithm='auto', workspace=None,
+              stream=None, blocking=True):
+    """MPI_Allreduce (sendbuf None = MPI_IN_PLACE); returns the MPI error class."""
+    a = AR_ALGORITHMS[algorithm] if isinstance(algorithm, str) else algorithm
+    ws, wsb = (None, 0) if workspace is None else (_addr(workspace), workspace.numel() *
+                                                    workspace.element_size())
+    if blocking:
+        return lib().MPIX_Allreduce(_addr(sendbuf), _addr(recvbuf), count, H.as_c_int(datatype),
+                                    H.as_c_int(op), comm.h, a, ws, wsb)
+    return lib().MPIX_Allreduce_async(_addr(sendbuf), _addr(recvbuf), count, H.as_c_int(datatype),
+                                      H.as_c_int(op), comm.h, a, ws, wsb,
+                                      redop._stream_ptr(stream))
+
+
+def rsb_workspace_bytes(recvcount, datatype, comm, algorithm='auto'):
+    a = RSB_ALGORITHMS[algorithm] if isinstance(algorithm, str) else algorithm
+    return lib().MPIX_Reduce_scatter_block_workspace(recvcount, H.as_c_int(datatype), comm.h, a)
+
+
+def allreduce_workspace_bytes(count, datatype, comm):
+    return lib().MPIX_Allreduce_workspace(count, H.as_c_int(datatype), comm.h)

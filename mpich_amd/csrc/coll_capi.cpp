@@ -1,0 +1,916 @@
+// coll_capi.cpp -- libmpix_coll.so: MPICH's reduce-scatter / allreduce
+// schedules in C++ host code (include/mpix_coll.h), every combine step a call
+// into libmpix_redop.so's HIP kernels, every exchange step one group of
+// point-to-point operations on a transport:
+//
+//   RCCL        ncclGroupStart / ncclSend + ncclRecv / ncclGroupEnd on the
+//               collective's stream (one process per MI355X, xGMI between them)
+//   local       ranks are threads of one process; a receive is a stream-ordered
+//               hipMemcpyAsync from the sender's buffer after the sender's
+//               "ready" event, and the sender's stream then waits for the
+//               receiver's "done" event before it may touch that buffer again
+//   host-local  the same over host memory with memcpy (schedule tests without
+//               a GPU; a combine must be installed, there is no CPU compute path)
+//   custom      a caller-supplied exchange function
+//
+// The schedules restate, index for index, the reference algorithms cited in
+// include/mpix_coll.h; mpich_amd/coll.py holds the same schedules over
+// torch.distributed and the oracle (oracle/redop_oracle.c) simulates them in
+// one process -- the tests hold all three to the same bits.
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <chrono>
+#include <condition_variable>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <tuple>
+#include <vector>
+
+#include "mpix_coll.h"
+
+namespace {
+
+enum Kind { K_CCL, K_LOCAL_DEV, K_LOCAL_HOST, K_CUSTOM };
+
+// a rank's receive group completion event, shared by the senders that must
+// wait for it; the last sender to enqueue its wait destroys it
+struct DoneEv {
+    hipEvent_t ev = nullptr;
+    int refs = 0;
+};
+
+struct Slot {
+    const void *buf = nullptr;
+    size_t bytes = 0;
+    hipEvent_t ready = nullptr;     // sender's stream state when the send was posted
+    std::shared_ptr<DoneEv> done;   // receiver's copy completion
+    bool consumed = false;
+};
+
+// shared mailbox of a local communicator: slots keyed (src, dst, seq), seq
+// counting the messages of that ordered pair (MPI's non-overtaking order)
+struct Local {
+    int size = 0;
+    bool host = false;
+    std::vector<int> devices;
+    std::mutex m;
+    std::condition_variable cv;
+    std::map<std::tuple<int, int, uint64_t>, Slot> slots;
+};
+
+// a peer that never reaches the matching step is an application bug; fail the
+// call instead of hanging the process
+const auto kPeerTimeout = std::chrono::seconds(300);
+
+}  // namespace
+
+struct MPIX_Comm_s {
+    int rank = 0, size = 1;
+    Kind kind = K_CUSTOM;
+    ncclComm_t nccl = nullptr;
+    std::shared_ptr<Local> local;
+    MPIX_Exchange_fn xfn = nullptr;
+    void *xctx = nullptr;
+    MPIX_Combine_fn combine = nullptr;
+    int device = -1;
+    hipStream_t own_stream = nullptr;
+    void *stream = nullptr;         // stream of the blocking forms (NULL: own_stream)
+    void *scratch = nullptr;
+    size_t scratch_bytes = 0;
+    std::vector<uint64_t> send_seq, recv_seq;
+    bool host() const { return kind == K_LOCAL_HOST || (kind == K_CUSTOM && device < 0); }
+};
+
+namespace {
+
+int hip_fail(hipError_t e) { return e == hipSuccess ? MPIX_REDOP_SUCCESS : MPIX_REDOP_ERR_OTHER; }
+
+#define TRY(x) do { int rc_ = (x); if (rc_ != MPIX_REDOP_SUCCESS) return rc_; } while (0)
+#define HTRY(x) do { if ((x) != hipSuccess) return MPIX_REDOP_ERR_OTHER; } while (0)
+
+size_t round256(size_t b) { return (b + 255) & ~(size_t) 255; }
+
+int pof2_of(int n)
+{
+    int p = 1;
+    while (p * 2 <= n)
+        p *= 2;
+    return p;
+}
+
+int set_device(MPIX_Comm c)
+{
+    if (c->device >= 0)
+        HTRY(hipSetDevice(c->device));
+    return MPIX_REDOP_SUCCESS;
+}
+
+hipStream_t stream_of(void *s) { return static_cast<hipStream_t>(s); }
+
+// ------------------------------------------------------------ transports
+int exchange_ccl(MPIX_Comm c, const MPIX_P2p_op *ops, int nops, hipStream_t s)
+{
+    if (ncclGroupStart() != ncclSuccess)
+        return MPIX_REDOP_ERR_OTHER;
+    ncclResult_t r = ncclSuccess;
+    for (int i = 0; i < nops && r == ncclSuccess; ++i) {
+        if (ops[i].bytes == 0)
+            continue;
+        r = ops[i].is_recv ? ncclRecv(ops[i].buf, ops[i].bytes, ncclUint8, ops[i].peer, c->nccl, s)
+                           : ncclSend(ops[i].buf, ops[i].bytes, ncclUint8, ops[i].peer, c->nccl, s);
+    }
+    ncclResult_t r2 = ncclGroupEnd();
+    return (r == ncclSuccess && r2 == ncclSuccess) ? MPIX_REDOP_SUCCESS : MPIX_REDOP_ERR_OTHER;
+}
+
+int exchange_local(MPIX_Comm c, const MPIX_P2p_op *ops, int nops, hipStream_t s)
+{
+    Local &L = *c->local;
+    const bool host = L.host;
+    typedef std::tuple<int, int, uint64_t> Key;
+    std::vector<Key> sends, recvs;
+    bool any_send = false;
+    for (int i = 0; i < nops; ++i)
+        any_send |= !ops[i].is_recv && ops[i].bytes;
+    // phase 1: post the sends, with the stream position they must follow
+    hipEvent_t ready = nullptr;
+    if (!host && any_send) {
+        HTRY(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+        HTRY(hipEventRecord(ready, s));
+    }
+    {
+        std::lock_guard<std::mutex> g(L.m);
+        for (int i = 0; i < nops; ++i) {
+            if (ops[i].is_recv || !ops[i].bytes)
+                continue;
+            Key k(c->rank, ops[i].peer, c->send_seq[ops[i].peer]++);
+            Slot &sl = L.slots[k];
+            sl.buf = ops[i].buf;
+            sl.bytes = ops[i].bytes;
+            sl.ready = ready;
+            sends.push_back(k);
+        }
+    }
+    L.cv.notify_all();
+    // phase 2: each receive copies from the matching posted send
+    int rc = MPIX_REDOP_SUCCESS;
+    for (int i = 0; i < nops && rc == MPIX_REDOP_SUCCESS; ++i) {
+        if (!ops[i].is_recv || !ops[i].bytes)
+            continue;
+        Key k(ops[i].peer, c->rank, c->recv_seq[ops[i].peer]++);
+        Slot sl;
+        {
+            std::unique_lock<std::mutex> g(L.m);
+            if (!L.cv.wait_for(g, kPeerTimeout, [&] { return L.slots.count(k) != 0; })) {
+                rc = MPIX_REDOP_ERR_OTHER;
+                break;
+            }
+            sl = L.slots[k];
+        }
+        if (sl.bytes > ops[i].bytes) {          // MPI_ERR_TRUNCATE
+            rc = MPIX_REDOP_ERR_COUNT;
+            break;
+        }
+        if (host) {
+            memcpy(ops[i].buf, sl.buf, sl.bytes);
+        } else if (hipStreamWaitEvent(s, sl.ready, 0) != hipSuccess ||
+                   hipMemcpyAsync(ops[i].buf, sl.buf, sl.bytes, hipMemcpyDefault, s) != hipSuccess) {
+            rc = MPIX_REDOP_ERR_OTHER;
+        }
+        recvs.push_back(k);
+    }
+    std::shared_ptr<DoneEv> done;
+    if (!recvs.empty()) {
+        done = std::make_shared<DoneEv>();
+        done->refs = (int) recvs.size();
+        if (!host && (hipEventCreateWithFlags(&done->ev, hipEventDisableTiming) != hipSuccess ||
+                      hipEventRecord(done->ev, s) != hipSuccess))
+            rc = MPIX_REDOP_ERR_OTHER;
+    }
+    {   // mark consumed even on failure so the senders do not wait forever
+        std::lock_guard<std::mutex> g(L.m);
+        for (auto &k : recvs) {
+            Slot &sl = L.slots[k];
+            sl.done = done;
+            sl.consumed = true;
+        }
+    }
+    L.cv.notify_all();
+    // phase 3: this stream may reuse its send buffers only after the copies
+    for (auto &k : sends) {
+        std::shared_ptr<DoneEv> d;
+        {
+            std::unique_lock<std::mutex> g(L.m);
+            if (!L.cv.wait_for(g, kPeerTimeout, [&] { return L.slots[k].consumed; })) {
+                rc = MPIX_REDOP_ERR_OTHER;
+                continue;
+            }
+            d = L.slots[k].done;
+            L.slots.erase(k);
+        }
+        if (!host && d && d->ev && hipStreamWaitEvent(s, d->ev, 0) != hipSuccess)
+            rc = MPIX_REDOP_ERR_OTHER;
+        std::lock_guard<std::mutex> g(L.m);
+        if (d && --d->refs == 0 && d->ev)
+            (void) hipEventDestroy(d->ev);      // waits already enqueued; HIP frees it later
+    }
+    if (ready)
+        (void) hipEventDestroy(ready);
+    return rc;
+}
+
+int exchange(MPIX_Comm c, const std::vector<MPIX_P2p_op> &ops, hipStream_t s)
+{
+    if (ops.empty())
+        return MPIX_REDOP_SUCCESS;
+    switch (c->kind) {
+        case K_CCL:
+            return exchange_ccl(c, ops.data(), (int) ops.size(), s);
+        case K_LOCAL_DEV:
+        case K_LOCAL_HOST:
+            return exchange_local(c, ops.data(), (int) ops.size(), s);
+        default:
+            return c->xfn(c->xctx, c->rank, ops.data(), (int) ops.size(), s) ? MPIX_REDOP_ERR_OTHER
+                                                                             : MPIX_REDOP_SUCCESS;
+    }
+}
+
+MPIX_P2p_op snd(int peer, const void *buf, size_t bytes)
+{
+    return MPIX_P2p_op{peer, 0, const_cast<void *>(buf), bytes};
+}
+MPIX_P2p_op rcv(int peer, void *buf, size_t bytes) { return MPIX_P2p_op{peer, 1, buf, bytes}; }
+
+// ------------------------------------------------------------ data movement
+int copy(MPIX_Comm c, void *dst, const void *src, size_t bytes, hipStream_t s)
+{
+    if (!bytes || dst == src)
+        return MPIX_REDOP_SUCCESS;
+    if (c->host()) {
+        memmove(dst, src, bytes);
+        return MPIX_REDOP_SUCCESS;
+    }
+    return hip_fail(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, s));
+}
+
+// MPIR_Reduce_local(in, inout, count, datatype, op) of the schedule
+int combine(MPIX_Comm c, const void *in, void *inout, MPIX_Aint count, MPIX_Datatype dt, MPIX_Op op,
+            hipStream_t s)
+{
+    if (!count)
+        return MPIX_REDOP_SUCCESS;
+    if (c->combine)
+        return c->combine(in, inout, count, dt, op, s);
+    if (c->host())
+        return MPIX_Reduce_local(in, inout, count, dt, op);
+    return MPIX_Reduce_local_async(in, inout, count, dt, op, s);
+}
+
+// k received blocks folded in order: one multi-input kernel pass (16 at most
+// per launch), the same association as k combine() calls
+int combine_multi(MPIX_Comm c, const std::vector<const void *> &ins, void *inout, MPIX_Aint count,
+                  MPIX_Datatype dt, MPIX_Op op, hipStream_t s)
+{
+    if (c->combine || c->host()) {
+        for (const void *p : ins)
+            TRY(combine(c, p, inout, count, dt, op, s));
+        return MPIX_REDOP_SUCCESS;
+    }
+    for (size_t lo = 0; lo < ins.size(); lo += 16) {
+        int k = (int) std::min<size_t>(16, ins.size() - lo);
+        TRY(MPIX_Reduce_local_multi_async(ins.data() + lo, k, inout, count, dt, op, s));
+    }
+    return MPIX_REDOP_SUCCESS;
+}
+
+int scratch(MPIX_Comm c, size_t bytes, hipStream_t s, char **out)
+{
+    if (c->scratch_bytes < bytes) {
+        if (c->scratch) {
+            if (c->host()) {
+                free(c->scratch);
+            } else {
+                HTRY(hipStreamSynchronize(s));
+                HTRY(hipFree(c->scratch));
+            }
+            c->scratch = nullptr;
+            c->scratch_bytes = 0;
+        }
+        if (c->host()) {
+            c->scratch = malloc(bytes);
+            if (!c->scratch)
+                return MPIX_REDOP_ERR_OTHER;
+        } else {
+            HTRY(hipMalloc(&c->scratch, bytes));
+        }
+        c->scratch_bytes = bytes;
+    }
+    *out = static_cast<char *>(c->scratch);
+    return MPIX_REDOP_SUCCESS;
+}
+
+int workspace(MPIX_Comm c, void *ws, size_t ws_bytes, size_t need, hipStream_t s, char **out)
+{
+    if (!need) {
+        *out = nullptr;
+        return MPIX_REDOP_SUCCESS;
+    }
+    if (ws) {
+        if (ws_bytes < need)
+            return MPIX_REDOP_ERR_ARG;
+        *out = static_cast<char *>(ws);
+        return MPIX_REDOP_SUCCESS;
+    }
+    return scratch(c, need, s, out);
+}
+
+int finish(MPIX_Comm c, int rc, hipStream_t s, bool blocking)
+{
+    if (rc == MPIX_REDOP_SUCCESS && blocking && !c->host())
+        rc = hip_fail(hipStreamSynchronize(s));
+    return rc;
+}
+
+int check_args(MPIX_Comm c, const void *recvbuf, MPIX_Aint count, MPIX_Datatype dt, MPIX_Op op,
+               size_t *ext)
+{
+    if (!c)
+        return MPIX_REDOP_ERR_ARG;
+    if (count < 0)
+        return MPIX_REDOP_ERR_COUNT;
+    if (!MPIX_Redop_op_dt_check(op, dt))
+        return MPIX_REDOP_ERR_OP;
+    *ext = (size_t) MPIX_Datatype_extent(dt);
+    if (!*ext)
+        return MPIX_REDOP_ERR_TYPE;
+    if (!recvbuf && count)
+        return MPIX_REDOP_ERR_BUFFER;
+    return MPIX_REDOP_SUCCESS;
+}
+
+// ------------------------------------------------------------ schedules
+// MPIR_Reduce_scatter_block_intra_recursive_halving
+// (reduce_scatter_block_intra_recursive_halving.c:38-260)
+int rsb_recursive_halving(const char *sb, char *rb, size_t recvcount, MPIX_Datatype dt, MPIX_Op op,
+                          MPIX_Comm c, char *ws, hipStream_t s, size_t ext)
+{
+    const int rank = c->rank, size = c->size;
+    const size_t total = recvcount * size;
+    char *tmp_results = ws;
+    char *tmp_recvbuf = ws + round256(total * ext);
+    TRY(copy(c, tmp_results, sb, total * ext, s));                         // :91-96
+    const int pof2 = pof2_of(size), rem = size - pof2;
+    int newrank;
+    if (rank < 2 * rem) {                                                   // :110-137
+        if (rank % 2 == 0) {
+            TRY(exchange(c, {snd(rank + 1, tmp_results, total * ext)}, s));
+            newrank = -1;
+        } else {
+            TRY(exchange(c, {rcv(rank - 1, tmp_recvbuf, total * ext)}, s));
+            TRY(combine(c, tmp_recvbuf, tmp_results, (MPIX_Aint) total, dt, op, s));
+            newrank = rank / 2;
+        }
+    } else {
+        newrank = rank - rem;
+    }
+    if (newrank != -1) {                                                    // :139-229
+        std::vector<size_t> newcnts(pof2), newdisps(pof2, 0);
+        for (int i = 0; i < pof2; ++i) {
+            int old_i = i < rem ? i * 2 + 1 : i + rem;
+            newcnts[i] = old_i < 2 * rem ? 2 * recvcount : recvcount;
+        }
+        for (int i = 1; i < pof2; ++i)
+            newdisps[i] = newdisps[i - 1] + newcnts[i - 1];
+        auto sum = [&](int lo, int hi) {
+            size_t t = 0;
+            for (int i = lo; i < hi; ++i)
+                t += newcnts[i];
+            return t;
+        };
+        int mask = pof2 >> 1, send_idx = 0, recv_idx = 0, last_idx = pof2;
+        while (mask > 0) {
+            int newdst = newrank ^ mask;
+            int dst = newdst < rem ? newdst * 2 + 1 : newdst + rem;
+            size_t send_cnt, recv_cnt;
+            if (newrank < newdst) {
+                send_idx = recv_idx + mask;
+                send_cnt = sum(send_idx, last_idx);
+                recv_cnt = sum(recv_idx, send_idx);
+            } else {
+                recv_idx = send_idx + mask;
+                send_cnt = sum(send_idx, recv_idx);
+                recv_cnt = sum(recv_idx, last_idx);
+            }
+            TRY(exchange(c, {snd(dst, tmp_results + newdisps[send_idx] * ext, send_cnt * ext),
+                             rcv(dst, tmp_recvbuf + newdisps[recv_idx] * ext, recv_cnt * ext)}, s));
+            TRY(combine(c, tmp_recvbuf + newdisps[recv_idx] * ext,
+                        tmp_results + newdisps[recv_idx] * ext, (MPIX_Aint) recv_cnt, dt, op, s));
+            send_idx = recv_idx;
+            last_idx = recv_idx + mask;
+            mask >>= 1;
+        }
+        TRY(copy(c, rb, tmp_results + rank * recvcount * ext, recvcount * ext, s));   // :232-234
+    }
+    if (rank < 2 * rem) {                                                   // :241-253
+        if (rank % 2)
+            TRY(exchange(c, {snd(rank - 1, tmp_results + (rank - 1) * recvcount * ext,
+                                 recvcount * ext)}, s));
+        else
+            TRY(exchange(c, {rcv(rank + 1, rb, recvcount * ext)}, s));
+    }
+    return MPIX_REDOP_SUCCESS;
+}
+
+// MPIR_Reduce_scatter_block_intra_pairwise (…_intra_pairwise.c:42-104):
+// step i = 1..P-1 sends block (rank+i) to rank+i and folds the block
+// received from rank-i into the result, in that order.  `concurrent` posts
+// all P-1 exchanges as one group (every xGMI link busy at once) and folds
+// the P-1 blocks in one multi-input pass; same order, same bits.
+int rsb_pairwise(const char *sb, char *rb, size_t recvcount, MPIX_Datatype dt, MPIX_Op op,
+                 MPIX_Comm c, char *ws, hipStream_t s, size_t ext, bool concurrent)
+{
+    const int rank = c->rank, size = c->size;
+    const size_t blk = recvcount * ext, sstride = round256(blk);
+    TRY(copy(c, rb, sb + rank * blk, blk, s));                              // :60-64
+    if (!concurrent) {
+        for (int i = 1; i < size; ++i) {
+            int dst = (rank + i) % size, src = (rank - i + size) % size;
+            TRY(exchange(c, {snd(dst, sb + dst * blk, blk), rcv(src, ws, blk)}, s));
+            TRY(combine(c, ws, rb, (MPIX_Aint) recvcount, dt, op, s));
+        }
+        return MPIX_REDOP_SUCCESS;
+    }
+    std::vector<MPIX_P2p_op> ops;
+    std::vector<const void *> ins;
+    for (int i = 1; i < size; ++i) {
+        int dst = (rank + i) % size, src = (rank - i + size) % size;
+        ops.push_back(snd(dst, sb + dst * blk, blk));
+        ops.push_back(rcv(src, ws + (i - 1) * sstride, blk));
+        ins.push_back(ws + (i - 1) * sstride);
+    }
+    TRY(exchange(c, ops, s));
+    return combine_multi(c, ins, rb, (MPIX_Aint) recvcount, dt, op, s);
+}
+
+int rsb_choose(int algorithm, size_t recvcount, size_t ext, int size)
+{
+    if (algorithm != MPIX_RSB_AUTO)
+        return algorithm;
+    // generic.json:316-341: recursive halving below 512 KiB, pairwise above
+    return recvcount * ext * size < (512u << 10) ? MPIX_RSB_RECURSIVE_HALVING : MPIX_RSB_PAIRWISE;
+}
+
+size_t rsb_workspace(size_t recvcount, size_t ext, int size, int algo)
+{
+    if (size == 1)
+        return 0;
+    switch (algo) {
+        case MPIX_RSB_RECURSIVE_HALVING:
+            return 2 * round256(recvcount * size * ext);
+        case MPIX_RSB_PAIRWISE:
+            return (size - 1) * round256(recvcount * ext);
+        case MPIX_RSB_PAIRWISE_SEQUENTIAL:
+            return round256(recvcount * ext);
+        default:
+            return 0;
+    }
+}
+
+int bitrev(int r, int pof2)
+{
+    int out = 0;
+    for (int b = pof2 >> 1; b; b >>= 1) {
+        out = (out << 1) | (r & 1);
+        r >>= 1;
+    }
+    return out;
+}
+
+// MPIR_Allreduce_intra_reduce_scatter_allgather
+// (allreduce_intra_reduce_scatter_allgather.c:41-277); `direct` replaces the
+// log2(P) allgather exchanges (:191-226) by one group of P-1 direct ones --
+// the allgather only moves finished blocks, so the bits do not change.
+int allreduce_rsag(char *rb, size_t count, MPIX_Datatype dt, MPIX_Op op, MPIX_Comm c, char *tmp,
+                   hipStream_t s, size_t ext, bool direct)
+{
+    const int rank = c->rank, size = c->size;
+    const int pof2 = pof2_of(size), rem = size - pof2;
+    const size_t nb = count * ext;
+    int newrank;
+    if (rank < 2 * rem) {                                                   // :85-112
+        if (rank % 2 == 0) {
+            TRY(exchange(c, {snd(rank + 1, rb, nb)}, s));
+            newrank = -1;
+        } else {
+            TRY(exchange(c, {rcv(rank - 1, tmp, nb)}, s));
+            TRY(combine(c, tmp, rb, (MPIX_Aint) count, dt, op, s));
+            newrank = rank / 2;
+        }
+    } else {
+        newrank = rank - rem;
+    }
+    if (newrank != -1) {
+        std::vector<size_t> cnts(pof2), disps(pof2, 0);
+        for (int i = 0; i < pof2; ++i)
+            cnts[i] = count / pof2 + ((size_t) i < count % pof2 ? 1 : 0);
+        for (int i = 1; i < pof2; ++i)
+            disps[i] = disps[i - 1] + cnts[i - 1];
+        auto sum = [&](int lo, int hi) {
+            size_t t = 0;
+            for (int i = lo; i < hi; ++i)
+                t += cnts[i];
+            return t;
+        };
+        auto real = [&](int nr) { return nr < rem ? nr * 2 + 1 : nr + rem; };
+        int mask = 1, send_idx = 0, recv_idx = 0, last_idx = pof2;
+        while (mask < pof2) {                                               // :138-189
+            int newdst = newrank ^ mask;
+            size_t send_cnt, recv_cnt;
+            if (newrank < newdst) {
+                send_idx = recv_idx + pof2 / (mask * 2);
+                send_cnt = sum(send_idx, last_idx);
+                recv_cnt = sum(recv_idx, send_idx);
+            } else {
+                recv_idx = send_idx + pof2 / (mask * 2);
+                send_cnt = sum(send_idx, recv_idx);
+                recv_cnt = sum(recv_idx, last_idx);
+            }
+            TRY(exchange(c, {snd(real(newdst), rb + disps[send_idx] * ext, send_cnt * ext),
+                             rcv(real(newdst), tmp + disps[recv_idx] * ext, recv_cnt * ext)}, s));
+            TRY(combine(c, tmp + disps[recv_idx] * ext, rb + disps[recv_idx] * ext,
+                        (MPIX_Aint) recv_cnt, dt, op, s));
+            send_idx = recv_idx;
+            mask <<= 1;
+            if (mask < pof2)
+                last_idx = recv_idx + pof2 / mask;
+        }
+        mask >>= 1;
+        if (direct) {
+            const int mine = bitrev(newrank, pof2);
+            std::vector<MPIX_P2p_op> ops;
+            for (int q = 0; q < pof2; ++q) {
+                if (q == newrank)
+                    continue;
+                const int b = bitrev(q, pof2);
+                ops.push_back(snd(real(q), rb + disps[mine] * ext, cnts[mine] * ext));
+                ops.push_back(rcv(real(q), rb + disps[b] * ext, cnts[b] * ext));
+            }
+            TRY(exchange(c, ops, s));
+            mask = 0;
+        }
+        while (mask > 0) {                                                  // :191-226
+            int newdst = newrank ^ mask;
+            size_t send_cnt, recv_cnt;
+            if (newrank < newdst) {
+                if (mask != pof2 / 2)
+                    last_idx = last_idx + pof2 / (mask * 2);
+                recv_idx = send_idx + pof2 / (mask * 2);
+                send_cnt = sum(send_idx, recv_idx);
+                recv_cnt = sum(recv_idx, last_idx);
+            } else {
+                recv_idx = send_idx - pof2 / (mask * 2);
+                send_cnt = sum(send_idx, last_idx);
+                recv_cnt = sum(recv_idx, send_idx);
+            }
+            TRY(exchange(c, {snd(real(newdst), rb + disps[send_idx] * ext, send_cnt * ext),
+                             rcv(real(newdst), rb + disps[recv_idx] * ext, recv_cnt * ext)}, s));
+            if (newrank > newdst)
+                send_idx = recv_idx;
+            mask >>= 1;
+        }
+    }
+    if (rank < 2 * rem) {                                                   // :229-238
+        if (rank % 2)
+            TRY(exchange(c, {snd(rank - 1, rb, nb)}, s));
+        else
+            TRY(exchange(c, {rcv(rank + 1, rb, nb)}, s));
+    }
+    return MPIX_REDOP_SUCCESS;
+}
+
+// MPIR_Allreduce_intra_recursive_doubling (allreduce_intra_recursive_doubling.c:24-150)
+int allreduce_rd(char *rb, size_t count, MPIX_Datatype dt, MPIX_Op op, MPIX_Comm c, char *tmp,
+                 hipStream_t s, size_t ext)
+{
+    const int rank = c->rank, size = c->size;
+    const int pof2 = pof2_of(size), rem = size - pof2;
+    const size_t nb = count * ext;
+    int newrank;
+    if (rank < 2 * rem) {                                                   // :59-86
+        if (rank % 2 == 0) {
+            TRY(exchange(c, {snd(rank + 1, rb, nb)}, s));
+            newrank = -1;
+        } else {
+            TRY(exchange(c, {rcv(rank - 1, tmp, nb)}, s));
+            TRY(combine(c, tmp, rb, (MPIX_Aint) count, dt, op, s));
+            newrank = rank / 2;
+        }
+    } else {
+        newrank = rank - rem;
+    }
+    if (newrank != -1) {
+        for (int mask = 1; mask < pof2; mask <<= 1) {                       // :97-129
+            int newdst = newrank ^ mask;
+            int dst = newdst < rem ? newdst * 2 + 1 : newdst + rem;
+            TRY(exchange(c, {snd(dst, rb, nb), rcv(dst, tmp, nb)}, s));
+            TRY(combine(c, tmp, rb, (MPIX_Aint) count, dt, op, s));
+        }
+    }
+    if (rank < 2 * rem) {                                                   // :131-141
+        if (rank % 2)
+            TRY(exchange(c, {snd(rank - 1, rb, nb)}, s));
+        else
+            TRY(exchange(c, {rcv(rank + 1, rb, nb)}, s));
+    }
+    return MPIX_REDOP_SUCCESS;
+}
+
+int rsb_entry(const void *sendbuf, void *recvbuf, MPIX_Aint recvcount, MPIX_Datatype dt, MPIX_Op op,
+              MPIX_Comm c, int algorithm, void *ws, size_t ws_bytes, void *stream, bool blocking)
+{
+    size_t ext;
+    TRY(check_args(c, recvbuf, recvcount, dt, op, &ext));
+    if (!sendbuf && recvcount)
+        return MPIX_REDOP_ERR_BUFFER;
+    if (algorithm < MPIX_RSB_AUTO || algorithm > MPIX_RSB_PAIRWISE_SEQUENTIAL)
+        return MPIX_REDOP_ERR_ARG;
+    if (!recvcount)
+        return MPIX_REDOP_SUCCESS;
+    TRY(set_device(c));
+    hipStream_t s = stream_of(stream);
+    const char *sb = static_cast<const char *>(sendbuf);
+    char *rb = static_cast<char *>(recvbuf);
+    int algo = rsb_choose(algorithm, (size_t) recvcount, ext, c->size);
+    if (c->size == 1)
+        return finish(c, copy(c, rb, sb, (size_t) recvcount * ext, s), s, blocking);
+    char *w;
+    TRY(workspace(c, ws, ws_bytes, rsb_workspace((size_t) recvcount, ext, c->size, algo), s, &w));
+    int rc = algo == MPIX_RSB_RECURSIVE_HALVING
+                 ? rsb_recursive_halving(sb, rb, (size_t) recvcount, dt, op, c, w, s, ext)
+                 : rsb_pairwise(sb, rb, (size_t) recvcount, dt, op, c, w, s, ext,
+                                algo == MPIX_RSB_PAIRWISE);
+    return finish(c, rc, s, blocking);
+}
+
+int allreduce_entry(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Datatype dt,
+                    MPIX_Op op, MPIX_Comm c, int algorithm, void *ws, size_t ws_bytes, void *stream,
+                    bool blocking)
+{
+    size_t ext;
+    TRY(check_args(c, recvbuf, count, dt, op, &ext));
+    if (algorithm < MPIX_ALLREDUCE_AUTO || algorithm > MPIX_ALLREDUCE_RSAG_RD_ALLGATHER)
+        return MPIX_REDOP_ERR_ARG;
+    if (!count)
+        return MPIX_REDOP_SUCCESS;
+    TRY(set_device(c));
+    hipStream_t s = stream_of(stream);
+    char *rb = static_cast<char *>(recvbuf);
+    const size_t nb = (size_t) count * ext;
+    const int pof2 = pof2_of(c->size);
+    if (algorithm == MPIX_ALLREDUCE_AUTO)       // the reference's condition, :127
+        algorithm = (size_t) count >= (size_t) pof2 ? MPIX_ALLREDUCE_REDUCE_SCATTER_ALLGATHER
+                                                    : MPIX_ALLREDUCE_RECURSIVE_DOUBLING;
+    if (algorithm != MPIX_ALLREDUCE_RECURSIVE_DOUBLING && (size_t) count < (size_t) pof2)
+        return MPIX_REDOP_ERR_COUNT;
+    if (sendbuf)
+        TRY(copy(c, rb, sendbuf, nb, s));
+    if (c->size == 1)
+        return finish(c, MPIX_REDOP_SUCCESS, s, blocking);
+    char *tmp;
+    TRY(workspace(c, ws, ws_bytes, round256(nb), s, &tmp));
+    int rc = algorithm == MPIX_ALLREDUCE_RECURSIVE_DOUBLING
+                 ? allreduce_rd(rb, (size_t) count, dt, op, c, tmp, s, ext)
+                 : allreduce_rsag(rb, (size_t) count, dt, op, c, tmp, s, ext,
+                                  algorithm == MPIX_ALLREDUCE_REDUCE_SCATTER_ALLGATHER);
+    return finish(c, rc, s, blocking);
+}
+
+MPIX_Comm new_comm(int rank, int size, Kind kind)
+{
+    MPIX_Comm c = new MPIX_Comm_s;
+    c->rank = rank;
+    c->size = size;
+    c->kind = kind;
+    c->send_seq.assign(size, 0);
+    c->recv_seq.assign(size, 0);
+    return c;
+}
+
+int make_own_stream(MPIX_Comm c)
+{
+    if (c->host())
+        return MPIX_REDOP_SUCCESS;
+    TRY(set_device(c));
+    HTRY(hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
+    return MPIX_REDOP_SUCCESS;
+}
+
+}  // namespace
+
+extern "C" {
+
+int MPIX_Ccl_get_unique_id(void *id_out)
+{
+    static_assert(sizeof(ncclUniqueId) <= MPIX_CCL_UNIQUE_ID_BYTES, "unique id size");
+    if (!id_out)
+        return MPIX_REDOP_ERR_ARG;
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess)
+        return MPIX_REDOP_ERR_OTHER;
+    memset(id_out, 0, MPIX_CCL_UNIQUE_ID_BYTES);
+    memcpy(id_out, &id, sizeof id);
+    return MPIX_REDOP_SUCCESS;
+}
+
+int MPIX_Comm_create_ccl(int rank, int size, const void *id, MPIX_Comm *comm)
+{
+    if (!comm || !id || size < 1 || rank < 0 || rank >= size)
+        return MPIX_REDOP_ERR_ARG;
+    *comm = nullptr;
+    int dev;
+    HTRY(hipGetDevice(&dev));
+    ncclUniqueId uid;
+    memcpy(&uid, id, sizeof uid);
+    MPIX_Comm c = new_comm(rank, size, K_CCL);
+    c->device = dev;
+    if (ncclCommInitRank(&c->nccl, size, uid, rank) != ncclSuccess) {     // rccl.c:43
+        delete c;
+        return MPIX_REDOP_ERR_OTHER;
+    }
+    int rc = make_own_stream(c);
+    if (rc) {
+        ncclCommDestroy(c->nccl);
+        delete c;
+        return rc;
+    }
+    *comm = c;
+    return MPIX_REDOP_SUCCESS;
+}
+
+int MPIX_Comm_create_local(int size, const int *devices, MPIX_Comm *comms)
+{
+    if (!comms || size < 1)
+        return MPIX_REDOP_ERR_ARG;
+    auto L = std::make_shared<Local>();
+    L->size = size;
+    L->host = devices == nullptr;
+    if (devices)
+        L->devices.assign(devices, devices + size);
+    for (int r = 0; r < size; ++r) {
+        MPIX_Comm c = new_comm(r, size, L->host ? K_LOCAL_HOST : K_LOCAL_DEV);
+        c->local = L;
+        c->device = devices ? devices[r] : -1;
+        int rc = make_own_stream(c);
+        if (rc) {
+            for (int q = 0; q < r; ++q)
+                MPIX_Comm_free(comms[q]);
+            delete c;
+            return rc;
+        }
+        comms[r] = c;
+    }
+    return MPIX_REDOP_SUCCESS;
+}
+
+int MPIX_Comm_create_custom(int rank, int size, MPIX_Exchange_fn fn, void *ctx, int host_memory,
+                            MPIX_Comm *comm)
+{
+    if (!comm || !fn || size < 1 || rank < 0 || rank >= size)
+        return MPIX_REDOP_ERR_ARG;
+    MPIX_Comm c = new_comm(rank, size, K_CUSTOM);
+    c->xfn = fn;
+    c->xctx = ctx;
+    if (!host_memory) {
+        int dev;
+        if (hipGetDevice(&dev) != hipSuccess) {
+            delete c;
+            return MPIX_REDOP_ERR_OTHER;
+        }
+        c->device = dev;
+    }
+    int rc = make_own_stream(c);
+    if (rc) {
+        delete c;
+        return rc;
+    }
+    *comm = c;
+    return MPIX_REDOP_SUCCESS;
+}
+
+int MPIX_Comm_set_combine(MPIX_Comm comm, MPIX_Combine_fn fn)
+{
+    if (!comm)
+        return MPIX_REDOP_ERR_ARG;
+    comm->combine = fn;
+    return MPIX_REDOP_SUCCESS;
+}
+
+int MPIX_Comm_set_stream(MPIX_Comm comm, void *stream)
+{
+    if (!comm)
+        return MPIX_REDOP_ERR_ARG;
+    comm->stream = stream;
+    return MPIX_REDOP_SUCCESS;
+}
+
+int MPIX_Comm_rank(MPIX_Comm comm, int *rank)
+{
+    if (!comm || !rank)
+        return MPIX_REDOP_ERR_ARG;
+    *rank = comm->rank;
+    return MPIX_REDOP_SUCCESS;
+}
+
+int MPIX_Comm_size(MPIX_Comm comm, int *size)
+{
+    if (!comm || !size)
+        return MPIX_REDOP_ERR_ARG;
+    *size = comm->size;
+    return MPIX_REDOP_SUCCESS;
+}
+
+int MPIX_Comm_free(MPIX_Comm comm)
+{
+    if (!comm)
+        return MPIX_REDOP_ERR_ARG;
+    int rc = MPIX_REDOP_SUCCESS;
+    if (!comm->host()) {
+        if (set_device(comm) != MPIX_REDOP_SUCCESS)
+            rc = MPIX_REDOP_ERR_OTHER;
+        if (comm->own_stream && hipStreamSynchronize(comm->own_stream) != hipSuccess)
+            rc = MPIX_REDOP_ERR_OTHER;
+        if (comm->scratch) {
+            (void) hipDeviceSynchronize();      // the scratch may be in use on a caller stream
+            (void) hipFree(comm->scratch);
+        }
+        if (comm->own_stream)
+            (void) hipStreamDestroy(comm->own_stream);
+    } else {
+        free(comm->scratch);
+    }
+    if (comm->nccl && ncclCommDestroy(comm->nccl) != ncclSuccess)         // rccl.c:237-250
+        rc = MPIX_REDOP_ERR_OTHER;
+    delete comm;        // the last local handle takes the shared mailbox with it
+    return rc;
+}
+
+size_t MPIX_Reduce_scatter_block_workspace(MPIX_Aint recvcount, MPIX_Datatype datatype,
+                                           MPIX_Comm comm, int algorithm)
+{
+    size_t ext = (size_t) MPIX_Datatype_extent(datatype);
+    if (!comm || !ext || recvcount <= 0)
+        return 0;
+    return rsb_workspace((size_t) recvcount, ext, comm->size,
+                         rsb_choose(algorithm, (size_t) recvcount, ext, comm->size));
+}
+
+int MPIX_Reduce_scatter_block(const void *sendbuf, void *recvbuf, MPIX_Aint recvcount,
+                              MPIX_Datatype datatype, MPIX_Op op, MPIX_Comm comm, int algorithm,
+                              void *workspace, size_t workspace_bytes)
+{
+    return rsb_entry(sendbuf, recvbuf, recvcount, datatype, op, comm, algorithm, workspace,
+                     workspace_bytes, comm ? (comm->stream ? comm->stream : comm->own_stream) : 0,
+                     true);
+}
+
+int MPIX_Reduce_scatter_block_async(const void *sendbuf, void *recvbuf, MPIX_Aint recvcount,
+                                    MPIX_Datatype datatype, MPIX_Op op, MPIX_Comm comm,
+                                    int algorithm, void *workspace, size_t workspace_bytes,
+                                    void *stream)
+{
+    return rsb_entry(sendbuf, recvbuf, recvcount, datatype, op, comm, algorithm, workspace,
+                     workspace_bytes, stream, false);
+}
+
+size_t MPIX_Allreduce_workspace(MPIX_Aint count, MPIX_Datatype datatype, MPIX_Comm comm)
+{
+    size_t ext = (size_t) MPIX_Datatype_extent(datatype);
+    if (!comm || !ext || count <= 0 || comm->size == 1)
+        return 0;
+    return round256((size_t) count * ext);
+}
+
+int MPIX_Allreduce(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Datatype datatype,
+                   MPIX_Op op, MPIX_Comm comm, int algorithm, void *workspace,
+                   size_t workspace_bytes)
+{
+    return allreduce_entry(sendbuf, recvbuf, count, datatype, op, comm, algorithm, workspace,
+                           workspace_bytes,
+                           comm ? (comm->stream ? comm->stream : comm->own_stream) : 0, true);
+}
+
+int MPIX_Allreduce_async(const void *sendbuf, void *recvbuf, MPIX_Aint count,
+                         MPIX_Datatype datatype, MPIX_Op op, MPIX_Comm comm, int algorithm,
+                         void *workspace, size_t workspace_bytes, void *stream)
+{
+    return allreduce_entry(sendbuf, recvbuf, count, datatype, op, comm, algorithm, workspace,
+                           workspace_bytes, stream, false);
+}
+
+}  // extern "C"

@@ -143,3 +143,9 @@ def allreduce_rabenseifner(sendbufs, count, datatype, op, algorithm='reduce_scat
 
 def wtime():
     return lib().oracle_wtime()
+
+
+def combine_fn_address():
+    """address of oracle_combine (MPIX_Combine_fn signature), for installing
+    the oracle as the combine of a host-memory libmpix_coll communicator"""
+    return ctypes.cast(lib().oracle_combine, ctypes.c_void_p).value

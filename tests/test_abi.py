@@ -10,10 +10,11 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, 'include', 'mpix_redop.h')
+COLL_HEADER = os.path.join(ROOT, 'include', 'mpix_coll.h')
 
 
-def declared_symbols():
-    src = open(HEADER).read()
+def declared_symbols(header=HEADER):
+    src = open(header).read()
     src = re.sub(r'/\*.*?\*/', '', src, flags=re.S)
     funcs = set(re.findall(r'\b(MPIX_\w+)\s*\(', src))
     funcs -= {m for m in funcs if re.search(r'#define\s+' + m + r'\b', src)}
@@ -32,6 +33,17 @@ def test_library_exports_every_declared_symbol(R):
     L = R.lib()
     syms = declared_symbols()
     assert len(syms) >= 30
+    missing = [s for s in sorted(syms) if not hasattr(L, s)]
+    assert not missing, missing
+
+
+def test_coll_library_exports_every_declared_symbol(R):
+    """libmpix_coll.so (include/mpix_coll.h) loads without a GPU and exports
+    every function it declares"""
+    from mpich_amd import ccl
+    L = ccl.lib()
+    syms = declared_symbols(COLL_HEADER)
+    assert len(syms) >= 15
     missing = [s for s in sorted(syms) if not hasattr(L, s)]
     assert not missing, missing
 

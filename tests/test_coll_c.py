@@ -1,0 +1,332 @@
+"""libmpix_coll.so -- the C++ restatement of MPICH's reduce-scatter and
+allreduce schedules (include/mpix_coll.h) -- driven with P in-process ranks,
+one thread each.
+
+CPU: the host-memory transport with the oracle installed as the combine
+(the product has no CPU compute path), checked bit-for-bit against the
+oracle's single-process simulation of the reference schedules
+(reduce_scatter_block_intra_recursive_halving.c:38-260, …_pairwise.c:42-104,
+allreduce_intra_reduce_scatter_allgather.c:41-277,
+allreduce_intra_recursive_doubling.c:24-150), against the redscatblk3.c
+closed form and against every allred.c KAT generated for that world size.
+
+GPU: the device transport (stream-ordered device-to-device copies with event
+hand-offs) and the HIP combine, all ranks on cuda:0 -- the same schedules
+with the product kernels, bit-identical to the oracle's simulation.
+"""
+import ctypes
+import threading
+
+import numpy as np
+import pytest
+
+from tests import golden_util as gu
+
+MPI_FLOAT, MPI_DOUBLE, MPI_INT = 0x4c00040a, 0x4c00080b, 0x4c000405
+MPI_2INT = 0x4c000816
+MPI_SUM, MPI_PROD, MPI_MAX, MPI_BXOR, MPI_MAXLOC = 0x58000003, 0x58000004, 0x58000001, \
+    0x5800000a, 0x5800000c
+
+
+def run_ranks(comms, fn, timeout=120):
+    """fn(rank, comm) on one thread per rank (ctypes drops the GIL inside the
+    C calls, so the ranks really run concurrently); returns fn's results"""
+    out = [None] * len(comms)
+
+    def body(r):
+        try:
+            out[r] = fn(r, comms[r])
+        except BaseException as e:      # noqa: B902 -- reported below
+            out[r] = e
+    ths = [threading.Thread(target=body, args=(r,)) for r in range(len(comms))]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(timeout)
+        assert not t.is_alive(), 'rank thread hung'
+    for r, x in enumerate(out):
+        if isinstance(x, BaseException):
+            raise AssertionError('rank %d: %r' % (r, x))
+    return out
+
+
+def host_comms(P, oracle):
+    from mpich_amd import ccl
+    comms = ccl.comm_create_local(P)
+    for c in comms:
+        c.set_combine(oracle.combine_fn_address())
+    return comms
+
+
+def free_all(comms):
+    for c in comms:
+        assert c.free() == 0
+
+
+def float_sends(P, n, seed=0x5EED0100):
+    return [np.random.default_rng(seed + r).uniform(-1, 1, n).astype(np.float32)
+            for r in range(P)]
+
+
+# ------------------------------------------------------------------ CPU
+@pytest.mark.parametrize('algo', ['recursive_halving', 'pairwise', 'pairwise_sequential'])
+@pytest.mark.parametrize('P', [1, 2, 3, 4, 5, 7, 8])
+def test_rsb_host_matches_oracle_schedule(oracle, P, algo):
+    from mpich_amd import ccl
+    recvcount = 1001
+    sends = float_sends(P, P * recvcount)
+    recvs = [np.zeros(recvcount, np.float32) for _ in range(P)]
+    comms = host_comms(P, oracle)
+    rcs = run_ranks(comms, lambda r, c: ccl.reduce_scatter_block(sends[r], recvs[r], recvcount,
+                                                                  MPI_FLOAT, MPI_SUM, c, algo))
+    free_all(comms)
+    assert rcs == [0] * P
+    sim = oracle.rsb_pairwise if algo.startswith('pairwise') else oracle.rsb_recursive_halving
+    exp = sim([s.view(np.uint8) for s in sends], recvcount, MPI_FLOAT, MPI_SUM)
+    for r in range(P):
+        assert recvs[r].tobytes() == exp[r].tobytes(), r
+
+
+@pytest.mark.parametrize('algo', ['recursive_halving', 'pairwise', 'auto'])
+@pytest.mark.parametrize('P', [2, 3, 4, 6, 8])
+def test_rsb_host_redscatblk3(oracle, P, algo):
+    """redscatblk3.c:43-56: block i of rank r holds r + i; the result on rank
+    r is P*r + P*(P-1)/2 everywhere"""
+    from mpich_amd import ccl
+    recvcount = (1 << 20) // P // 64
+    sends = [np.concatenate([np.full(recvcount, r + i, np.int32) for i in range(P)])
+             for r in range(P)]
+    recvs = [np.zeros(recvcount, np.int32) for _ in range(P)]
+    comms = host_comms(P, oracle)
+    rcs = run_ranks(comms, lambda r, c: ccl.reduce_scatter_block(sends[r], recvs[r], recvcount,
+                                                                  MPI_INT, MPI_SUM, c, algo))
+    free_all(comms)
+    assert rcs == [0] * P
+    for r in range(P):
+        assert np.all(recvs[r] == P * r + P * (P - 1) // 2), r
+
+
+@pytest.mark.parametrize('algo', ['reduce_scatter_allgather', 'rsag_rd_allgather',
+                                  'recursive_doubling'])
+@pytest.mark.parametrize('P', [1, 2, 3, 4, 7, 8])
+def test_allreduce_host_matches_oracle_and_kats(oracle, P, algo):
+    from mpich_amd import ccl
+    count = 1037
+    sends = float_sends(P, count, 0x5EED0200)
+    recvs = [np.zeros(count, np.float32) for _ in range(P)]
+    comms = host_comms(P, oracle)
+    rcs = run_ranks(comms, lambda r, c: ccl.allreduce(sends[r], recvs[r], count, MPI_FLOAT,
+                                                       MPI_SUM, c, algo))
+    assert rcs == [0] * P
+    exp = oracle.allreduce_rabenseifner(
+        [s.view(np.uint8) for s in sends], count, MPI_FLOAT, MPI_SUM,
+        algorithm='recursive_doubling' if algo == 'recursive_doubling' else
+        'reduce_scatter_allgather')
+    for r in range(P):
+        assert recvs[r].tobytes() == exp[r].tobytes(), r
+    # the allred.c KATs generated for this world size, every op and type
+    pof2 = 1 << (P.bit_length() - 1)
+    ncase = 0
+    for case in gu.load_cases():
+        if case['nranks'] != P or not case['name'].startswith('allred '):
+            continue
+        if algo != 'recursive_doubling' and case['count'] < pof2:
+            continue
+        ext = len(case['expected']) // case['count']
+        outs = [np.zeros(case['count'] * ext, np.uint8) for _ in range(P)]
+        ins = [np.ascontiguousarray(case['inputs'][r]) for r in range(P)]
+        rcs = run_ranks(comms, lambda r, c: ccl.allreduce(ins[r], outs[r], case['count'],
+                                                           case['datatype'], case['op'], c, algo))
+        assert rcs == [0] * P, case['id']
+        for r in range(P):
+            assert not gu.mismatches(case, outs[r]), (case['id'], r)
+        ncase += 1
+    free_all(comms)
+    if P in (4, 7):
+        assert ncase > 0
+
+
+def test_in_place_allreduce_and_workspace(oracle):
+    """MPI_IN_PLACE (sendbuf None) and a caller-provided workspace"""
+    import torch
+    from mpich_amd import ccl
+    P, count = 4, 4099
+    sends = float_sends(P, count, 7)
+    bufs = [s.copy() for s in sends]
+    comms = host_comms(P, oracle)
+    need = ccl.allreduce_workspace_bytes(count, MPI_FLOAT, comms[0])
+    assert need >= count * 4
+    wss = [torch.zeros(need, dtype=torch.uint8) for _ in range(P)]
+    rcs = run_ranks(comms, lambda r, c: ccl.allreduce(None, bufs[r], count, MPI_FLOAT, MPI_SUM, c,
+                                                       workspace=wss[r]))
+    assert rcs == [0] * P
+    exp = oracle.allreduce_rabenseifner([s.view(np.uint8) for s in sends], count, MPI_FLOAT,
+                                        MPI_SUM)
+    for r in range(P):
+        assert bufs[r].tobytes() == exp[r].tobytes()
+    # a too-small workspace is an argument error, detected before any exchange
+    small = torch.zeros(16, dtype=torch.uint8)
+    assert ccl.allreduce(None, bufs[0], count, MPI_FLOAT, MPI_SUM, comms[0], workspace=small) == 12
+    free_all(comms)
+
+
+def test_argument_errors(oracle):
+    from mpich_amd import ccl
+    from mpich_amd import handles as H
+    comms = host_comms(2, oracle)
+    a = np.zeros(8, np.float32)
+    b = np.zeros(4, np.float32)
+    c0 = comms[0]
+    assert ccl.reduce_scatter_block(a, b, -1, MPI_FLOAT, MPI_SUM, c0) == H.MPI_ERR_COUNT
+    assert ccl.reduce_scatter_block(a, b, 4, MPI_FLOAT, MPI_BXOR, c0) == H.MPI_ERR_OP
+    assert ccl.reduce_scatter_block(None, b, 4, MPI_FLOAT, MPI_SUM, c0) == H.MPI_ERR_BUFFER
+    assert ccl.reduce_scatter_block(a, b, 4, MPI_FLOAT, MPI_SUM, c0, 9) == H.MPI_ERR_ARG
+    assert ccl.reduce_scatter_block(a, b, 0, MPI_FLOAT, MPI_SUM, c0) == 0
+    # the reduce-scatter+allgather allreduce needs count >= pof2 (:127)
+    assert ccl.allreduce(a, a, 1, MPI_FLOAT, MPI_SUM, c0, 'reduce_scatter_allgather') == \
+        H.MPI_ERR_COUNT
+    assert ccl.allreduce(a, a, 8, MPI_FLOAT, MPI_SUM, c0, 7) == H.MPI_ERR_ARG
+    free_all(comms)
+
+
+def test_custom_transport_and_symbols(oracle):
+    """MPIX_Comm_create_custom with a caller exchange function (here a
+    1-rank loop that must never be called) and the exported symbol set"""
+    from mpich_amd import ccl
+    L = ccl.lib()
+    calls = []
+    XFN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                           ctypes.c_int, ctypes.c_void_p)
+    fn = XFN(lambda ctx, rank, ops, nops, stream: calls.append(nops) or 0)
+    h = ctypes.c_void_p()
+    assert L.MPIX_Comm_create_custom(0, 1, ctypes.cast(fn, ctypes.c_void_p), None, 1,
+                                     ctypes.byref(h)) == 0
+    c = ccl.Comm(h.value)
+    c.set_combine(oracle.combine_fn_address())
+    x = np.arange(10, dtype=np.float32)
+    y = np.zeros(10, np.float32)
+    assert ccl.reduce_scatter_block(x, y, 10, MPI_FLOAT, MPI_SUM, c) == 0
+    assert np.array_equal(x, y) and calls == []
+    assert c.free() == 0
+
+
+# ------------------------------------------------------------------ GPU
+def _dev_comms(P):
+    from mpich_amd import ccl
+    return ccl.comm_create_local(P, [0] * P)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('algo', ['recursive_halving', 'pairwise', 'pairwise_sequential'])
+@pytest.mark.parametrize('P', [2, 3, 4, 8])
+def test_rsb_device_local_matches_oracle(oracle, P, algo):
+    import torch
+    from mpich_amd import ccl
+    recvcount = (1 << 18) + 13
+    sends = float_sends(P, P * recvcount)
+    dsend = [torch.from_numpy(s).cuda() for s in sends]
+    drecv = [torch.zeros(recvcount, dtype=torch.float32, device='cuda') for _ in range(P)]
+    torch.cuda.synchronize()
+    comms = _dev_comms(P)
+    rcs = run_ranks(comms, lambda r, c: ccl.reduce_scatter_block(dsend[r], drecv[r], recvcount,
+                                                                  MPI_FLOAT, MPI_SUM, c, algo))
+    free_all(comms)
+    assert rcs == [0] * P
+    sim = oracle.rsb_pairwise if algo.startswith('pairwise') else oracle.rsb_recursive_halving
+    exp = sim([s.view(np.uint8) for s in sends], recvcount, MPI_FLOAT, MPI_SUM)
+    for r in range(P):
+        assert drecv[r].cpu().numpy().tobytes() == exp[r].tobytes(), r
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('dt,op', [(MPI_INT, MPI_PROD), (MPI_DOUBLE, MPI_MAX),
+                                   (MPI_INT, MPI_BXOR), (MPI_2INT, MPI_MAXLOC)])
+@pytest.mark.parametrize('algo', ['recursive_halving', 'pairwise'])
+def test_rsb_device_local_types(oracle, dt, op, algo):
+    import torch
+    from mpich_amd import ccl
+    P, recvcount = 5, 4097
+    ext = oracle.extent(dt)
+    rng = np.random.default_rng(0x5EED0003)
+    if dt == MPI_2INT:      # values in 0..3 force ties (loc = min)
+        sends = [rng.integers(0, 4, (P * recvcount, 2)).astype(np.int32) for _ in range(P)]
+    elif dt == MPI_DOUBLE:
+        sends = [rng.uniform(-1, 1, P * recvcount) for _ in range(P)]
+    else:
+        sends = [rng.integers(-2**31, 2**31, P * recvcount).astype(np.int32) for _ in range(P)]
+    dsend = [torch.from_numpy(np.ascontiguousarray(s).view(np.uint8).reshape(-1)).cuda()
+             for s in sends]
+    drecv = [torch.zeros(recvcount * ext, dtype=torch.uint8, device='cuda') for _ in range(P)]
+    torch.cuda.synchronize()
+    comms = _dev_comms(P)
+    rcs = run_ranks(comms, lambda r, c: ccl.reduce_scatter_block(dsend[r], drecv[r], recvcount,
+                                                                  dt, op, c, algo))
+    free_all(comms)
+    assert rcs == [0] * P
+    sim = oracle.rsb_pairwise if algo == 'pairwise' else oracle.rsb_recursive_halving
+    exp = sim([np.ascontiguousarray(s).view(np.uint8).reshape(-1) for s in sends], recvcount,
+              dt, op)
+    for r in range(P):
+        assert drecv[r].cpu().numpy().tobytes() == exp[r].tobytes(), r
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('algo', ['reduce_scatter_allgather', 'rsag_rd_allgather',
+                                  'recursive_doubling'])
+@pytest.mark.parametrize('P', [2, 3, 4, 7, 8])
+def test_allreduce_device_local_matches_oracle(oracle, P, algo):
+    import torch
+    from mpich_amd import ccl
+    count = (1 << 18) + 37
+    sends = float_sends(P, count, 0x5EED0200)
+    dsend = [torch.from_numpy(s).cuda() for s in sends]
+    drecv = [torch.zeros(count, dtype=torch.float32, device='cuda') for _ in range(P)]
+    torch.cuda.synchronize()
+    comms = _dev_comms(P)
+    for rep in range(2):        # the second call reuses the communicators' scratch
+        rcs = run_ranks(comms, lambda r, c: ccl.allreduce(dsend[r], drecv[r], count, MPI_FLOAT,
+                                                           MPI_SUM, c, algo))
+        assert rcs == [0] * P
+    free_all(comms)
+    exp = oracle.allreduce_rabenseifner(
+        [s.view(np.uint8) for s in sends], count, MPI_FLOAT, MPI_SUM,
+        algorithm='recursive_doubling' if algo == 'recursive_doubling' else
+        'reduce_scatter_allgather')
+    for r in range(P):
+        assert drecv[r].cpu().numpy().tobytes() == exp[r].tobytes(), r
+
+
+@pytest.mark.gpu
+def test_async_on_caller_streams_back_to_back(oracle):
+    """stream-ordered form on each rank's own torch stream, three collectives
+    queued back to back without host synchronisation in between: the event
+    hand-offs alone must order the copies against the combines"""
+    import torch
+    from mpich_amd import ccl
+    P, recvcount = 4, 100003
+    sends = float_sends(P, P * recvcount, 99)
+    dsend = [torch.from_numpy(s).cuda() for s in sends]
+    outs = [[torch.zeros(recvcount, dtype=torch.float32, device='cuda') for _ in range(3)]
+            for _ in range(P)]
+    streams = [torch.cuda.Stream() for _ in range(P)]
+    torch.cuda.synchronize()
+    comms = _dev_comms(P)
+
+    def body(r, c):
+        rc = []
+        for k, algo in enumerate(['recursive_halving', 'pairwise', 'recursive_halving']):
+            rc.append(ccl.reduce_scatter_block(dsend[r], outs[r][k], recvcount, MPI_FLOAT,
+                                               MPI_SUM, c, algo, stream=streams[r],
+                                               blocking=False))
+        streams[r].synchronize()
+        return rc
+    rcs = run_ranks(comms, body)
+    free_all(comms)
+    assert rcs == [[0, 0, 0]] * P
+    rh = oracle.rsb_recursive_halving([s.view(np.uint8) for s in sends], recvcount, MPI_FLOAT,
+                                      MPI_SUM)
+    pw = oracle.rsb_pairwise([s.view(np.uint8) for s in sends], recvcount, MPI_FLOAT, MPI_SUM)
+    for r in range(P):
+        assert outs[r][0].cpu().numpy().tobytes() == rh[r].tobytes()
+        assert outs[r][1].cpu().numpy().tobytes() == pw[r].tobytes()
+        assert outs[r][2].cpu().numpy().tobytes() == rh[r].tobytes()
