@@ -357,6 +357,8 @@ def main():
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.barrier()
+        if _CCL.get('comm') is not None:
+            _CCL.pop('comm').free()
         dist.destroy_process_group()
 
 
@@ -435,11 +437,75 @@ def rsb_bench(args, world, rank, dev):
 
         except Exception as e:          # keep the other algorithms' figures
             out[algo] = dict(error='%s: %s' % (type(e).__name__, e))
-    del send, recv, ws
+    del ws
+    torch.cuda.empty_cache()
+    # the same schedules as C++ host code (libmpix_coll.so) on their own RCCL
+    # communicator: no Python between the steps
+    cc = ccl_comm() if p2p_ok else None
+    for algo in ('recursive_halving', 'pairwise'):
+        key = 'c_' + algo
+        if cc is None:
+            out[key] = dict(skipped='no RCCL communicator (%s)' % _CCL.get('error', 'gloo'))
+            continue
+        try:
+            from mpich_amd import ccl
+            rc_small = 4096 + 3
+            blk = torch.cat([torch.full((rc_small,), rank + i, dtype=torch.int32, device=dev)
+                             for i in range(world)])
+            o = torch.empty(rc_small, dtype=torch.int32, device=dev)
+            torch.cuda.synchronize()
+            redop.check(ccl.reduce_scatter_block(blk, o, rc_small, H.MPI_INT, H.MPI_SUM, cc, algo),
+                        'MPIX_Reduce_scatter_block')
+            ok = allreduce_scalar(1 if bool(torch.all(o == world * rank + world * (world - 1) // 2))
+                                  else 0, dist.ReduceOp.MIN, dev)
+
+            def once():
+                redop.check(ccl.reduce_scatter_block(send, recv, recvcount, H.MPI_FLOAT, H.MPI_SUM,
+                                                     cc, algo), 'MPIX_Reduce_scatter_block')
+            once()
+            reps = max(3, min(10, args.steps))
+            dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                once()
+            torch.cuda.synchronize()
+            dist.barrier()
+            t = (time.perf_counter() - t0) / reps
+            t = allreduce_scalar(t, dist.ReduceOp.MAX, dev)
+            busbytes = (world - 1) / world * total * 4
+            if algo == 'recursive_halving':
+                link_bytes, links = (pof2 - 1) / pof2 * total * 4, 1
+            else:
+                link_bytes, links = total * 4 / world, world - 1
+            out[key] = dict(parity_redscatblk3_all_ranks=bool(ok), ms=round(t * 1e3, 3),
+                            busbw_GBs=round(busbytes / t / 1e9, 2),
+                            per_link_GBs=round(link_bytes / t / 1e9, 2), links_active=links,
+                            frac_of_xgmi_link=round(link_bytes / t / 1e9 / 153.0, 4))
+        except Exception as e:
+            out[key] = dict(error='%s: %s' % (type(e).__name__, e))
+    del send, recv
     torch.cuda.empty_cache()
     out.update(P=world, bytes_per_rank=total * 4, recvcount=recvcount,
                xgmi_link_GBs_assumed=153.0)
     return out
+
+
+_CCL = {}
+
+
+def ccl_comm():
+    """one libmpix_coll RCCL communicator per process (MPIR_RCCLcomm_init,
+    rccl.c:21-52: rank 0's unique id broadcast over the process group).
+    Every rank always reaches the collective init, so a failure cannot leave
+    the others waiting in ncclCommInitRank."""
+    if 'comm' not in _CCL and 'error' not in _CCL:
+        try:
+            from mpich_amd import ccl
+            _CCL['comm'] = ccl.comm_create_ccl_from_process_group()
+        except Exception as e:
+            _CCL['error'] = '%s: %s' % (type(e).__name__, e)
+    return _CCL.get('comm')
 
 
 def allreduce_bench(args, world, rank, dev):
@@ -486,6 +552,31 @@ def allreduce_bench(args, world, rank, dev):
         t = allreduce_scalar(t, dist.ReduceOp.MAX, dev)
         res[name] = dict(ms=round(t * 1e3, 3),
                          busbw_GBs=round(2 * (world - 1) / world * n * 4 / t / 1e9, 2))
+    cc = ccl_comm()
+    if cc is None:
+        res['c_reduce_scatter_allgather'] = dict(skipped=_CCL.get('error', 'no communicator'))
+    else:
+        from mpich_amd import ccl
+
+        def c_ar():
+            redop.check(ccl.allreduce(send, recv, n, H.MPI_FLOAT, H.MPI_SUM, cc,
+                                      'reduce_scatter_allgather', workspace=ws), 'MPIX_Allreduce')
+        try:
+            c_ar()
+            reps = max(3, min(10, args.steps))
+            dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                c_ar()
+            torch.cuda.synchronize()
+            dist.barrier()
+            t = (time.perf_counter() - t0) / reps
+            t = allreduce_scalar(t, dist.ReduceOp.MAX, dev)
+            res['c_reduce_scatter_allgather'] = dict(
+                ms=round(t * 1e3, 3), busbw_GBs=round(2 * (world - 1) / world * n * 4 / t / 1e9, 2))
+        except Exception as e:
+            res['c_reduce_scatter_allgather'] = dict(error='%s: %s' % (type(e).__name__, e))
     del send, recv, ws
     torch.cuda.empty_cache()
     return res

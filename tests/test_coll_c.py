@@ -330,3 +330,27 @@ def test_async_on_caller_streams_back_to_back(oracle):
         assert outs[r][0].cpu().numpy().tobytes() == rh[r].tobytes()
         assert outs[r][1].cpu().numpy().tobytes() == pw[r].tobytes()
         assert outs[r][2].cpu().numpy().tobytes() == rh[r].tobytes()
+
+
+@pytest.mark.gpu
+def test_rccl_communicator_single_rank():
+    """MPIX_Comm_create_ccl (MPIR_RCCLcomm_init, rccl.c:21-52) on the test
+    box's one GPU: unique id, ncclCommInitRank with one rank, the P = 1
+    collectives (a local copy, coll_api.txt:402-411) and MPIX_Comm_free.
+    The P > 1 RCCL exchanges run in the driver's multi-GPU bench, which checks
+    the redscatblk3.c closed form on every rank first."""
+    import torch
+    from mpich_amd import ccl
+    uid = ccl.get_unique_id()
+    assert len(uid) == ccl.UNIQUE_ID_BYTES and any(uid)
+    c = ccl.comm_create_ccl(0, 1, uid)
+    assert (c.rank, c.size) == (0, 1)
+    x = torch.arange(1000, dtype=torch.float32, device='cuda')
+    y = torch.zeros_like(x)
+    torch.cuda.synchronize()
+    assert ccl.reduce_scatter_block(x, y, 1000, MPI_FLOAT, MPI_SUM, c) == 0
+    assert torch.equal(x, y)
+    z = torch.zeros_like(x)
+    assert ccl.allreduce(x, z, 1000, MPI_FLOAT, MPI_SUM, c) == 0
+    assert torch.equal(x, z)
+    assert c.free() == 0
