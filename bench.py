@@ -57,6 +57,8 @@ def parse():
     p.add_argument('--sweep', action='store_true', help='config 2 chunk/size sweep')
     p.add_argument('--rsb', action='store_true', help='time reduce_scatter_block even at N=1')
     p.add_argument('--rsb-bytes', type=int, default=4 << 30, help='RSB vector bytes per rank')
+    p.add_argument('--extras-timeout', type=float, default=300.0,
+                   help='watchdog (s) over the N>1 collective figures and teardown')
     p.add_argument('--pmc', default=os.path.join(ROOT, 'profiles', 'r01_pmc_summary.json'),
                    help='PMC traffic summary (from tools/pmc_summary.py) to quote as traffic')
     return p.parse_args()
@@ -341,36 +343,90 @@ def main():
     del inout, inb
     torch.cuda.empty_cache()
 
+    # The headline is complete here.  Everything after it (collective
+    # figures, teardown) runs under a watchdog: if a secondary collective
+    # hangs on some rank, rank 0 still prints the line (with what it has)
+    # and every rank leaves, instead of the job dying silently at the
+    # driver's limit.
+    emit = _Emitter(rank, result)
+    dog = None
     if world > 1 or args.rsb:
-        try:
-            result['reduce_scatter_block'] = rsb_bench(args, world, rank, dev)
-        except Exception as e:      # secondary figure: never lose the headline line
-            result['reduce_scatter_block'] = dict(error='%s: %s' % (type(e).__name__, e))
-        try:
-            result['allreduce'] = allreduce_bench(args, world, rank, dev)
-        except Exception as e:
-            result['allreduce'] = dict(error='%s: %s' % (type(e).__name__, e))
+        dog = _watchdog(args.extras_timeout, emit)
+        result['extras_timeout_s'] = args.extras_timeout
+        if os.environ.get('MPIX_BENCH_STALL_RANK') == str(rank):
+            time.sleep(1e6)     # rehearsal knob: a rank that never arrives
+        # filled in place, so a watchdog line carries the figures already taken
+        for key, fn in (('reduce_scatter_block', rsb_bench), ('allreduce', allreduce_bench)):
+            part = result[key] = {}
+            try:
+                fn(args, world, rank, dev, part)
+            except Exception as e:  # secondary figure: never lose the headline line
+                part['error'] = '%s: %s' % (type(e).__name__, e)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result['cpu_baseline'] = cpu_baseline(args.cpu_seconds, args.count)
-    if rank == 0:
-        print(json.dumps(result), flush=True)
+    emit.emit()
     if world > 1:
-        dist.barrier()
-        if _CCL.get('comm') is not None:
-            _CCL.pop('comm').free()
-        dist.destroy_process_group()
+        try:
+            dist.barrier()
+            if _CCL.get('comm') is not None:
+                _CCL.pop('comm').free()
+            dist.destroy_process_group()
+        except Exception as e:  # a peer already left (its error is in the line)
+            print('teardown: %s: %s' % (type(e).__name__, e), file=sys.stderr, flush=True)
+    if dog is not None:
+        dog.cancel()
 
 
-def rsb_bench(args, world, rank, dev):
+class _Emitter:
+    """prints rank 0's one JSON line exactly once, from whichever thread
+    (main, or the watchdog) gets there first"""
+
+    def __init__(self, rank, result):
+        import threading
+        self.rank, self.result, self.done = rank, result, False
+        self.lock = threading.Lock()
+
+    def emit(self, note=None):
+        with self.lock:
+            if self.done:
+                return
+            self.done = True
+            if self.rank != 0:
+                return
+            r = dict(self.result)
+            if note:
+                r['extras_watchdog'] = note
+                for k in ('reduce_scatter_block', 'allreduce'):
+                    part = dict(r.get(k) or {})
+                    part.setdefault('error', 'not finished: ' + note)
+                    r[k] = part
+            print(json.dumps(r, default=str), flush=True)
+
+
+def _watchdog(seconds, emit):
+    import threading
+
+    def fire():
+        emit.emit('secondary collectives exceeded %.0f s; headline kept, rank exits' % seconds)
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
+    t = threading.Timer(seconds, fire)
+    t.daemon = True
+    t.start()
+    return t
+
+
+def rsb_bench(args, world, rank, dev, out):
     """BASELINE config 4: MPI_Reduce_scatter_block fp32 SUM, fixed vector per
     rank (strong scaling): the reference's recursive-halving schedule and
     the pairwise one over RCCL/xGMI (all links at once), and the fused
     pull + combine kernel over hipIpc-mapped peer buffers."""
     from mpich_amd import coll
     if world == 1 or not dist.is_initialized():
-        return dict(note='P=1 is a local copy (coll_api.txt:402-411); see value for the combine')
-    out = {}
+        out['note'] = 'P=1 is a local copy (coll_api.txt:402-411); see value for the combine'
+        return out
     total = args.rsb_bytes // 4
     recvcount = total // world
     total = recvcount * world
@@ -508,7 +564,7 @@ def ccl_comm():
     return _CCL.get('comm')
 
 
-def allreduce_bench(args, world, rank, dev):
+def allreduce_bench(args, world, rank, dev, res):
     """MPI_Allreduce fp32 SUM, 1 GiB per rank: the reference's
     reduce-scatter + allgather schedule on RCCL point-to-point + the HIP
     combine (bit-identical to the reference association), next to RCCL's own
@@ -516,9 +572,11 @@ def allreduce_bench(args, world, rank, dev):
     MPIR_Allreduce_intra_ccl route, rccl.c:223) as the comparator."""
     from mpich_amd import coll
     if world == 1 or not dist.is_initialized():
-        return dict(note='P=1 is a local copy')
+        res['note'] = 'P=1 is a local copy'
+        return res
     if dist.get_backend() != 'nccl':
-        return dict(skipped='needs the nccl (RCCL) backend')
+        res['skipped'] = 'needs the nccl (RCCL) backend'
+        return res
     # parity: allred.c sum_test_1 closed form (in = i, sol = i*P), on device
     m = 100003
     x = torch.arange(m, dtype=torch.int32, device=dev)
@@ -531,7 +589,7 @@ def allreduce_bench(args, world, rank, dev):
     fill_uniform(send, 0x5EED0200 + rank)
     recv = torch.empty_like(send)
     ws = torch.empty(n * 4, dtype=torch.uint8, device=dev)
-    res = dict(parity_allred_sum_test_1_all_ranks=bool(ok), bytes_per_rank=n * 4, P=world)
+    res.update(parity_allred_sum_test_1_all_ranks=bool(ok), bytes_per_rank=n * 4, P=world)
     for name, fn in (('mpich_schedule_hip_combine',
                       lambda: coll.allreduce(send, recv, n, H.MPI_FLOAT, H.MPI_SUM, extent=4,
                                              workspace=ws)),
