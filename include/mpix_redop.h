@@ -183,15 +183,30 @@ int MPIX_Reduce_local_vector(const void *inbuf, void *inoutbuf, MPIX_Aint count,
                              MPIX_Datatype basic_type, MPIX_Op op);
 
 /* General derived target given as its flattened iov, packed source --
- * typerep_op_fallback (typerep_op.c:100-150) for a basic (non-pair) type:
- * for s < nseg, in segment order, seg_counts[s] elements at byte offset
- * seg_offsets[s] of inoutbuf are combined with the next seg_counts[s]
- * elements of inbuf.  Offsets must be multiples of the type's extent and
- * segments must not overlap (MPI accumulate targets).  The two tables are
- * host arrays, read before the call returns.  Device buffers. */
+ * typerep_op_fallback (typerep_op.c:100-150) with the target's iov already
+ * resolved to element runs: for s < nseg, in order, seg_counts[s] elements
+ * (extent stride) at byte offset seg_offsets[s] of inoutbuf are combined
+ * with the next seg_counts[s] elements of inbuf.  Offsets may be negative
+ * (lb < 0) and need only the 4-byte alignment of the element loads (2 for
+ * 2-byte types); runs must not overlap (MPI accumulate targets).  The
+ * tables are host arrays, read before the call returns.  Device buffers. */
 int MPIX_Reduce_local_iov_async(const void *inbuf, void *inoutbuf, MPIX_Aint nseg,
                                 const MPIX_Aint *seg_offsets, const MPIX_Aint *seg_counts,
                                 MPIX_Datatype basic_type, MPIX_Op op, void *stream);
+
+/* The same fallback over the raw iov, as MPIR_Typerep_to_iov_offset gives
+ * it (typerep_op.c:100-110): segment i is iov_lens[i] BYTES at byte offset
+ * iov_offsets[i] of inoutbuf.  For a basic type each segment must hold
+ * whole elements (the reference asserts, :147; here MPI_ERR_ARG).  For a
+ * pair type whose size is below its extent (DOUBLE_INT, LONG_INT,
+ * SHORT_INT: the padding splits each element into {value, int} segments)
+ * segments are gathered until they hold curr_len >= size bytes, then
+ * curr_len / size elements are combined at extent stride from the first
+ * gathered segment, and a partial element left at a segment's end starts
+ * the next run -- typerep_op.c:117-148 exactly. */
+int MPIX_Reduce_local_iovec_async(const void *inbuf, void *inoutbuf, MPIX_Aint nseg,
+                                  const MPIX_Aint *iov_offsets, const MPIX_Aint *iov_lens,
+                                  MPIX_Datatype basic_type, MPIX_Op op, void *stream);
 
 /* Multi-input form: equivalent to `ninputs` MPIX_Reduce_local calls
  *   for k = 0 .. ninputs-1:  inoutbuf = inoutbuf OP inbufs[k]
@@ -229,6 +244,10 @@ int MPIX_Redop_internal_op_dt_check(MPIX_Op op, MPIX_Datatype datatype);
 MPIX_Datatype MPIX_Datatype_internal(MPIX_Datatype datatype);
 /* Extent in bytes of one element (pair types include padding); 0 if unknown. */
 MPIX_Aint MPIX_Datatype_extent(MPIX_Datatype datatype);
+/* Size in bytes of one element's data (MPIR_Datatype_get_size_macro):
+ * the extent, except for the padded pairs DOUBLE_INT / LONG_INT (12),
+ * SHORT_INT (6) and LONG_DOUBLE_INT (20); 0 if unknown. */
+MPIX_Aint MPIX_Datatype_size(MPIX_Datatype datatype);
 
 /* Fortran .TRUE./.FALSE. used by LAND/LOR/LXOR on Fortran logicals
  * (mpii_fortlogical.h:15,28; defaults 1 / 0 as typeutil.c:502-510). */

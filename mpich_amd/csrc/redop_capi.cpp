@@ -17,6 +17,7 @@
 
 #include <atomic>
 #include <mutex>
+#include <vector>
 
 #include "mpix_redop.h"
 #include "redop_dispatch.h"
@@ -107,6 +108,59 @@ uint64_t extent_of(uint32_t it)
 bool is_pairtype(uint32_t it)
 {
     return is_struct_pair(it) || (is_builtin(it) && (it & 0x400000u));
+}
+
+int hip_err(hipError_t e);
+
+// Type map of the struct pairs (pairtypes.c:24-80: a struct {value @0,
+// int @idx_offset}, extent = sizeof the C struct).  DOUBLE_INT, LONG_INT,
+// SHORT_INT and LONG_DOUBLE_INT have size < extent: their padding is not
+// part of the type map, so a typemap copy (MPIR_Localcopy) leaves it alone
+// and typerep_op_fallback treats them as "pairtype" (typerep_op.c:88).
+struct PairMap {
+    uint32_t value_bytes, loc_off;
+};
+bool padded_pair(uint32_t it, PairMap *pm)
+{
+    static const PairMap m[5] = {{4, 4}, {8, 8}, {8, 8}, {2, 4}, {16, 16}};
+    if (!is_struct_pair(it) || (it & 0xff) == 0)
+        return false;
+    *pm = m[it & 0xff];
+    return true;
+}
+
+// MPIR_Datatype_get_size_macro: bytes of data in one element
+uint64_t size_of(uint32_t it)
+{
+    PairMap pm;
+    if (padded_pair(it, &pm))
+        return pm.value_bytes + 4;
+    return extent_of(it);
+}
+
+// MPI_REPLACE (op_fns.c:445-457) = MPIR_Localcopy: `rows` elements at the
+// given pitches.  Contiguous types copy whole extents; padded pairs copy the
+// value and the int of each element (two pitched copies), so inout keeps its
+// padding bytes exactly as the typemap copy does.
+int replace_rows(void *dst, size_t dpitch, const void *src, size_t spitch, uint64_t rows,
+                 uint32_t it, uint64_t ext, hipStream_t s)
+{
+    if (rows == 0)
+        return MPIX_REDOP_SUCCESS;
+    PairMap pm;
+    if (!padded_pair(it, &pm)) {
+        if (dpitch == ext && spitch == ext)
+            return hip_err(hipMemcpyAsync(dst, src, rows * ext, hipMemcpyDeviceToDevice, s));
+        return hip_err(hipMemcpy2DAsync(dst, dpitch, src, spitch, ext, rows,
+                                        hipMemcpyDeviceToDevice, s));
+    }
+    int rc = hip_err(hipMemcpy2DAsync(dst, dpitch, src, spitch, pm.value_bytes, rows,
+                                      hipMemcpyDeviceToDevice, s));
+    if (rc == MPIX_REDOP_SUCCESS)
+        rc = hip_err(hipMemcpy2DAsync((char *) dst + pm.loc_off, dpitch,
+                                      (const char *) src + pm.loc_off, spitch, 4, rows,
+                                      hipMemcpyDeviceToDevice, s));
+    return rc;
 }
 
 // MPIR_Internal_op_dt_check (mpir_datatype.h:870-933)
@@ -390,7 +444,7 @@ int enqueue(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext,
     if (opi == 14)      // MPI_NO_OP
         return MPIX_REDOP_SUCCESS;
     if (opi == 13)      // MPI_REPLACE = MPIR_Localcopy (op_fns.c:445-457)
-        return hip_err(hipMemcpyAsync(io, in, count * ext, hipMemcpyDeviceToDevice, s));
+        return replace_rows(io, ext, in, ext, count, it, ext, s);
     if (opi == 15)      // MPIX_EQUAL, MPI_BYTE only (opequal.c:22-23)
         return ((it & 0xffffff00u) == U8 && count >= 8)
             ? hip_err(mpix::launch_equal(in, io, count, s)) : MPIX_REDOP_ERR_TYPE;
@@ -521,6 +575,138 @@ struct DeviceGuard {
             (void) hipSetDevice(prev);
     }
 };
+
+// ------------------------------------------- derived targets as runs
+// One uop call of typerep_op_fallback: `n` elements at extent stride from
+// byte offset `off` of inout (may be negative: lb < 0), combined with the
+// next n elements of the packed source.
+struct Run {
+    int64_t off, n;
+};
+
+// Enqueue a list of runs on `s`.  Runs are split by their offset modulo the
+// extent so each launch indexes inout in whole elements from one base
+// (inout + residue); the source offset table keeps the packed source in the
+// original run order.  Residues must keep the 4-byte (2-byte for 2-byte
+// types) alignment the element loads need.
+int enqueue_runs(const void *inbuf, void *inoutbuf, const std::vector<Run> &runs, uint32_t dt,
+                 uint32_t op, hipStream_t s)
+{
+    uint32_t it;
+    uint64_t ext;
+    int rc = validate(inbuf, inoutbuf, 0, dt, op, &it, &ext);
+    if (rc != MPIX_REDOP_SUCCESS)
+        return rc;
+    int64_t total = 0;
+    for (const Run &r : runs)
+        total += r.n;
+    if (total == 0)
+        return MPIX_REDOP_SUCCESS;
+    if (!inbuf || !inoutbuf || inbuf == (const void *) -1 || inoutbuf == (void *) -1)
+        return MPIX_REDOP_ERR_BUFFER;
+    {
+        const void *pin, *pio;
+        if (!device_accessible(inbuf, &pin) || !device_accessible(inoutbuf, &pio))
+            return MPIX_REDOP_ERR_BUFFER;
+        inbuf = pin;
+        inoutbuf = (void *) pio;
+    }
+    const int64_t e = (int64_t) ext, align = e < 4 ? e : 4;
+    for (const Run &r : runs)
+        if ((((r.off % e) + e) % e) % align)
+            return MPIX_REDOP_ERR_ARG;
+    uint32_t opi = op & 0xf;
+    if (opi == 14)
+        return MPIX_REDOP_SUCCESS;
+    if (opi == 13) {    // REPLACE: one typemap copy per run
+        int64_t src = 0;
+        for (size_t k = 0; k < runs.size() && rc == MPIX_REDOP_SUCCESS; ++k) {
+            rc = replace_rows((char *) inoutbuf + runs[k].off, ext,
+                              (const char *) inbuf + src * e, ext, (uint64_t) runs[k].n, it, ext, s);
+            src += runs[k].n;
+        }
+        return rc;
+    }
+    const Entry *en = gpu_entry(opi, it);
+    if (!en)
+        return MPIX_REDOP_ERR_TYPE;
+    // group by residue; per group the table is [seg_off n][prefix n+1][src_off n]
+    std::vector<int64_t> resid;
+    std::vector<std::vector<size_t>> groups;
+    for (size_t k = 0; k < runs.size(); ++k) {
+        if (runs[k].n == 0)
+            continue;
+        int64_t r = ((runs[k].off % e) + e) % e;
+        size_t g = 0;
+        while (g < resid.size() && resid[g] != r)
+            ++g;
+        if (g == resid.size()) {
+            resid.push_back(r);
+            groups.emplace_back();
+        }
+        groups[g].push_back(k);
+    }
+    std::vector<int64_t> src_of(runs.size());
+    {
+        int64_t src = 0;
+        for (size_t k = 0; k < runs.size(); ++k) {
+            src_of[k] = src;
+            src += runs[k].n;
+        }
+    }
+    size_t need = 0;
+    for (const auto &g : groups)
+        need += 3 * g.size() + 1;
+    std::vector<int64_t> tab(need);
+    std::vector<size_t> base(groups.size());
+    std::vector<int64_t> gtotal(groups.size());
+    size_t at = 0;
+    for (size_t g = 0; g < groups.size(); ++g) {
+        const size_t n = groups[g].size();
+        base[g] = at;
+        int64_t pre = 0;
+        for (size_t q = 0; q < n; ++q) {
+            const Run &r = runs[groups[g][q]];
+            tab[at + q] = (r.off - resid[g]) / e;
+            tab[at + n + q] = pre;
+            tab[at + 2 * n + 1 + q] = src_of[groups[g][q]];
+            pre += r.n;
+        }
+        tab[at + 2 * n] = pre;
+        gtotal[g] = pre;
+        at += 3 * n + 1;
+    }
+    int dev = 0;
+    (void) hipGetDevice(&dev);
+    DevState *d = dev_state(dev);
+    if (!d)
+        return MPIX_REDOP_ERR_OTHER;
+    if (d->iov_cap < need) {
+        // the previous table may still be read by work queued on this stream
+        (void) hipStreamSynchronize(s);
+        if (d->iov_tab)
+            (void) hipFree(d->iov_tab);
+        d->iov_tab = nullptr;
+        d->iov_cap = 0;
+        if (hipMalloc((void **) &d->iov_tab, need * sizeof(int64_t)) != hipSuccess)
+            return MPIX_REDOP_ERR_OTHER;
+        d->iov_cap = need;
+    }
+    // pageable source: hipMemcpyAsync stages it, and the sync makes the
+    // host vector free to go; stream order keeps the new table behind
+    // earlier kernels that still read the old one
+    rc = hip_err(hipMemcpyAsync(d->iov_tab, tab.data(), need * sizeof(int64_t),
+                                hipMemcpyHostToDevice, s));
+    if (rc == MPIX_REDOP_SUCCESS)
+        rc = hip_err(hipStreamSynchronize(s));
+    for (size_t g = 0; g < groups.size() && rc == MPIX_REDOP_SUCCESS; ++g) {
+        const int64_t n = (int64_t) groups[g].size();
+        const int64_t *t = d->iov_tab + base[g];
+        rc = hip_err(en->iov(inbuf, (char *) inoutbuf + resid[g], t, t + n, t + 2 * n + 1, n,
+                             (uint64_t) gtotal[g], params(), launch_cfg(), s));
+    }
+    return rc;
+}
 
 }  // namespace
 
@@ -653,10 +839,23 @@ int MPIX_Reduce_local_vector_async(const void *inbuf, void *inoutbuf, MPIX_Aint 
     if (opi == 14)
         return set_err(MPIX_REDOP_SUCCESS);
     if (opi == 13) {
-        rc = hip_err(hipMemcpy2DAsync(inoutbuf, (size_t) stride * ext, inbuf,
-                                      (size_t) blocklen * ext, (size_t) blocklen * ext,
-                                      (size_t) count, hipMemcpyDeviceToDevice,
-                                      (hipStream_t) stream));
+        PairMap pm;
+        if (!padded_pair(it, &pm)) {
+            rc = hip_err(hipMemcpy2DAsync(inoutbuf, (size_t) stride * ext, inbuf,
+                                          (size_t) blocklen * ext, (size_t) blocklen * ext,
+                                          (size_t) count, hipMemcpyDeviceToDevice,
+                                          (hipStream_t) stream));
+        } else if (blocklen <= count) {     // column k of every block
+            for (MPIX_Aint k = 0; k < blocklen && rc == MPIX_REDOP_SUCCESS; ++k)
+                rc = replace_rows((char *) inoutbuf + k * ext, (size_t) stride * ext,
+                                  (const char *) inbuf + k * ext, (size_t) blocklen * ext,
+                                  (uint64_t) count, it, ext, (hipStream_t) stream);
+        } else {                            // block by block
+            for (MPIX_Aint b = 0; b < count && rc == MPIX_REDOP_SUCCESS; ++b)
+                rc = replace_rows((char *) inoutbuf + b * stride * ext, ext,
+                                  (const char *) inbuf + b * blocklen * ext, ext,
+                                  (uint64_t) blocklen, it, ext, (hipStream_t) stream);
+        }
         return set_err(rc);
     }
     const Entry *e = gpu_entry(opi, it);
@@ -691,92 +890,65 @@ int MPIX_Reduce_local_iov_async(const void *inbuf, void *inoutbuf, MPIX_Aint nse
 {
     if (nseg < 0)
         return set_err(MPIX_REDOP_ERR_COUNT);
-    uint32_t it;
-    uint64_t ext;
-    int rc = validate(inbuf, inoutbuf, 0, (uint32_t) basic_type, (uint32_t) op, &it, &ext);
-    if (rc != MPIX_REDOP_SUCCESS)
-        return set_err(rc);
-    if (nseg == 0)
-        return set_err(MPIX_REDOP_SUCCESS);
-    if (!seg_offsets || !seg_counts || !inbuf || !inoutbuf || inbuf == (const void *) -1 ||
-        inoutbuf == (void *) -1)
+    if (nseg > 0 && (!seg_offsets || !seg_counts))
         return set_err(MPIX_REDOP_ERR_BUFFER);
-    if (is_pairtype(it))
-        return set_err(MPIX_REDOP_ERR_TYPE);    // pair targets split across segments: not here
-    {
-        const void *pin, *pio;
-        if (!device_accessible(inbuf, &pin) || !device_accessible(inoutbuf, &pio))
-            return set_err(MPIX_REDOP_ERR_BUFFER);
-        inbuf = pin;
-        inoutbuf = (void *) pio;
-    }
-    // host-side tables: element offsets + prefix counts (2*nseg + 1 entries)
-    int64_t *tab = (int64_t *) malloc(sizeof(int64_t) * (2 * (size_t) nseg + 1));
-    if (!tab)
-        return set_err(MPIX_REDOP_ERR_OTHER);
-    int64_t total = 0;
+    std::vector<Run> runs;
+    runs.reserve((size_t) nseg);
     for (MPIX_Aint s = 0; s < nseg; ++s) {
-        if (seg_counts[s] < 0 || seg_offsets[s] % (MPIX_Aint) ext) {
-            free(tab);
-            return set_err(seg_counts[s] < 0 ? MPIX_REDOP_ERR_COUNT : MPIX_REDOP_ERR_ARG);
-        }
-        tab[s] = seg_offsets[s] / (int64_t) ext;
-        tab[nseg + s] = total;
-        total += seg_counts[s];
+        if (seg_counts[s] < 0)
+            return set_err(MPIX_REDOP_ERR_COUNT);
+        runs.push_back(Run{seg_offsets[s], seg_counts[s]});
     }
-    tab[2 * nseg] = total;
-    uint32_t opi = (uint32_t) op & 0xf;
-    if (opi == 14 || total == 0) {
-        free(tab);
-        return set_err(MPIX_REDOP_SUCCESS);
-    }
-    const Entry *e = opi == 13 ? nullptr : gpu_entry(opi, it);
-    if (!e && opi != 13) {
-        free(tab);
-        return set_err(MPIX_REDOP_ERR_TYPE);
-    }
-    if (opi == 13) {    // REPLACE: one copy per segment
-        for (MPIX_Aint s2 = 0; s2 < nseg && rc == MPIX_REDOP_SUCCESS; ++s2)
-            rc = hip_err(hipMemcpyAsync((char *) inoutbuf + seg_offsets[s2],
-                                        (const char *) inbuf + tab[nseg + s2] * ext,
-                                        (size_t) seg_counts[s2] * ext, hipMemcpyDeviceToDevice,
-                                        (hipStream_t) stream));
-        free(tab);
-        return set_err(rc);
-    }
-    int dev = 0;
-    (void) hipGetDevice(&dev);
-    DevState *d = dev_state(dev);
-    if (!d) {
-        free(tab);
-        return set_err(MPIX_REDOP_ERR_OTHER);
-    }
-    size_t need = 2 * (size_t) nseg + 1;
-    if (d->iov_cap < need) {
-        // the previous table may still be read by work queued on this stream
-        (void) hipStreamSynchronize((hipStream_t) stream);
-        if (d->iov_tab)
-            (void) hipFree(d->iov_tab);
-        d->iov_tab = nullptr;
-        d->iov_cap = 0;
-        if (hipMalloc((void **) &d->iov_tab, need * sizeof(int64_t)) != hipSuccess) {
-            free(tab);
-            return set_err(MPIX_REDOP_ERR_OTHER);
-        }
-        d->iov_cap = need;
-    }
-    // pageable source: the copy is complete (staged) when the call returns,
-    // and stream order keeps it behind earlier kernels that read the table
-    rc = hip_err(hipMemcpyAsync(d->iov_tab, tab, need * sizeof(int64_t), hipMemcpyHostToDevice,
+    return set_err(enqueue_runs(inbuf, inoutbuf, runs, (uint32_t) basic_type, (uint32_t) op,
                                 (hipStream_t) stream));
-    if (rc == MPIX_REDOP_SUCCESS)
-        rc = hip_err(hipStreamSynchronize((hipStream_t) stream));
-    free(tab);
-    if (rc != MPIX_REDOP_SUCCESS)
-        return set_err(rc);
-    return set_err(hip_err(e->iov(inbuf, inoutbuf, d->iov_tab, d->iov_tab + nseg, (int64_t) nseg,
-                                  (uint64_t) total, params(), launch_cfg(),
-                                  (hipStream_t) stream)));
+}
+
+int MPIX_Reduce_local_iovec_async(const void *inbuf, void *inoutbuf, MPIX_Aint nseg,
+                                  const MPIX_Aint *iov_offsets, const MPIX_Aint *iov_lens,
+                                  MPIX_Datatype basic_type, MPIX_Op op, void *stream)
+{
+    if (nseg < 0)
+        return set_err(MPIX_REDOP_ERR_COUNT);
+    if (nseg > 0 && (!iov_offsets || !iov_lens))
+        return set_err(MPIX_REDOP_ERR_BUFFER);
+    uint32_t it = to_internal((uint32_t) basic_type);
+    uint64_t ext = extent_of(it), size = size_of(it);
+    if (it == kNull || ext == 0)
+        return set_err(MPIX_REDOP_ERR_TYPE);
+    // typerep_op.c:115-149: segments are gathered until they hold one
+    // element's data (pairtypes split by their padding); each call covers
+    // curr_len / size elements laid out at extent stride from target_ptr,
+    // and a partial element left at the end of a segment starts the next one
+    const bool pairtype = size < ext;
+    std::vector<Run> runs;
+    runs.reserve((size_t) nseg);
+    MPIX_Aint curr = 0, target = 0;
+    for (MPIX_Aint i = 0; i < nseg; ++i) {
+        if (iov_lens[i] < 0)
+            return set_err(MPIX_REDOP_ERR_COUNT);
+        if (pairtype) {
+            if (curr == 0)
+                target = iov_offsets[i];
+            curr += iov_lens[i];
+            if (curr < (MPIX_Aint) size)
+                continue;
+        } else {
+            target = iov_offsets[i];
+            curr = iov_lens[i];
+        }
+        MPIX_Aint n = curr / (MPIX_Aint) size;
+        MPIX_Aint data = n * (MPIX_Aint) size;
+        runs.push_back(Run{target, n});
+        if (pairtype) {
+            curr -= data;
+            if (curr > 0)
+                target = iov_offsets[i] + (iov_lens[i] - curr);
+        } else if (curr != data) {
+            return set_err(MPIX_REDOP_ERR_ARG);   // the reference's MPIR_Assert (:147)
+        }
+    }
+    return set_err(enqueue_runs(inbuf, inoutbuf, runs, (uint32_t) basic_type, (uint32_t) op,
+                                (hipStream_t) stream));
 }
 
 int MPIX_Reduce_local_multi_async(const void *const *inbufs, int ninputs, void *inoutbuf,
@@ -808,8 +980,8 @@ int MPIX_Reduce_local_multi_async(const void *const *inbufs, int ninputs, void *
     if (opi == 14)
         return set_err(MPIX_REDOP_SUCCESS);
     if (opi == 13)      // REPLACE k times = copy of the last input
-        return set_err(hip_err(hipMemcpyAsync(inoutbuf, inbufs[ninputs - 1], (size_t) count * ext,
-                                              hipMemcpyDeviceToDevice, (hipStream_t) stream)));
+        return set_err(replace_rows(inoutbuf, ext, inbufs[ninputs - 1], ext, (uint64_t) count, it,
+                                    ext, (hipStream_t) stream));
     const Entry *e = gpu_entry(opi, it);
     if (!e)
         return set_err(MPIX_REDOP_ERR_TYPE);
@@ -881,6 +1053,11 @@ MPIX_Datatype MPIX_Datatype_internal(MPIX_Datatype datatype)
 MPIX_Aint MPIX_Datatype_extent(MPIX_Datatype datatype)
 {
     return (MPIX_Aint) extent_of(to_internal((uint32_t) datatype));
+}
+
+MPIX_Aint MPIX_Datatype_size(MPIX_Datatype datatype)
+{
+    return (MPIX_Aint) size_of(to_internal((uint32_t) datatype));
 }
 
 int MPIX_Redop_set_fortran_booleans(int true_value, int false_value)

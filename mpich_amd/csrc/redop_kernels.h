@@ -264,15 +264,17 @@ k_vector_s2(const typename C::unit *__restrict__ in, typename C::unit *__restric
 }
 
 // General derived target given as its flattened iov (typerep_op.c:100-150):
-// segment s covers seg_off[s] (element offset into inout) .. + cnt[s], the
-// packed source is consumed in segment order.  prefix[s] = elements before
-// segment s (prefix[nseg] = total).  Thread per source element, segment found
-// by binary search over the L2-resident prefix table.
+// run s covers seg_off[s] (element offset into inout) .. + its count; its
+// source elements start at src_off[s] of the packed source (runs are
+// consumed in order, so src_off is the running prefix unless the host split
+// the runs by alignment class).  prefix[s] = elements before run s in this
+// launch (prefix[nseg] = total).  Thread per element, run found by binary
+// search over the L2-resident prefix table.
 template <class C>
 __global__ void __launch_bounds__(256)
 k_iov(const typename C::unit *__restrict__ in, typename C::unit *__restrict__ io,
-      const int64_t *__restrict__ seg_off, const int64_t *__restrict__ prefix, int64_t nseg,
-      uint64_t total, Params prm)
+      const int64_t *__restrict__ seg_off, const int64_t *__restrict__ prefix,
+      const int64_t *__restrict__ src_off, int64_t nseg, uint64_t total, Params prm)
 {
     const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
     for (uint64_t j = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x; j < total; j += stride) {
@@ -284,8 +286,9 @@ k_iov(const typename C::unit *__restrict__ in, typename C::unit *__restrict__ io
             else
                 hi = mid - 1;
         }
-        int64_t t = seg_off[lo] + (int64_t) (j - (uint64_t) prefix[lo]);
-        io[t] = C::apply(io[t], in[j], prm);
+        const int64_t k = (int64_t) (j - (uint64_t) prefix[lo]);
+        const int64_t t = seg_off[lo] + k;
+        io[t] = C::apply(io[t], in[src_off[lo] + k], prm);
     }
 }
 
@@ -393,15 +396,15 @@ hipError_t launch_vector(const void *in, void *io, uint64_t count, uint64_t bl, 
 
 template <class C>
 hipError_t launch_iov(const void *in, void *io, const int64_t *d_seg_off, const int64_t *d_prefix,
-                      int64_t nseg, uint64_t total, const Params &prm, const LaunchCfg &cfg,
-                      hipStream_t s)
+                      const int64_t *d_src_off, int64_t nseg, uint64_t total, const Params &prm,
+                      const LaunchCfg &cfg, hipStream_t s)
 {
     using T = typename C::unit;
     if (total == 0 || nseg == 0)
         return hipSuccess;
     unsigned grid = grid_for(256ull * 4, total, cfg.max_grid);
     hipLaunchKernelGGL((k_iov<C>), dim3(grid), dim3(256), 0, s, static_cast<const T *>(in),
-                       static_cast<T *>(io), d_seg_off, d_prefix, nseg, total, prm);
+                       static_cast<T *>(io), d_seg_off, d_prefix, d_src_off, nseg, total, prm);
     return hipGetLastError();
 }
 

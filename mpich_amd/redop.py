@@ -50,6 +50,8 @@ def lib():
                                               i32),
             'MPIX_Reduce_local_iov_async': ([vp, vp, aint, ctypes.POINTER(aint),
                                              ctypes.POINTER(aint), i32, i32, vp], i32),
+            'MPIX_Reduce_local_iovec_async': ([vp, vp, aint, ctypes.POINTER(aint),
+                                               ctypes.POINTER(aint), i32, i32, vp], i32),
             'MPIX_Redop_is_supported': ([i32, aint, i32], i32),
             'MPIX_Ipc_export': ([vp, vp, ctypes.POINTER(aint)], i32),
             'MPIX_Ipc_open': ([vp, ctypes.POINTER(vp)], i32),
@@ -58,6 +60,7 @@ def lib():
             'MPIX_Redop_internal_op_dt_check': ([i32, i32], i32),
             'MPIX_Datatype_internal': ([i32], i32),
             'MPIX_Datatype_extent': ([i32], aint),
+            'MPIX_Datatype_size': ([i32], aint),
             'MPIX_Redop_set_fortran_booleans': ([i32, i32], i32),
             'MPIX_Redop_set_launch': ([i32, i32], i32),
             'MPIX_Redop_get_launch': ([ctypes.POINTER(i32)] * 3, i32),
@@ -131,6 +134,18 @@ def reduce_local_iov_async(inbuf, inoutbuf, seg_offsets, seg_counts, basic_type,
                                              _stream_ptr(stream))
 
 
+def reduce_local_iovec_async(inbuf, inoutbuf, iov_offsets, iov_lens, basic_type, op,
+                             stream=None):
+    """derived target given as its raw iov (byte offsets, byte lengths):
+    typerep_op_fallback incl. the pairtype gather (typerep_op.c:100-150)"""
+    n = len(iov_offsets)
+    offs = (ctypes.c_ssize_t * n)(*iov_offsets)
+    lens = (ctypes.c_ssize_t * n)(*iov_lens)
+    return lib().MPIX_Reduce_local_iovec_async(_addr(inbuf), _addr(inoutbuf), n, offs, lens,
+                                               H.as_c_int(basic_type), H.as_c_int(op),
+                                               _stream_ptr(stream))
+
+
 def reduce_local_multi_async(inbufs, inoutbuf, count, datatype, op, stream=None):
     """inoutbuf = (...((inoutbuf OP in[0]) OP in[1])...) OP in[k-1], one pass."""
     arr = (ctypes.c_void_p * len(inbufs))(*[_addr(b) for b in inbufs])
@@ -185,6 +200,10 @@ def datatype_internal(datatype):
 
 def datatype_extent(datatype):
     return lib().MPIX_Datatype_extent(H.as_c_int(datatype))
+
+
+def datatype_size(datatype):
+    return lib().MPIX_Datatype_size(H.as_c_int(datatype))
 
 
 def set_fortran_booleans(true_value, false_value):

@@ -37,6 +37,9 @@ def lib():
         L.oracle_reduce_local_vector.argtypes = [vp, vp, il, il, il, i32, i32]
         L.oracle_reduce_local_iov.argtypes = [vp, vp, il, ctypes.POINTER(il), ctypes.POINTER(il),
                                               i32, i32]
+        L.oracle_reduce_local_iovec.argtypes = L.oracle_reduce_local_iov.argtypes
+        L.oracle_size.argtypes = [i32]
+        L.oracle_size.restype = il
         L.oracle_internal.argtypes = [i32]
         L.oracle_extent.argtypes = [i32]
         L.oracle_extent.restype = il
@@ -82,6 +85,19 @@ def reduce_local_iov(inbuf, inoutbuf, seg_offsets, seg_counts, datatype, op):
                                          (ctypes.c_long * n)(*seg_offsets),
                                          (ctypes.c_long * n)(*seg_counts), _i32(datatype),
                                          _i32(op))
+
+
+def reduce_local_iovec(inbuf, inoutbuf, iov_offsets, iov_lens, datatype, op):
+    """typerep_op_fallback over a raw iov (byte offsets, byte lengths)"""
+    n = len(iov_offsets)
+    return lib().oracle_reduce_local_iovec(_ptr(inbuf), _ptr(inoutbuf), n,
+                                           (ctypes.c_long * n)(*iov_offsets),
+                                           (ctypes.c_long * n)(*iov_lens), _i32(datatype),
+                                           _i32(op))
+
+
+def size(datatype):
+    return lib().oracle_size(_i32(datatype))
 
 
 def internal(datatype):
