@@ -51,12 +51,26 @@ def _default_combine(datatype, op):
     return combine
 
 
+# largest single message handed to the p2p layer: bigger ones go as several
+# messages to the same peer in the same group (matched in posting order), so
+# no count ever reaches 2^31 bytes inside the transport
+MAX_MSG_BYTES = 1 << 30
+
+
+def _p2p(fn, t, peer, group):
+    """P2POps moving tensor `t` to/from `peer`, split at MAX_MSG_BYTES"""
+    step = max(1, MAX_MSG_BYTES // t.element_size())
+    flat = t.reshape(-1)
+    return [dist.P2POp(fn, flat[k:k + step], peer, group=group, tag=TAG)
+            for k in range(0, flat.numel(), step)]
+
+
 def _exchange(send_t, dst_send, recv_t, src_recv, group):
     ops = []
     if send_t is not None:
-        ops.append(dist.P2POp(dist.isend, send_t, dst_send, group=group, tag=TAG))
+        ops += _p2p(dist.isend, send_t, dst_send, group)
     if recv_t is not None:
-        ops.append(dist.P2POp(dist.irecv, recv_t, src_recv, group=group, tag=TAG))
+        ops += _p2p(dist.irecv, recv_t, src_recv, group)
     if not ops:
         return
     for w in dist.batch_isend_irecv(ops):
@@ -240,8 +254,8 @@ def reduce_scatter_block_pairwise(sendbuf, recvbuf, recvcount, datatype, op, gro
         return recvbuf
     ops = []
     for i, (dst, src) in enumerate(peers):
-        ops.append(dist.P2POp(dist.isend, sb[block(dst)], g2l(dst), group=group, tag=TAG))
-        ops.append(dist.P2POp(dist.irecv, slot(i), g2l(src), group=group, tag=TAG))
+        ops += _p2p(dist.isend, sb[block(dst)], g2l(dst), group)
+        ops += _p2p(dist.irecv, slot(i), g2l(src), group)
     for w in dist.batch_isend_irecv(ops):
         w.wait()
     ins = [slot(i) for i in range(size - 1)]
@@ -374,10 +388,8 @@ def allreduce(sendbuf, recvbuf, count, datatype, op, group=None, combine=None, e
                 if q == newrank:
                     continue
                 b = _bitrev(q, pof2)
-                ops.append(dist.P2POp(dist.isend, rb[el(disps[mine], cnts[mine])],
-                                      g2l(real(q)), group=group, tag=TAG))
-                ops.append(dist.P2POp(dist.irecv, rb[el(disps[b], cnts[b])], g2l(real(q)),
-                                      group=group, tag=TAG))
+                ops += _p2p(dist.isend, rb[el(disps[mine], cnts[mine])], g2l(real(q)), group)
+                ops += _p2p(dist.irecv, rb[el(disps[b], cnts[b])], g2l(real(q)), group)
             for w in dist.batch_isend_irecv(ops):
                 w.wait()
             mask = 0

@@ -114,16 +114,22 @@ int set_device(MPIX_Comm c)
 hipStream_t stream_of(void *s) { return static_cast<hipStream_t>(s); }
 
 // ------------------------------------------------------------ transports
+constexpr size_t kMaxMsg = size_t(1) << 30;
+
 int exchange_ccl(MPIX_Comm c, const MPIX_P2p_op *ops, int nops, hipStream_t s)
 {
     if (ncclGroupStart() != ncclSuccess)
         return MPIX_REDOP_ERR_OTHER;
     ncclResult_t r = ncclSuccess;
     for (int i = 0; i < nops && r == ncclSuccess; ++i) {
-        if (ops[i].bytes == 0)
-            continue;
-        r = ops[i].is_recv ? ncclRecv(ops[i].buf, ops[i].bytes, ncclUint8, ops[i].peer, c->nccl, s)
-                           : ncclSend(ops[i].buf, ops[i].bytes, ncclUint8, ops[i].peer, c->nccl, s);
+        // messages above kMaxMsg go as several to the same peer in this
+        // group (matched in posting order): no count reaches 2^31 in RCCL
+        char *p = static_cast<char *>(ops[i].buf);
+        for (size_t off = 0; off < ops[i].bytes && r == ncclSuccess; off += kMaxMsg) {
+            size_t n = ops[i].bytes - off < kMaxMsg ? ops[i].bytes - off : kMaxMsg;
+            r = ops[i].is_recv ? ncclRecv(p + off, n, ncclUint8, ops[i].peer, c->nccl, s)
+                               : ncclSend(p + off, n, ncclUint8, ops[i].peer, c->nccl, s);
+        }
     }
     ncclResult_t r2 = ncclGroupEnd();
     return (r == ncclSuccess && r2 == ncclSuccess) ? MPIX_REDOP_SUCCESS : MPIX_REDOP_ERR_OTHER;

@@ -29,6 +29,9 @@ def _worker(rank, world, port, outdir, recvcount, mode, algo='recursive_halving'
     dist.init_process_group('gloo', rank=rank, world_size=world)
     from oracle import oracle as orc
     from mpich_amd import coll
+    if algo.endswith('+small'):     # every message split into 256-byte pieces
+        coll.MAX_MSG_BYTES = 256
+        algo = algo[:-len('+small')]
     MPI_FLOAT, MPI_INT, MPI_SUM = 0x4c00040a, 0x4c000405, 0x58000003
     if mode == 'float':
         rng = np.random.default_rng(0x5EED0100 + rank)
@@ -73,6 +76,19 @@ def test_rsb_gloo_matches_oracle_schedule(oracle, tmp_path, world):
     sends, recvs = _run(world, recvcount, 'float', tmp_path)
     exp = oracle.rsb_recursive_halving([s.view(np.uint8) for s in sends], recvcount, 0x4c00040a,
                                        0x58000003)
+    for r in range(world):
+        assert recvs[r].tobytes() == exp[r].tobytes(), r
+
+
+@pytest.mark.parametrize('world,algo', [(3, 'recursive_halving'), (4, 'recursive_halving'),
+                                        (4, 'pairwise'), (3, 'pairwise_sequential')])
+def test_rsb_gloo_split_messages(oracle, tmp_path, world, algo):
+    """messages above MAX_MSG_BYTES travel as several same-peer messages
+    (here every block in 256-byte pieces): same bits as the oracle"""
+    recvcount = 1001
+    sends, recvs = _run(world, recvcount, 'float', tmp_path, algo + '+small')
+    sim = oracle.rsb_pairwise if algo != 'recursive_halving' else oracle.rsb_recursive_halving
+    exp = sim([s.view(np.uint8) for s in sends], recvcount, 0x4c00040a, 0x58000003)
     for r in range(world):
         assert recvs[r].tobytes() == exp[r].tobytes(), r
 
