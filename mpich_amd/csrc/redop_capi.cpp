@@ -283,8 +283,9 @@ struct DevState {
     uint32_t seq = 0;
     void *scratch = nullptr;    // 2 slots x (in chunk + inout chunk)
     size_t scratch_bytes = 0;
-    int64_t *iov_tab = nullptr; // device copy of an iov segment table (offsets + prefix)
-    size_t iov_cap = 0;         // entries per half
+    int64_t *iov_tab = nullptr; // device copy of the last iov run table
+    size_t iov_cap = 0;         // its capacity in int64 entries
+    hipEvent_t iov_done = nullptr;  // recorded after the launches that read iov_tab
     char *bounce = nullptr;     // pinned host: in half + inout half, bounce_half bytes each
     char *bounce_dev = nullptr; // its device mapping
     size_t bounce_half = 0;
@@ -681,9 +682,14 @@ int enqueue_runs(const void *inbuf, void *inoutbuf, const std::vector<Run> &runs
     DevState *d = dev_state(dev);
     if (!d)
         return MPIX_REDOP_ERR_OTHER;
+    if (!d->iov_done && hipEventCreateWithFlags(&d->iov_done, hipEventDisableTiming) != hipSuccess)
+        return MPIX_REDOP_ERR_OTHER;
+    // the previous table may still be read by kernels queued on any stream
+    // (this thread may have used another one last time): wait for them
+    rc = hip_err(hipEventSynchronize(d->iov_done));
+    if (rc != MPIX_REDOP_SUCCESS)
+        return rc;
     if (d->iov_cap < need) {
-        // the previous table may still be read by work queued on this stream
-        (void) hipStreamSynchronize(s);
         if (d->iov_tab)
             (void) hipFree(d->iov_tab);
         d->iov_tab = nullptr;
@@ -705,7 +711,8 @@ int enqueue_runs(const void *inbuf, void *inoutbuf, const std::vector<Run> &runs
         rc = hip_err(en->iov(inbuf, (char *) inoutbuf + resid[g], t, t + n, t + 2 * n + 1, n,
                              (uint64_t) gtotal[g], params(), launch_cfg(), s));
     }
-    return rc;
+    int rc2 = hip_err(hipEventRecord(d->iov_done, s));
+    return rc ? rc : rc2;
 }
 
 }  // namespace
@@ -739,6 +746,10 @@ int MPIX_Redop_finalize(void)
             (void) hipHostFree((void *) d.flag);
         if (d.scratch)
             (void) hipFree(d.scratch);
+        if (d.iov_done) {
+            (void) hipEventSynchronize(d.iov_done);
+            (void) hipEventDestroy(d.iov_done);
+        }
         if (d.iov_tab)
             (void) hipFree(d.iov_tab);
         if (d.bounce)

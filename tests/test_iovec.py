@@ -272,3 +272,33 @@ def test_replace_keeps_padding_on_gpu(R, oracle, dt):
     e3 = tgt.view(np.uint8).copy()
     oracle.reduce_local(ins[-1].view(np.uint8).copy(), e3, n, dt, REPLACE)
     assert _host(d3).tobytes() == e3.tobytes()
+
+
+@pytest.mark.gpu
+def test_iov_tables_on_two_streams(R, oracle):
+    """back-to-back iov calls on two different streams from one thread: the
+    second call's run table must not overwrite the first one's while its
+    kernel still reads it"""
+    import torch
+    rng = np.random.default_rng(4242)
+    jobs = []
+    for j in range(2):
+        nseg = 400000 - 150000 * j
+        cnts = rng.integers(1, 5, nseg)
+        offs, pos = [], 0
+        for c in cnts:
+            pos += int(rng.integers(0, 3))
+            offs.append(pos * 8)
+            pos += int(c)
+        src = rng.uniform(-1, 1, int(cnts.sum()))
+        dst = rng.uniform(-1, 1, pos + 1)
+        jobs.append((offs, [int(c) for c in cnts], src, dst))
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    devs = [(_dev(dst), _dev(src)) for _, _, src, dst in jobs]
+    for (offs, cnts, _, _), (dd, ds), st in zip(jobs, devs, streams):
+        assert R.reduce_local_iov_async(ds, dd, offs, cnts, MPI_DOUBLE, SUM, st) == 0
+    torch.cuda.synchronize()
+    for (offs, cnts, src, dst), (dd, _) in zip(jobs, devs):
+        exp = dst.copy()
+        assert oracle.reduce_local_iov(src, exp, offs, cnts, MPI_DOUBLE, SUM) == 0
+        assert _host(dd).tobytes() == exp.view(np.uint8).tobytes()
