@@ -83,6 +83,7 @@ struct MPIX_Comm_s {
     void *stream = nullptr;         // stream of the blocking forms (NULL: own_stream)
     void *scratch = nullptr;
     size_t scratch_bytes = 0;
+    hipEvent_t scratch_ev = nullptr;   // recorded after the last collective that used scratch
     std::vector<uint64_t> send_seq, recv_seq;
     bool host() const { return kind == K_LOCAL_HOST || (kind == K_CUSTOM && device < 0); }
 };
@@ -295,14 +296,23 @@ int combine_multi(MPIX_Comm c, const std::vector<const void *> &ins, void *inout
     return MPIX_REDOP_SUCCESS;
 }
 
+// The communicator's scratch is shared by every collective issued on it, on
+// any stream: a new user is ordered behind the previous one on the device
+// (stream wait on scratch_ev, no host sync), and the buffer is only freed
+// for growth once that work has drained.
 int scratch(MPIX_Comm c, size_t bytes, hipStream_t s, char **out)
 {
+    if (!c->host()) {
+        if (!c->scratch_ev)
+            HTRY(hipEventCreateWithFlags(&c->scratch_ev, hipEventDisableTiming));
+        HTRY(hipStreamWaitEvent(s, c->scratch_ev, 0));
+    }
     if (c->scratch_bytes < bytes) {
         if (c->scratch) {
             if (c->host()) {
                 free(c->scratch);
             } else {
-                HTRY(hipStreamSynchronize(s));
+                HTRY(hipEventSynchronize(c->scratch_ev));
                 HTRY(hipFree(c->scratch));
             }
             c->scratch = nullptr;
@@ -334,6 +344,16 @@ int workspace(MPIX_Comm c, void *ws, size_t ws_bytes, size_t need, hipStream_t s
         return MPIX_REDOP_SUCCESS;
     }
     return scratch(c, need, s, out);
+}
+
+// after a collective enqueued its work on s: mark where the scratch is free
+int release_scratch(MPIX_Comm c, const char *used, int rc, hipStream_t s)
+{
+    if (used && used == c->scratch && c->scratch_ev) {
+        int rc2 = hip_fail(hipEventRecord(c->scratch_ev, s));
+        return rc ? rc : rc2;
+    }
+    return rc;
 }
 
 int finish(MPIX_Comm c, int rc, hipStream_t s, bool blocking)
@@ -661,7 +681,7 @@ int rsb_entry(const void *sendbuf, void *recvbuf, MPIX_Aint recvcount, MPIX_Data
                  ? rsb_recursive_halving(sb, rb, (size_t) recvcount, dt, op, c, w, s, ext)
                  : rsb_pairwise(sb, rb, (size_t) recvcount, dt, op, c, w, s, ext,
                                 algo == MPIX_RSB_PAIRWISE);
-    return finish(c, rc, s, blocking);
+    return finish(c, release_scratch(c, w, rc, s), s, blocking);
 }
 
 int allreduce_entry(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Datatype dt,
@@ -694,7 +714,7 @@ int allreduce_entry(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Da
                  ? allreduce_rd(rb, (size_t) count, dt, op, c, tmp, s, ext)
                  : allreduce_rsag(rb, (size_t) count, dt, op, c, tmp, s, ext,
                                   algorithm == MPIX_ALLREDUCE_REDUCE_SCATTER_ALLGATHER);
-    return finish(c, rc, s, blocking);
+    return finish(c, release_scratch(c, tmp, rc, s), s, blocking);
 }
 
 MPIX_Comm new_comm(int rank, int size, Kind kind)
@@ -851,10 +871,12 @@ int MPIX_Comm_free(MPIX_Comm comm)
             rc = MPIX_REDOP_ERR_OTHER;
         if (comm->own_stream && hipStreamSynchronize(comm->own_stream) != hipSuccess)
             rc = MPIX_REDOP_ERR_OTHER;
-        if (comm->scratch) {
-            (void) hipDeviceSynchronize();      // the scratch may be in use on a caller stream
+        if (comm->scratch_ev)   // the scratch may still be in use on a caller stream
+            (void) hipEventSynchronize(comm->scratch_ev);
+        if (comm->scratch)
             (void) hipFree(comm->scratch);
-        }
+        if (comm->scratch_ev)
+            (void) hipEventDestroy(comm->scratch_ev);
         if (comm->own_stream)
             (void) hipStreamDestroy(comm->own_stream);
     } else {

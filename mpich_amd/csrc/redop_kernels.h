@@ -256,9 +256,13 @@ k_vector_s2(const typename C::unit *__restrict__ in, typename C::unit *__restric
     using R = typename RawOf<2 * sizeof(T)>::type;
     const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
     for (uint64_t j = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride) {
-        R raw = reinterpret_cast<const R *>(io)[j];
         T t;
-        __builtin_memcpy(&t, &raw, sizeof(T));
+        if (j + 1 < n) {
+            R raw = reinterpret_cast<const R *>(io)[j];
+            __builtin_memcpy(&t, &raw, sizeof(T));
+        } else {    // the last pair would reach one element past the type's span
+            t = io[2 * j];
+        }
         io[2 * j] = C::apply(t, in[j], prm);
     }
 }

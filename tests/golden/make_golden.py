@@ -291,6 +291,89 @@ for P in (2, 3, 4, 5):
         'sol ((maxsize-1)!,0), i^P by P%4, (0,0)')
 
 # ---------------------------------------------------------------------------
+# 3b. test/mpi/coll/op{band,bor,bxor,land,lor,lxor,max,min,sum,prod}.c --
+#     3-element KATs per type at the testlist sizes (testlist.in:113-127).
+#     Inputs as the tests set them per rank; expected values are the tests'
+#     own assertions (for the logical ops, which the tests only check for
+#     truth, the exact 0/1 of op_fns.c:99-187).  MPI_LONG_DOUBLE legs are
+#     left out: x87 arithmetic has no GPU path.
+# ---------------------------------------------------------------------------
+OPKAT_NP = {'MPI_CHAR': '<i1', 'MPI_SIGNED_CHAR': '<i1', 'MPI_UNSIGNED_CHAR': '<u1',
+            'MPI_BYTE': '<u1', 'MPI_SHORT': '<i2', 'MPI_UNSIGNED_SHORT': '<u2',
+            'MPI_UNSIGNED': '<u4', 'MPI_INT': '<i4', 'MPI_LONG': '<i8',
+            'MPI_UNSIGNED_LONG': '<u8', 'MPI_LONG_LONG': '<i8'}
+
+
+def opkat(test, line, op, dtname, per_rank, expected, Ps, rule):
+    """per_rank(r, P) -> 3 values; expected(P) -> 3 values (C assignment
+    semantics: values are cast to the type's width)"""
+    npt = OPKAT_NP[dtname]
+    for P in Ps:
+        add('%s %s' % (test, dtname), dtname, op,
+            [int_cast(per_rank(r, P), npt) for r in range(P)], int_cast(expected(P), npt),
+            'test/mpi/coll/%s.c:%d (P=%d)' % (test, line, P), rule)
+
+
+def pat(width, byte):
+    """the tests' literal per width: 0xXX, 0xXXXX, or 0xXXXXXXXX for 4- and
+    8-byte types (the 8-byte legs assign the same 32-bit literal)"""
+    return int.from_bytes(bytes([byte]) * min(width, 4), 'little')
+
+
+BITWISE_TYPES = {
+    'opband': [('MPI_CHAR', 56), ('MPI_SIGNED_CHAR', 87), ('MPI_UNSIGNED_CHAR', 117),
+               ('MPI_BYTE', 147), ('MPI_SHORT', 177), ('MPI_UNSIGNED_SHORT', 207),
+               ('MPI_UNSIGNED', 237), ('MPI_LONG', 267), ('MPI_UNSIGNED_LONG', 297),
+               ('MPI_LONG_LONG', 331)],
+    'opbor': [('MPI_CHAR', 57), ('MPI_SIGNED_CHAR', 88), ('MPI_UNSIGNED_CHAR', 118),
+              ('MPI_BYTE', 148), ('MPI_SHORT', 178), ('MPI_UNSIGNED_SHORT', 208),
+              ('MPI_UNSIGNED', 238), ('MPI_INT', 268), ('MPI_LONG', 298),
+              ('MPI_UNSIGNED_LONG', 328), ('MPI_LONG_LONG', 362)],
+}
+BITWISE_TYPES['opbxor'] = BITWISE_TYPES['opbor']
+for dtname, line in BITWISE_TYPES['opband']:
+    w = np.dtype(OPKAT_NP[dtname]).itemsize
+    ones, f0 = pat(w, 0xff), pat(w, 0xf0)
+    opkat('opband', line, 'BAND', dtname, lambda r, P: [ones, 0, ones if r > 0 else f0],
+          lambda P: [ones, 0, f0], (4,), 'sol {ones, 0, 0xf0..}')
+for dtname, line in BITWISE_TYPES['opbor']:
+    w = np.dtype(OPKAT_NP[dtname]).itemsize
+    ones, x3c, xc3 = pat(w, 0xff), pat(w, 0x3c), pat(w, 0xc3)
+    opkat('opbor', line, 'BOR', dtname, lambda r, P: [ones, 0, x3c if r > 0 else xc3],
+          lambda P: [ones, 0, ones], (4,), 'sol {ones, 0, ones}')
+    opkat('opbxor', line, 'BXOR', dtname, lambda r, P: [ones, 0, x3c if r > 0 else xc3],
+          lambda P: [ones if P % 2 else 0, 0, xc3 if P % 2 else ones], (4, 5),
+          'sol {P%2 ? ones : 0, 0, P%2 ? 0xc3.. : ones}')
+
+for test, op, lines, sol, Ps in (
+        ('opland', 'LAND', (50, 81, 111, 145), lambda P: [1, 0, 0], (4,)),
+        ('oplor', 'LOR', (67, 98, 128, 162), lambda P: [1, 0, 1], (4,)),
+        ('oplxor', 'LXOR', (52, 83, 113, 147), lambda P: [P % 2, 0, (P - 1) % 2], (4, 5))):
+    for dtname, line in zip(('MPI_CHAR', 'MPI_SIGNED_CHAR', 'MPI_UNSIGNED_CHAR', 'MPI_LONG_LONG'),
+                            lines):
+        opkat(test, line, op, dtname, lambda r, P: [1, 0, int(r > 0)], sol, Ps,
+              'in {1, 0, rank>0}; 0/1 results (op_fns.c:99-187)')
+
+for dtname, line in zip(('MPI_CHAR', 'MPI_SIGNED_CHAR', 'MPI_UNSIGNED_CHAR', 'MPI_LONG_LONG'),
+                        (46, 72, 97, 158)):
+    opkat('opmax', line, 'MAX', dtname, lambda r, P: [1, 0, r], lambda P: [1, 0, P - 1], (5,),
+          'sol {1, 0, size-1}')
+    opkat('opmin', line, 'MIN', dtname, lambda r, P: [1, 0, r & 0x7f], lambda P: [1, 0, 0], (4,),
+          'sol {1, 0, 0}')
+
+for dtname, line in zip(('MPI_CHAR', 'MPI_SIGNED_CHAR', 'MPI_UNSIGNED_CHAR', 'MPI_LONG_LONG'),
+                        (70, 96, 121, 262)):
+    opkat('opsum', line, 'SUM', dtname, lambda r, P: [1, 0, int(r > 0)],
+          lambda P: [P, 0, P - 1], (4,), 'sol {size, 0, size-1}')
+
+FACT = [1, 1, 2, 6, 24, 120]                                    # opprod.c:43
+for dtname, line, gt in (('MPI_CHAR', 79, 1), ('MPI_SIGNED_CHAR', 106, 1),
+                         ('MPI_UNSIGNED_CHAR', 132, 0), ('MPI_LONG_LONG', 314, 0)):
+    opkat('opprod', line, 'PROD', dtname,
+          lambda r, P: [r if 0 < r < min(P, 5) else 1, 0, int(r > gt)],
+          lambda P: [FACT[min(P, 5) - 1], 0, 0], (5, 6), 'sol {(maxsize-1)!, 0, 0}')
+
+# ---------------------------------------------------------------------------
 # 4. test/mpi/impls/mpich/hip/stream_allred.hip:47-90 -- device buffers
 # ---------------------------------------------------------------------------
 P, N = 4, 10

@@ -333,6 +333,42 @@ def test_async_on_caller_streams_back_to_back(oracle):
 
 
 @pytest.mark.gpu
+def test_async_scratch_shared_across_streams(oracle):
+    """back-to-back async collectives of one rank on TWO streams, no
+    workspace given: they share the communicator's scratch (the third call
+    needs a bigger one, so it also grows), and the scratch event must order
+    each user behind the previous one"""
+    import torch
+    from mpich_amd import ccl
+    P = 4
+    counts = (50021, 50021, 200003)
+    sends = [float_sends(P, P * m, 7 + k) for k, m in enumerate(counts)]
+    dsend = [[torch.from_numpy(s[r]).cuda() for r in range(P)] for s in sends]
+    outs = [[torch.zeros(m, dtype=torch.float32, device='cuda') for m in counts]
+            for _ in range(P)]
+    streams = [(torch.cuda.Stream(), torch.cuda.Stream()) for _ in range(P)]
+    torch.cuda.synchronize()
+    comms = _dev_comms(P)
+
+    def body(r, c):
+        rc = [ccl.reduce_scatter_block(dsend[k][r], outs[r][k], m, MPI_FLOAT, MPI_SUM, c,
+                                       'recursive_halving', stream=streams[r][k & 1],
+                                       blocking=False)
+              for k, m in enumerate(counts)]
+        for s in streams[r]:
+            s.synchronize()
+        return rc
+    rcs = run_ranks(comms, body)
+    free_all(comms)
+    assert rcs == [[0, 0, 0]] * P
+    for k, m in enumerate(counts):
+        exp = oracle.rsb_recursive_halving([s.view(np.uint8) for s in sends[k]], m, MPI_FLOAT,
+                                           MPI_SUM)
+        for r in range(P):
+            assert outs[r][k].cpu().numpy().tobytes() == exp[r].tobytes(), (k, r)
+
+
+@pytest.mark.gpu
 def test_rccl_communicator_single_rank():
     """MPIX_Comm_create_ccl (MPIR_RCCLcomm_init, rccl.c:21-52) on the test
     box's one GPU: unique id, ncclCommInitRank with one rank, the P = 1
