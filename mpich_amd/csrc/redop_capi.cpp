@@ -430,6 +430,9 @@ int validate(const void *in, const void *io, MPIX_Aint count, uint32_t dt, uint3
         return MPIX_REDOP_ERR_OP;
     if (count == 0)
         return MPIX_REDOP_SUCCESS;
+    // no buffer spans 2^56 bytes; beyond that count * extent could wrap
+    if ((uint64_t) count > ((uint64_t) 1 << 56) / *ext)
+        return MPIX_REDOP_ERR_COUNT;
     if (!in || !io || in == (const void *) -1 || io == (const void *) -1)
         return MPIX_REDOP_ERR_BUFFER;
     if (overlaps(in, io, (uint64_t) count * *ext))

@@ -129,6 +129,23 @@ def test_errors_without_gpu(R):
     assert R.MPI_Reduce_local(4096, 1 << 20, 10, 0x4c0000ff, H.MPI_SUM) == H.MPI_ERR_TYPE
     assert R.MPI_Reduce_local(4096, 1 << 20, 10, H.MPI_INT, H.MPI_OP_NULL) == H.MPI_ERR_OP
     assert R.MPI_Reduce_local(4096, 1 << 20, 10, H.MPI_LONG_DOUBLE, H.MPI_SUM) == H.MPI_ERR_TYPE
+    # count * extent that would wrap 64 bits (no buffer spans 2^56 bytes)
+    assert R.MPI_Reduce_local(4096, 1 << 20, 1 << 62, H.MPI_INT, H.MPI_SUM) == H.MPI_ERR_COUNT
+
+
+def test_errors_reduce_local_errors_test(R):
+    """test/mpi/errors/coll/reduce_local.c:38-58: MPI_IN_PLACE as either
+    buffer and inbuf == inoutbuf are MPI_ERR_BUFFER (checked before any
+    device work, so host pointers suffice here)"""
+    import numpy as np
+    from mpich_amd import handles as H
+    size = 4
+    buf = np.arange(size, dtype=np.int32)
+    recv = np.full(size, -1, np.int32)
+    in_place = 2 ** 64 - 1      # MPI_IN_PLACE == (void *) -1 (mpi.h.in)
+    assert R.MPI_Reduce_local(in_place, recv, size, H.MPI_INT, H.MPI_SUM) == H.MPI_ERR_BUFFER
+    assert R.MPI_Reduce_local(buf, in_place, size, H.MPI_INT, H.MPI_SUM) == H.MPI_ERR_BUFFER
+    assert R.MPI_Reduce_local(recv, recv, size, H.MPI_INT, H.MPI_SUM) == H.MPI_ERR_BUFFER
 
 
 def test_launch_knobs(R):
