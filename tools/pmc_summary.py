@@ -50,7 +50,7 @@ def main():
     avg_ns = float(k['AverageNs'])
     summary = dict(
         source='rocprofv3 on MI355X (gfx950), ROCm 7.2, command: python3 bench.py (see '
-               'tools/gpu_tune_profile.sh)',
+               'tools/gpu_evidence.sh)',
         kernels={'reduce_local_fp32_sum': dict(
             kernel=a.kernel, count=a.count, launches_traced=int(k['Calls']),
             avg_duration_ns=avg_ns, min_ns=float(k['MinNs']), max_ns=float(k['MaxNs']),
