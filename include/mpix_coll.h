@@ -91,7 +91,9 @@ int MPIX_Comm_size(MPIX_Comm comm, int *size);
 int MPIX_Comm_free(MPIX_Comm comm);
 
 /* ---- MPI_Reduce_scatter_block(sendbuf, recvbuf, recvcount, datatype, op) ----
- * sendbuf holds size*recvcount elements; recvbuf recvcount.  workspace: NULL
+ * sendbuf holds size*recvcount elements; recvbuf recvcount.  sendbuf NULL =
+ * MPI_IN_PLACE: recvbuf holds the size*recvcount inputs and gets the result
+ * in its first recvcount elements (red_scat_block.c:58-70).  workspace: NULL
  * (the communicator keeps a grow-only scratch) or at least
  * MPIX_Reduce_scatter_block_workspace() bytes of the buffers' memory kind. */
 #define MPIX_RSB_AUTO               0   /* generic.json: recursive halving < 512 KiB, else pairwise */

@@ -145,7 +145,9 @@ def reduce_scatter_block(sendbuf, recvbuf, recvcount, datatype, op, group=None, 
     """MPI_Reduce_scatter_block(sendbuf, recvbuf, recvcount, datatype, op, comm).
 
     sendbuf: tensor holding comm_size*recvcount elements (any torch dtype;
-    it is addressed as bytes); recvbuf: tensor of recvcount elements.  The
+    it is addressed as bytes); recvbuf: tensor of recvcount elements.
+    sendbuf=None is MPI_IN_PLACE: recvbuf then holds the comm_size*recvcount
+    input elements and receives the result in its first block (:91-96).  The
     op must be commutative (all predefined ops are; :62-67).
     workspace: optional (tmp_results, tmp_recvbuf) byte tensors to reuse.
     timer: optional list; a step timer is appended whose .result() is the
@@ -161,10 +163,11 @@ def reduce_scatter_block(sendbuf, recvbuf, recvcount, datatype, op, group=None, 
         combine = _default_combine(datatype, op)
     g2l = (lambda r: dist.get_global_rank(group, r)) if group is not None else (lambda r: r)
     total = size * recvcount
-    sb = sendbuf.reshape(-1).view(torch.uint8)
     rb = recvbuf.reshape(-1).view(torch.uint8)
+    sb = rb if sendbuf is None else sendbuf.reshape(-1).view(torch.uint8)
     if size == 1:
-        rb.copy_(sb[:recvcount * extent])
+        if sendbuf is not None:
+            rb[:recvcount * extent].copy_(sb[:recvcount * extent])
         return recvbuf
     if workspace is not None:
         tmp_results, tmp_recvbuf = workspace
@@ -198,13 +201,13 @@ def reduce_scatter_block(sendbuf, recvbuf, recvcount, datatype, op, group=None, 
             combine(tmp_recvbuf[el(roff, rcnt)], tmp_results[el(roff, rcnt)], rcnt)
         tm.mark('combine %d' % k)
     if p['newrank'] != -1:                                          # :232-234
-        rb.copy_(tmp_results[el(rank * recvcount, recvcount)])
+        rb[:recvcount * extent].copy_(tmp_results[el(rank * recvcount, recvcount)])
     if rank < 2 * rem:                                              # :241-253
         if rank % 2:
             _exchange(tmp_results[el((rank - 1) * recvcount, recvcount)], g2l(rank - 1),
                       None, None, group)
         else:
-            _exchange(None, None, rb, g2l(rank + 1), group)
+            _exchange(None, None, rb[:recvcount * extent], g2l(rank + 1), group)
     tm.mark('epilogue')
     if timer is not None:
         timer.append(tm)
@@ -215,21 +218,26 @@ def reduce_scatter_block_pairwise(sendbuf, recvbuf, recvcount, datatype, op, gro
                                   combine=None, extent=None, workspace=None, concurrent=True):
     """MPI_Reduce_scatter_block, pairwise exchange (reference algorithm
     `pairwise`).  workspace: optional byte tensor of >= (P-1) * (block bytes
-    rounded up to 256) for the received blocks."""
+    rounded up to 256) for the received blocks.  sendbuf=None is
+    MPI_IN_PLACE: blocks are sent from recvbuf, the own block is reduced in
+    place and moved to the front at the end (:58-64, :71-110)."""
     rank = dist.get_rank(group)
     size = dist.get_world_size(group)
     if extent is None:
         from . import redop
         extent = redop.datatype_extent(datatype)
     g2l = (lambda r: dist.get_global_rank(group, r)) if group is not None else (lambda r: r)
-    sb = sendbuf.reshape(-1).view(torch.uint8)
     rb = recvbuf.reshape(-1).view(torch.uint8)
+    in_place = sendbuf is None
+    sb = rb if in_place else sendbuf.reshape(-1).view(torch.uint8)
     blk = recvcount * extent
 
     def block(i):
         return slice(i * blk, (i + 1) * blk)
 
-    rb[:blk].copy_(sb[block(rank)])                                 # :60-64
+    acc = rb[block(rank)] if in_place else rb[:blk]         # where the result accumulates
+    if not in_place:
+        rb[:blk].copy_(sb[block(rank)])                             # :60-64
     if size == 1:
         return recvbuf
     nslot = size - 1 if concurrent else 1
@@ -244,14 +252,18 @@ def reduce_scatter_block_pairwise(sendbuf, recvbuf, recvcount, datatype, op, gro
     def slot(i):
         return slots[i * sstride:i * sstride + blk]
     peers = [((rank + i) % size, (rank - i + size) % size) for i in range(1, size)]
+    def finish():
+        if in_place and rank != 0:      # :102-110: the result moves to the front
+            rb[:blk].copy_(acc)
+        return recvbuf
     if not concurrent:                                              # the reference's loop
         for dst, src in peers:
             _exchange(sb[block(dst)], g2l(dst), slot(0), g2l(src), group)
             if combine is not None:
-                combine(slot(0), rb[:blk], recvcount)
+                combine(slot(0), acc, recvcount)
             else:
-                _default_combine(datatype, op)(slot(0), rb[:blk], recvcount)
-        return recvbuf
+                _default_combine(datatype, op)(slot(0), acc, recvcount)
+        return finish()
     ops = []
     for i, (dst, src) in enumerate(peers):
         ops += _p2p(dist.isend, sb[block(dst)], g2l(dst), group)
@@ -261,14 +273,14 @@ def reduce_scatter_block_pairwise(sendbuf, recvbuf, recvcount, datatype, op, gro
     ins = [slot(i) for i in range(size - 1)]
     if combine is not None:
         for x in ins:                                               # :86-100, i = 1..P-1
-            combine(x, rb[:blk], recvcount)
+            combine(x, acc, recvcount)
     else:
         from . import redop
         for lo in range(0, len(ins), 16):
-            redop.check(redop.reduce_local_multi_async(ins[lo:lo + 16], rb[:blk], recvcount,
+            redop.check(redop.reduce_local_multi_async(ins[lo:lo + 16], acc, recvcount,
                                                        datatype, op),
                         'MPIX_Reduce_local_multi_async')
-    return recvbuf
+    return finish()
 
 
 ALGORITHMS = {'recursive_halving': reduce_scatter_block, 'pairwise': reduce_scatter_block_pairwise}
@@ -450,10 +462,13 @@ def reduce_scatter_block_pull(sendbuf, recvbuf, recvcount, datatype, op, group=N
     size = dist.get_world_size(group)
     if extent is None:
         extent = redop.datatype_extent(datatype)
-    sb = sendbuf.reshape(-1).view(torch.uint8)
     rb = recvbuf.reshape(-1).view(torch.uint8)
+    in_place = sendbuf is None      # MPI_IN_PLACE: peers pull from recvbuf, own block reduced there
+    sb = rb if in_place else sendbuf.reshape(-1).view(torch.uint8)
     blk = recvcount * extent
-    rb[:blk].copy_(sb[rank * blk:(rank + 1) * blk])
+    acc = rb[rank * blk:(rank + 1) * blk] if in_place else rb[:blk]
+    if not in_place:
+        rb[:blk].copy_(sb[rank * blk:(rank + 1) * blk])
     if size == 1:
         return recvbuf
     handle, off = redop.ipc_export(sb)
@@ -471,9 +486,11 @@ def reduce_scatter_block_pull(sendbuf, recvbuf, recvcount, datatype, op, group=N
     _sync_barrier(group)                        # every peer's sendbuf is complete
     ins = [bases[(rank - i + size) % size] + rank * blk for i in range(1, size)]
     for lo in range(0, len(ins), 16):
-        redop.check(redop.reduce_local_multi_async(ins[lo:lo + 16], rb[:blk], recvcount,
+        redop.check(redop.reduce_local_multi_async(ins[lo:lo + 16], acc, recvcount,
                                                    datatype, op), 'MPIX_Reduce_local_multi_async')
     _sync_barrier(group)                        # nobody reuses sendbuf while peers read it
+    if in_place and rank != 0:
+        rb[:blk].copy_(acc)
     return recvbuf
 
 

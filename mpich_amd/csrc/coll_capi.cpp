@@ -458,30 +458,38 @@ int rsb_recursive_halving(const char *sb, char *rb, size_t recvcount, MPIX_Datat
 // received from rank-i into the result, in that order.  `concurrent` posts
 // all P-1 exchanges as one group (every xGMI link busy at once) and folds
 // the P-1 blocks in one multi-input pass; same order, same bits.
+// MPI_IN_PLACE (sb == rb): blocks go out of recvbuf, the own block is
+// reduced where it lies and moved to the front at the end (:58-64, :71-110).
 int rsb_pairwise(const char *sb, char *rb, size_t recvcount, MPIX_Datatype dt, MPIX_Op op,
                  MPIX_Comm c, char *ws, hipStream_t s, size_t ext, bool concurrent)
 {
     const int rank = c->rank, size = c->size;
     const size_t blk = recvcount * ext, sstride = round256(blk);
-    TRY(copy(c, rb, sb + rank * blk, blk, s));                              // :60-64
+    const bool in_place = sb == rb;
+    char *acc = in_place ? rb + rank * blk : rb;
+    if (!in_place)
+        TRY(copy(c, rb, sb + rank * blk, blk, s));                          // :60-64
     if (!concurrent) {
         for (int i = 1; i < size; ++i) {
             int dst = (rank + i) % size, src = (rank - i + size) % size;
             TRY(exchange(c, {snd(dst, sb + dst * blk, blk), rcv(src, ws, blk)}, s));
-            TRY(combine(c, ws, rb, (MPIX_Aint) recvcount, dt, op, s));
+            TRY(combine(c, ws, acc, (MPIX_Aint) recvcount, dt, op, s));
         }
-        return MPIX_REDOP_SUCCESS;
+    } else {
+        std::vector<MPIX_P2p_op> ops;
+        std::vector<const void *> ins;
+        for (int i = 1; i < size; ++i) {
+            int dst = (rank + i) % size, src = (rank - i + size) % size;
+            ops.push_back(snd(dst, sb + dst * blk, blk));
+            ops.push_back(rcv(src, ws + (i - 1) * sstride, blk));
+            ins.push_back(ws + (i - 1) * sstride);
+        }
+        TRY(exchange(c, ops, s));
+        TRY(combine_multi(c, ins, acc, (MPIX_Aint) recvcount, dt, op, s));
     }
-    std::vector<MPIX_P2p_op> ops;
-    std::vector<const void *> ins;
-    for (int i = 1; i < size; ++i) {
-        int dst = (rank + i) % size, src = (rank - i + size) % size;
-        ops.push_back(snd(dst, sb + dst * blk, blk));
-        ops.push_back(rcv(src, ws + (i - 1) * sstride, blk));
-        ins.push_back(ws + (i - 1) * sstride);
-    }
-    TRY(exchange(c, ops, s));
-    return combine_multi(c, ins, rb, (MPIX_Aint) recvcount, dt, op, s);
+    if (in_place && rank != 0)
+        TRY(copy(c, rb, acc, blk, s));
+    return MPIX_REDOP_SUCCESS;
 }
 
 int rsb_choose(int algorithm, size_t recvcount, size_t ext, int size)
@@ -662,19 +670,19 @@ int rsb_entry(const void *sendbuf, void *recvbuf, MPIX_Aint recvcount, MPIX_Data
 {
     size_t ext;
     TRY(check_args(c, recvbuf, recvcount, dt, op, &ext));
-    if (!sendbuf && recvcount)
-        return MPIX_REDOP_ERR_BUFFER;
     if (algorithm < MPIX_RSB_AUTO || algorithm > MPIX_RSB_PAIRWISE_SEQUENTIAL)
         return MPIX_REDOP_ERR_ARG;
     if (!recvcount)
         return MPIX_REDOP_SUCCESS;
     TRY(set_device(c));
     hipStream_t s = stream_of(stream);
-    const char *sb = static_cast<const char *>(sendbuf);
     char *rb = static_cast<char *>(recvbuf);
+    // sendbuf NULL = MPI_IN_PLACE: recvbuf holds the size*recvcount inputs
+    const char *sb = sendbuf ? static_cast<const char *>(sendbuf) : rb;
     int algo = rsb_choose(algorithm, (size_t) recvcount, ext, c->size);
     if (c->size == 1)
-        return finish(c, copy(c, rb, sb, (size_t) recvcount * ext, s), s, blocking);
+        return finish(c, sendbuf ? copy(c, rb, sb, (size_t) recvcount * ext, s)
+                                 : MPIX_REDOP_SUCCESS, s, blocking);
     char *w;
     TRY(workspace(c, ws, ws_bytes, rsb_workspace((size_t) recvcount, ext, c->size, algo), s, &w));
     int rc = algo == MPIX_RSB_RECURSIVE_HALVING

@@ -170,6 +170,36 @@ def test_in_place_allreduce_and_workspace(oracle):
     free_all(comms)
 
 
+@pytest.mark.parametrize('algo', ['recursive_halving', 'pairwise', 'pairwise_sequential'])
+@pytest.mark.parametrize('P', [1, 2, 3, 4, 5, 8])
+def test_rsb_host_in_place(oracle, P, algo):
+    """MPI_IN_PLACE (sendbuf NULL): recvbuf holds the P*recvcount inputs and
+    gets the result in its first block.  red_scat_block.c:33-70 (recvcount 1,
+    block i of rank r = r + i, sum P*r + P(P-1)/2) with and without IN_PLACE,
+    and bit-identity with the oracle's simulation on floats"""
+    from mpich_amd import ccl
+    comms = host_comms(P, oracle)
+    for in_place in (False, True):
+        sends = [np.arange(r, r + P, dtype=np.int32) for r in range(P)]
+        bufs = [s.copy() if in_place else np.zeros(1, np.int32) for s in sends]
+        rcs = run_ranks(comms, lambda r, c: ccl.reduce_scatter_block(
+            None if in_place else sends[r], bufs[r], 1, MPI_INT, MPI_SUM, c, algo))
+        assert rcs == [0] * P
+        for r in range(P):
+            assert bufs[r][0] == P * r + P * (P - 1) // 2, (in_place, r)
+    recvcount = 333
+    sends = float_sends(P, P * recvcount, 11)
+    bufs = [s.copy() for s in sends]
+    rcs = run_ranks(comms, lambda r, c: ccl.reduce_scatter_block(None, bufs[r], recvcount,
+                                                                  MPI_FLOAT, MPI_SUM, c, algo))
+    free_all(comms)
+    assert rcs == [0] * P
+    sim = oracle.rsb_pairwise if algo.startswith('pairwise') else oracle.rsb_recursive_halving
+    exp = sim([s.view(np.uint8) for s in sends], recvcount, MPI_FLOAT, MPI_SUM)
+    for r in range(P):
+        assert bufs[r][:recvcount].tobytes() == exp[r].tobytes(), r
+
+
 def test_argument_errors(oracle):
     from mpich_amd import ccl
     from mpich_amd import handles as H
@@ -179,7 +209,7 @@ def test_argument_errors(oracle):
     c0 = comms[0]
     assert ccl.reduce_scatter_block(a, b, -1, MPI_FLOAT, MPI_SUM, c0) == H.MPI_ERR_COUNT
     assert ccl.reduce_scatter_block(a, b, 4, MPI_FLOAT, MPI_BXOR, c0) == H.MPI_ERR_OP
-    assert ccl.reduce_scatter_block(None, b, 4, MPI_FLOAT, MPI_SUM, c0) == H.MPI_ERR_BUFFER
+    assert ccl.reduce_scatter_block(a, None, 4, MPI_FLOAT, MPI_SUM, c0) == H.MPI_ERR_BUFFER
     assert ccl.reduce_scatter_block(a, b, 4, MPI_FLOAT, MPI_SUM, c0, 9) == H.MPI_ERR_ARG
     assert ccl.reduce_scatter_block(a, b, 0, MPI_FLOAT, MPI_SUM, c0) == 0
     # the reduce-scatter+allgather allreduce needs count >= pof2 (:127)
@@ -330,6 +360,28 @@ def test_async_on_caller_streams_back_to_back(oracle):
         assert outs[r][0].cpu().numpy().tobytes() == rh[r].tobytes()
         assert outs[r][1].cpu().numpy().tobytes() == pw[r].tobytes()
         assert outs[r][2].cpu().numpy().tobytes() == rh[r].tobytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('algo', ['recursive_halving', 'pairwise', 'pairwise_sequential'])
+def test_rsb_device_in_place(oracle, algo):
+    """MPI_IN_PLACE on device buffers: inputs in recvbuf, result in its
+    first block, bit-identical to the oracle's simulation"""
+    import torch
+    from mpich_amd import ccl
+    P, recvcount = 5, 20011
+    sends = float_sends(P, P * recvcount, 31)
+    bufs = [torch.from_numpy(s.copy()).cuda() for s in sends]
+    torch.cuda.synchronize()
+    comms = _dev_comms(P)
+    rcs = run_ranks(comms, lambda r, c: ccl.reduce_scatter_block(None, bufs[r], recvcount,
+                                                                  MPI_FLOAT, MPI_SUM, c, algo))
+    free_all(comms)
+    assert rcs == [0] * P
+    sim = oracle.rsb_pairwise if algo.startswith('pairwise') else oracle.rsb_recursive_halving
+    exp = sim([s.view(np.uint8) for s in sends], recvcount, MPI_FLOAT, MPI_SUM)
+    for r in range(P):
+        assert bufs[r][:recvcount].cpu().numpy().tobytes() == exp[r].tobytes(), r
 
 
 @pytest.mark.gpu

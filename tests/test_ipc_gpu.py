@@ -31,26 +31,32 @@ def _worker(rank, world, port, outdir, recvcount, dtype_name):
     from mpich_amd import coll
     from mpich_amd import handles as H
     rng = np.random.default_rng(0x5EED0300 + rank)
-    if dtype_name == 'float':
+    in_place = dtype_name.endswith('_inplace')
+    if dtype_name.startswith('float'):
         send = rng.uniform(-1, 1, world * recvcount).astype(np.float32)
         dt, op = H.MPI_FLOAT, H.MPI_SUM
     else:
         send = rng.integers(-100, 100, world * recvcount).astype(np.int32)
         dt, op = H.MPI_INT, H.MPI_MAX
     ds = torch.from_numpy(send).cuda()
-    dr = torch.empty(recvcount, dtype=ds.dtype, device='cuda')
-    for _ in range(2):          # second call reuses the cached peer mappings
-        coll.reduce_scatter_block_pull(ds, dr, recvcount, dt, op, extent=4)
+    if in_place:                # MPI_IN_PLACE: peers pull from recvbuf itself
+        dr = ds.clone()
+        coll.reduce_scatter_block_pull(None, dr, recvcount, dt, op, extent=4)
+    else:
+        dr = torch.empty(recvcount, dtype=ds.dtype, device='cuda')
+        for _ in range(2):      # second call reuses the cached peer mappings
+            coll.reduce_scatter_block_pull(ds, dr, recvcount, dt, op, extent=4)
     torch.cuda.synchronize()
     np.save(os.path.join(outdir, 'send%d.npy' % rank), send)
-    np.save(os.path.join(outdir, 'recv%d.npy' % rank), dr.cpu().numpy())
+    np.save(os.path.join(outdir, 'recv%d.npy' % rank), dr[:recvcount].cpu().numpy())
     dist.barrier()
     coll.ipc_cache_clear()
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('world,dtype_name', [(2, 'float'), (3, 'int'), (4, 'float')])
+@pytest.mark.parametrize('world,dtype_name', [(2, 'float'), (3, 'int'), (4, 'float'),
+                                              (3, 'float_inplace')])
 def test_pull_combine_matches_pairwise(oracle, tmp_path, world, dtype_name):
     if not torch.cuda.is_available():
         pytest.skip('no GPU')
@@ -58,7 +64,8 @@ def test_pull_combine_matches_pairwise(oracle, tmp_path, world, dtype_name):
     mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), recvcount, dtype_name),
              nprocs=world, join=True)
     sends = [np.load(tmp_path / ('send%d.npy' % r)) for r in range(world)]
-    dt, op = (0x4c00040a, 0x58000003) if dtype_name == 'float' else (0x4c000405, 0x58000001)
+    dt, op = (0x4c00040a, 0x58000003) if dtype_name.startswith('float') else \
+        (0x4c000405, 0x58000001)
     exp = oracle.rsb_pairwise([s.view(np.uint8) for s in sends], recvcount, dt, op)
     for r in range(world):
         assert np.load(tmp_path / ('recv%d.npy' % r)).tobytes() == exp[r].tobytes(), r

@@ -32,6 +32,9 @@ def _worker(rank, world, port, outdir, recvcount, mode, algo='recursive_halving'
     if algo.endswith('+small'):     # every message split into 256-byte pieces
         coll.MAX_MSG_BYTES = 256
         algo = algo[:-len('+small')]
+    in_place = algo.endswith('+inplace')    # MPI_IN_PLACE: inputs in recvbuf, sendbuf None
+    if in_place:
+        algo = algo[:-len('+inplace')]
     MPI_FLOAT, MPI_INT, MPI_SUM = 0x4c00040a, 0x4c000405, 0x58000003
     if mode == 'float':
         rng = np.random.default_rng(0x5EED0100 + rank)
@@ -42,6 +45,8 @@ def _worker(rank, world, port, outdir, recvcount, mode, algo='recursive_halving'
         dt = MPI_INT
     sendt = torch.from_numpy(send.copy())
     recv = torch.zeros(recvcount, dtype=sendt.dtype)
+    if in_place:
+        recv, sendt = sendt, None
 
     def combine(inb, inoutb, count):
         a = inoutb.numpy()
@@ -57,7 +62,7 @@ def _worker(rank, world, port, outdir, recvcount, mode, algo='recursive_halving'
         coll.reduce_scatter_block_pairwise(sendt, recv, recvcount, dt, MPI_SUM, combine=combine,
                                            extent=4, concurrent=(algo == 'pairwise'))
     np.save(os.path.join(outdir, 'send%d.npy' % rank), send)
-    np.save(os.path.join(outdir, 'recv%d.npy' % rank), recv.numpy())
+    np.save(os.path.join(outdir, 'recv%d.npy' % rank), recv.numpy()[:recvcount])
     dist.barrier()
     dist.destroy_process_group()
 
@@ -68,6 +73,20 @@ def _run(world, recvcount, mode, tmp_path, algo='recursive_halving'):
     sends = [np.load(tmp_path / ('send%d.npy' % r)) for r in range(world)]
     recvs = [np.load(tmp_path / ('recv%d.npy' % r)) for r in range(world)]
     return sends, recvs
+
+
+@pytest.mark.parametrize('world,algo', [(2, 'recursive_halving'), (3, 'recursive_halving'),
+                                        (5, 'recursive_halving'), (4, 'pairwise'),
+                                        (3, 'pairwise_sequential')])
+def test_rsb_gloo_in_place(oracle, tmp_path, world, algo):
+    """MPI_IN_PLACE (sendbuf None): the inputs sit in recvbuf, the result
+    lands in its first block; same bits as the oracle's schedule"""
+    recvcount = 1001
+    sends, recvs = _run(world, recvcount, 'float', tmp_path, algo + '+inplace')
+    sim = oracle.rsb_pairwise if algo != 'recursive_halving' else oracle.rsb_recursive_halving
+    exp = sim([s.view(np.uint8) for s in sends], recvcount, 0x4c00040a, 0x58000003)
+    for r in range(world):
+        assert recvs[r].tobytes() == exp[r].tobytes(), r
 
 
 @pytest.mark.parametrize('world', [2, 3, 4, 5, 8])
