@@ -12,6 +12,9 @@
  *                                  reduce_scatter_block_intra_recursive_halving.c:38-260
  *                                 and ..._intra_pairwise.c:42-104 (MPICH's large-message
  *                                  choice, maint/tuning/coll/mpir/generic.json:316-341)
+ *   MPIX_Reduce_scatter        <- MPIR_Reduce_scatter_intra_recursive_halving /
+ *                                 _intra_pairwise  src/mpi/coll/reduce_scatter/ (per-rank
+ *                                  recvcounts; generic.json:277-291)
  *   MPIX_Allreduce             <- MPIR_Allreduce_intra_reduce_scatter_allgather
  *                                  src/mpi/coll/allreduce/
  *                                  allreduce_intra_reduce_scatter_allgather.c:41-277
@@ -109,6 +112,22 @@ int MPIX_Reduce_scatter_block_async(const void *sendbuf, void *recvbuf, MPIX_Ain
                                     MPIX_Datatype datatype, MPIX_Op op, MPIX_Comm comm,
                                     int algorithm, void *workspace, size_t workspace_bytes,
                                     void *stream);
+
+/* ---- MPI_Reduce_scatter(sendbuf, recvbuf, recvcounts, datatype, op) ----
+ * (src/mpi/coll/reduce_scatter/reduce_scatter_intra_{recursive_halving,
+ * pairwise}.c): rank i's result block has recvcounts[i] elements (zeros
+ * allowed; size entries, host array); sendbuf holds sum(recvcounts)
+ * elements, NULL = MPI_IN_PLACE (recvbuf holds them and gets the result in
+ * its first recvcounts[rank] elements).  Algorithms and the auto switch
+ * (512 KiB of total message, generic.json:277-291) as for the _block form. */
+size_t MPIX_Reduce_scatter_workspace(const MPIX_Aint *recvcounts, MPIX_Datatype datatype,
+                                     MPIX_Comm comm, int algorithm);
+int MPIX_Reduce_scatter(const void *sendbuf, void *recvbuf, const MPIX_Aint *recvcounts,
+                        MPIX_Datatype datatype, MPIX_Op op, MPIX_Comm comm, int algorithm,
+                        void *workspace, size_t workspace_bytes);
+int MPIX_Reduce_scatter_async(const void *sendbuf, void *recvbuf, const MPIX_Aint *recvcounts,
+                              MPIX_Datatype datatype, MPIX_Op op, MPIX_Comm comm, int algorithm,
+                              void *workspace, size_t workspace_bytes, void *stream);
 
 /* ---- MPI_Allreduce(sendbuf, recvbuf, count, datatype, op) ----
  * sendbuf NULL = MPI_IN_PLACE (recvbuf holds the input). */

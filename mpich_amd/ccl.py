@@ -56,6 +56,11 @@ def lib():
             'MPIX_Reduce_scatter_block': ([vp, vp, aint, i32, i32, vp, i32, vp, sz], i32),
             'MPIX_Reduce_scatter_block_async': ([vp, vp, aint, i32, i32, vp, i32, vp, sz, vp],
                                                 i32),
+            'MPIX_Reduce_scatter_workspace': ([ctypes.POINTER(aint), i32, vp, i32], sz),
+            'MPIX_Reduce_scatter': ([vp, vp, ctypes.POINTER(aint), i32, i32, vp, i32, vp, sz],
+                                    i32),
+            'MPIX_Reduce_scatter_async': ([vp, vp, ctypes.POINTER(aint), i32, i32, vp, i32, vp,
+                                           sz, vp], i32),
             'MPIX_Allreduce_workspace': ([aint, i32, vp], sz),
             'MPIX_Allreduce': ([vp, vp, aint, i32, i32, vp, i32, vp, sz], i32),
             'MPIX_Allreduce_async': ([vp, vp, aint, i32, i32, vp, i32, vp, sz, vp], i32),
@@ -148,6 +153,28 @@ def reduce_scatter_block(sendbuf, recvbuf, recvcount, datatype, op, comm, algori
     return lib().MPIX_Reduce_scatter_block_async(_addr(sendbuf), _addr(recvbuf), recvcount,
                                                  H.as_c_int(datatype), H.as_c_int(op), comm.h, a,
                                                  ws, wsb, redop._stream_ptr(stream))
+
+
+def reduce_scatter(sendbuf, recvbuf, recvcounts, datatype, op, comm, algorithm='auto',
+                   workspace=None, stream=None, blocking=True):
+    """MPI_Reduce_scatter with per-rank recvcounts (sendbuf None =
+    MPI_IN_PLACE); returns the MPI error class."""
+    a = RSB_ALGORITHMS[algorithm] if isinstance(algorithm, str) else algorithm
+    ws, wsb = (None, 0) if workspace is None else (_addr(workspace), workspace.numel() *
+                                                    workspace.element_size())
+    cnts = (ctypes.c_ssize_t * len(recvcounts))(*recvcounts)
+    if blocking:
+        return lib().MPIX_Reduce_scatter(_addr(sendbuf), _addr(recvbuf), cnts,
+                                         H.as_c_int(datatype), H.as_c_int(op), comm.h, a, ws, wsb)
+    return lib().MPIX_Reduce_scatter_async(_addr(sendbuf), _addr(recvbuf), cnts,
+                                           H.as_c_int(datatype), H.as_c_int(op), comm.h, a, ws,
+                                           wsb, redop._stream_ptr(stream))
+
+
+def rs_workspace_bytes(recvcounts, datatype, comm, algorithm='auto'):
+    a = RSB_ALGORITHMS[algorithm] if isinstance(algorithm, str) else algorithm
+    cnts = (ctypes.c_ssize_t * len(recvcounts))(*recvcounts)
+    return lib().MPIX_Reduce_scatter_workspace(cnts, H.as_c_int(datatype), comm.h, a)
 
 
 def allreduce(sendbuf, recvbuf, count, datatype, op, comm, algorithm='auto', workspace=None,

@@ -234,17 +234,25 @@ int exchange_local(MPIX_Comm c, const MPIX_P2p_op *ops, int nops, hipStream_t s)
 
 int exchange(MPIX_Comm c, const std::vector<MPIX_P2p_op> &ops, hipStream_t s)
 {
-    if (ops.empty())
+    // zero-length messages are not sent (both sides know the lengths, so
+    // both skip them; the reference does the same, e.g.
+    // reduce_scatter_intra_recursive_halving.c:188-208)
+    std::vector<MPIX_P2p_op> nz;
+    nz.reserve(ops.size());
+    for (const MPIX_P2p_op &o : ops)
+        if (o.bytes)
+            nz.push_back(o);
+    if (nz.empty())
         return MPIX_REDOP_SUCCESS;
     switch (c->kind) {
         case K_CCL:
-            return exchange_ccl(c, ops.data(), (int) ops.size(), s);
+            return exchange_ccl(c, nz.data(), (int) nz.size(), s);
         case K_LOCAL_DEV:
         case K_LOCAL_HOST:
-            return exchange_local(c, ops.data(), (int) ops.size(), s);
+            return exchange_local(c, nz.data(), (int) nz.size(), s);
         default:
-            return c->xfn(c->xctx, c->rank, ops.data(), (int) ops.size(), s) ? MPIX_REDOP_ERR_OTHER
-                                                                             : MPIX_REDOP_SUCCESS;
+            return c->xfn(c->xctx, c->rank, nz.data(), (int) nz.size(), s) ? MPIX_REDOP_ERR_OTHER
+                                                                           : MPIX_REDOP_SUCCESS;
     }
 }
 
@@ -381,13 +389,21 @@ int check_args(MPIX_Comm c, const void *recvbuf, MPIX_Aint count, MPIX_Datatype 
 }
 
 // ------------------------------------------------------------ schedules
-// MPIR_Reduce_scatter_block_intra_recursive_halving
-// (reduce_scatter_block_intra_recursive_halving.c:38-260)
-int rsb_recursive_halving(const char *sb, char *rb, size_t recvcount, MPIX_Datatype dt, MPIX_Op op,
-                          MPIX_Comm c, char *ws, hipStream_t s, size_t ext)
+// MPIR_Reduce_scatter_intra_recursive_halving
+// (reduce_scatter_intra_recursive_halving.c:38-260; the _block variant,
+// reduce_scatter_block_intra_recursive_halving.c:38-260, is the case of
+// equal counts).  cnts[i] = elements of rank i's result block.
+int rs_recursive_halving(const char *sb, char *rb, const std::vector<size_t> &cnts,
+                         MPIX_Datatype dt, MPIX_Op op, MPIX_Comm c, char *ws, hipStream_t s,
+                         size_t ext)
 {
     const int rank = c->rank, size = c->size;
-    const size_t total = recvcount * size;
+    std::vector<size_t> disps(size, 0);
+    for (int i = 1; i < size; ++i)
+        disps[i] = disps[i - 1] + cnts[i - 1];
+    const size_t total = disps[size - 1] + cnts[size - 1];
+    if (!total)
+        return MPIX_REDOP_SUCCESS;
     char *tmp_results = ws;
     char *tmp_recvbuf = ws + round256(total * ext);
     TRY(copy(c, tmp_results, sb, total * ext, s));                         // :91-96
@@ -409,7 +425,7 @@ int rsb_recursive_halving(const char *sb, char *rb, size_t recvcount, MPIX_Datat
         std::vector<size_t> newcnts(pof2), newdisps(pof2, 0);
         for (int i = 0; i < pof2; ++i) {
             int old_i = i < rem ? i * 2 + 1 : i + rem;
-            newcnts[i] = old_i < 2 * rem ? 2 * recvcount : recvcount;
+            newcnts[i] = old_i < 2 * rem ? cnts[old_i] + cnts[old_i - 1] : cnts[old_i];
         }
         for (int i = 1; i < pof2; ++i)
             newdisps[i] = newdisps[i - 1] + newcnts[i - 1];
@@ -433,6 +449,7 @@ int rsb_recursive_halving(const char *sb, char *rb, size_t recvcount, MPIX_Datat
                 send_cnt = sum(send_idx, recv_idx);
                 recv_cnt = sum(recv_idx, last_idx);
             }
+            // zero-length legs are skipped on both sides (:188-208)
             TRY(exchange(c, {snd(dst, tmp_results + newdisps[send_idx] * ext, send_cnt * ext),
                              rcv(dst, tmp_recvbuf + newdisps[recv_idx] * ext, recv_cnt * ext)}, s));
             TRY(combine(c, tmp_recvbuf + newdisps[recv_idx] * ext,
@@ -441,79 +458,98 @@ int rsb_recursive_halving(const char *sb, char *rb, size_t recvcount, MPIX_Datat
             last_idx = recv_idx + mask;
             mask >>= 1;
         }
-        TRY(copy(c, rb, tmp_results + rank * recvcount * ext, recvcount * ext, s));   // :232-234
+        TRY(copy(c, rb, tmp_results + disps[rank] * ext, cnts[rank] * ext, s));   // :232-240
     }
-    if (rank < 2 * rem) {                                                   // :241-253
+    if (rank < 2 * rem) {                                                   // :245-262
         if (rank % 2)
-            TRY(exchange(c, {snd(rank - 1, tmp_results + (rank - 1) * recvcount * ext,
-                                 recvcount * ext)}, s));
+            TRY(exchange(c, {snd(rank - 1, tmp_results + disps[rank - 1] * ext,
+                                 cnts[rank - 1] * ext)}, s));
         else
-            TRY(exchange(c, {rcv(rank + 1, rb, recvcount * ext)}, s));
+            TRY(exchange(c, {rcv(rank + 1, rb, cnts[rank] * ext)}, s));
     }
     return MPIX_REDOP_SUCCESS;
 }
 
-// MPIR_Reduce_scatter_block_intra_pairwise (…_intra_pairwise.c:42-104):
+// MPIR_Reduce_scatter_intra_pairwise (reduce_scatter_intra_pairwise.c:42-115;
+// the _block variant …_block_intra_pairwise.c:42-104 with equal counts):
 // step i = 1..P-1 sends block (rank+i) to rank+i and folds the block
 // received from rank-i into the result, in that order.  `concurrent` posts
 // all P-1 exchanges as one group (every xGMI link busy at once) and folds
 // the P-1 blocks in one multi-input pass; same order, same bits.
 // MPI_IN_PLACE (sb == rb): blocks go out of recvbuf, the own block is
-// reduced where it lies and moved to the front at the end (:58-64, :71-110).
-int rsb_pairwise(const char *sb, char *rb, size_t recvcount, MPIX_Datatype dt, MPIX_Op op,
-                 MPIX_Comm c, char *ws, hipStream_t s, size_t ext, bool concurrent)
+// reduced where it lies and moved to the front at the end (:58-64, :71-115).
+int rs_pairwise(const char *sb, char *rb, const std::vector<size_t> &cnts, MPIX_Datatype dt,
+                MPIX_Op op, MPIX_Comm c, char *ws, hipStream_t s, size_t ext, bool concurrent)
 {
     const int rank = c->rank, size = c->size;
-    const size_t blk = recvcount * ext, sstride = round256(blk);
+    std::vector<size_t> disps(size, 0);
+    for (int i = 1; i < size; ++i)
+        disps[i] = disps[i - 1] + cnts[i - 1];
+    const size_t blk = cnts[rank] * ext, sstride = round256(blk);
     const bool in_place = sb == rb;
-    char *acc = in_place ? rb + rank * blk : rb;
+    char *acc = in_place ? rb + disps[rank] * ext : rb;
     if (!in_place)
-        TRY(copy(c, rb, sb + rank * blk, blk, s));                          // :60-64
+        TRY(copy(c, rb, sb + disps[rank] * ext, blk, s));                   // :58-64
     if (!concurrent) {
         for (int i = 1; i < size; ++i) {
             int dst = (rank + i) % size, src = (rank - i + size) % size;
-            TRY(exchange(c, {snd(dst, sb + dst * blk, blk), rcv(src, ws, blk)}, s));
-            TRY(combine(c, ws, acc, (MPIX_Aint) recvcount, dt, op, s));
+            TRY(exchange(c, {snd(dst, sb + disps[dst] * ext, cnts[dst] * ext),
+                             rcv(src, ws, blk)}, s));
+            TRY(combine(c, ws, acc, (MPIX_Aint) cnts[rank], dt, op, s));
         }
     } else {
         std::vector<MPIX_P2p_op> ops;
         std::vector<const void *> ins;
         for (int i = 1; i < size; ++i) {
             int dst = (rank + i) % size, src = (rank - i + size) % size;
-            ops.push_back(snd(dst, sb + dst * blk, blk));
+            ops.push_back(snd(dst, sb + disps[dst] * ext, cnts[dst] * ext));
             ops.push_back(rcv(src, ws + (i - 1) * sstride, blk));
             ins.push_back(ws + (i - 1) * sstride);
         }
         TRY(exchange(c, ops, s));
-        TRY(combine_multi(c, ins, acc, (MPIX_Aint) recvcount, dt, op, s));
+        if (cnts[rank])
+            TRY(combine_multi(c, ins, acc, (MPIX_Aint) cnts[rank], dt, op, s));
     }
     if (in_place && rank != 0)
         TRY(copy(c, rb, acc, blk, s));
     return MPIX_REDOP_SUCCESS;
 }
 
-int rsb_choose(int algorithm, size_t recvcount, size_t ext, int size)
+// generic.json:277-291 / :316-341: recursive halving below 512 KiB of total
+// message, pairwise above (commutative ops)
+int rs_choose(int algorithm, size_t total_bytes)
 {
     if (algorithm != MPIX_RSB_AUTO)
         return algorithm;
-    // generic.json:316-341: recursive halving below 512 KiB, pairwise above
-    return recvcount * ext * size < (512u << 10) ? MPIX_RSB_RECURSIVE_HALVING : MPIX_RSB_PAIRWISE;
+    return total_bytes < (512u << 10) ? MPIX_RSB_RECURSIVE_HALVING : MPIX_RSB_PAIRWISE;
 }
 
-size_t rsb_workspace(size_t recvcount, size_t ext, int size, int algo)
+int rsb_choose(int algorithm, size_t recvcount, size_t ext, int size)
+{
+    return rs_choose(algorithm, recvcount * ext * size);
+}
+
+// scratch bytes of a schedule: total = all ranks' elements, mine = this
+// rank's result elements
+size_t rs_workspace(size_t total, size_t mine, size_t ext, int size, int algo)
 {
     if (size == 1)
         return 0;
     switch (algo) {
         case MPIX_RSB_RECURSIVE_HALVING:
-            return 2 * round256(recvcount * size * ext);
+            return 2 * round256(total * ext);
         case MPIX_RSB_PAIRWISE:
-            return (size - 1) * round256(recvcount * ext);
+            return (size - 1) * round256(mine * ext);
         case MPIX_RSB_PAIRWISE_SEQUENTIAL:
-            return round256(recvcount * ext);
+            return round256(mine * ext);
         default:
             return 0;
     }
+}
+
+size_t rsb_workspace(size_t recvcount, size_t ext, int size, int algo)
+{
+    return rs_workspace(recvcount * size, recvcount, ext, size, algo);
 }
 
 int bitrev(int r, int pof2)
@@ -665,31 +701,62 @@ int allreduce_rd(char *rb, size_t count, MPIX_Datatype dt, MPIX_Op op, MPIX_Comm
     return MPIX_REDOP_SUCCESS;
 }
 
-int rsb_entry(const void *sendbuf, void *recvbuf, MPIX_Aint recvcount, MPIX_Datatype dt, MPIX_Op op,
-              MPIX_Comm c, int algorithm, void *ws, size_t ws_bytes, void *stream, bool blocking)
+// MPI_Reduce_scatter (cnts = recvcounts) and MPI_Reduce_scatter_block
+// (equal cnts).  sendbuf NULL = MPI_IN_PLACE: recvbuf holds all ranks' inputs.
+int rs_entry(const void *sendbuf, void *recvbuf, const std::vector<size_t> &cnts, MPIX_Datatype dt,
+             MPIX_Op op, MPIX_Comm c, int algorithm, void *ws, size_t ws_bytes, void *stream,
+             bool blocking)
 {
-    size_t ext;
-    TRY(check_args(c, recvbuf, recvcount, dt, op, &ext));
+    size_t ext, total = 0;
+    for (size_t n : cnts)
+        total += n;
+    TRY(check_args(c, recvbuf, (MPIX_Aint) cnts[c->rank], dt, op, &ext));
     if (algorithm < MPIX_RSB_AUTO || algorithm > MPIX_RSB_PAIRWISE_SEQUENTIAL)
         return MPIX_REDOP_ERR_ARG;
-    if (!recvcount)
+    if (!total)
         return MPIX_REDOP_SUCCESS;
+    if (!recvbuf && !sendbuf)
+        return MPIX_REDOP_ERR_BUFFER;
     TRY(set_device(c));
     hipStream_t s = stream_of(stream);
     char *rb = static_cast<char *>(recvbuf);
-    // sendbuf NULL = MPI_IN_PLACE: recvbuf holds the size*recvcount inputs
     const char *sb = sendbuf ? static_cast<const char *>(sendbuf) : rb;
-    int algo = rsb_choose(algorithm, (size_t) recvcount, ext, c->size);
+    int algo = rs_choose(algorithm, total * ext);
     if (c->size == 1)
-        return finish(c, sendbuf ? copy(c, rb, sb, (size_t) recvcount * ext, s)
-                                 : MPIX_REDOP_SUCCESS, s, blocking);
+        return finish(c, sendbuf ? copy(c, rb, sb, cnts[0] * ext, s) : MPIX_REDOP_SUCCESS, s,
+                      blocking);
     char *w;
-    TRY(workspace(c, ws, ws_bytes, rsb_workspace((size_t) recvcount, ext, c->size, algo), s, &w));
+    TRY(workspace(c, ws, ws_bytes, rs_workspace(total, cnts[c->rank], ext, c->size, algo), s, &w));
     int rc = algo == MPIX_RSB_RECURSIVE_HALVING
-                 ? rsb_recursive_halving(sb, rb, (size_t) recvcount, dt, op, c, w, s, ext)
-                 : rsb_pairwise(sb, rb, (size_t) recvcount, dt, op, c, w, s, ext,
-                                algo == MPIX_RSB_PAIRWISE);
+                 ? rs_recursive_halving(sb, rb, cnts, dt, op, c, w, s, ext)
+                 : rs_pairwise(sb, rb, cnts, dt, op, c, w, s, ext, algo == MPIX_RSB_PAIRWISE);
     return finish(c, release_scratch(c, w, rc, s), s, blocking);
+}
+
+int rsb_entry(const void *sendbuf, void *recvbuf, MPIX_Aint recvcount, MPIX_Datatype dt, MPIX_Op op,
+              MPIX_Comm c, int algorithm, void *ws, size_t ws_bytes, void *stream, bool blocking)
+{
+    if (!c)
+        return MPIX_REDOP_ERR_ARG;
+    if (recvcount < 0)
+        return MPIX_REDOP_ERR_COUNT;
+    return rs_entry(sendbuf, recvbuf, std::vector<size_t>(c->size, (size_t) recvcount), dt, op, c,
+                    algorithm, ws, ws_bytes, stream, blocking);
+}
+
+int rs_counts(MPIX_Comm c, const MPIX_Aint *recvcounts, std::vector<size_t> *cnts)
+{
+    if (!c)
+        return MPIX_REDOP_ERR_ARG;
+    if (!recvcounts)
+        return MPIX_REDOP_ERR_COUNT;
+    cnts->resize(c->size);
+    for (int i = 0; i < c->size; ++i) {
+        if (recvcounts[i] < 0)
+            return MPIX_REDOP_ERR_COUNT;
+        (*cnts)[i] = (size_t) recvcounts[i];
+    }
+    return MPIX_REDOP_SUCCESS;
 }
 
 int allreduce_entry(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Datatype dt,
@@ -922,6 +989,39 @@ int MPIX_Reduce_scatter_block_async(const void *sendbuf, void *recvbuf, MPIX_Ain
 {
     return rsb_entry(sendbuf, recvbuf, recvcount, datatype, op, comm, algorithm, workspace,
                      workspace_bytes, stream, false);
+}
+
+size_t MPIX_Reduce_scatter_workspace(const MPIX_Aint *recvcounts, MPIX_Datatype datatype,
+                                     MPIX_Comm comm, int algorithm)
+{
+    size_t ext = (size_t) MPIX_Datatype_extent(datatype), total = 0;
+    std::vector<size_t> cnts;
+    if (!ext || rs_counts(comm, recvcounts, &cnts) != MPIX_REDOP_SUCCESS)
+        return 0;
+    for (size_t n : cnts)
+        total += n;
+    return rs_workspace(total, cnts[comm->rank], ext, comm->size,
+                        rs_choose(algorithm, total * ext));
+}
+
+int MPIX_Reduce_scatter(const void *sendbuf, void *recvbuf, const MPIX_Aint *recvcounts,
+                        MPIX_Datatype datatype, MPIX_Op op, MPIX_Comm comm, int algorithm,
+                        void *workspace, size_t workspace_bytes)
+{
+    std::vector<size_t> cnts;
+    TRY(rs_counts(comm, recvcounts, &cnts));
+    return rs_entry(sendbuf, recvbuf, cnts, datatype, op, comm, algorithm, workspace,
+                    workspace_bytes, comm->stream ? comm->stream : comm->own_stream, true);
+}
+
+int MPIX_Reduce_scatter_async(const void *sendbuf, void *recvbuf, const MPIX_Aint *recvcounts,
+                              MPIX_Datatype datatype, MPIX_Op op, MPIX_Comm comm, int algorithm,
+                              void *workspace, size_t workspace_bytes, void *stream)
+{
+    std::vector<size_t> cnts;
+    TRY(rs_counts(comm, recvcounts, &cnts));
+    return rs_entry(sendbuf, recvbuf, cnts, datatype, op, comm, algorithm, workspace,
+                    workspace_bytes, stream, false);
 }
 
 size_t MPIX_Allreduce_workspace(MPIX_Aint count, MPIX_Datatype datatype, MPIX_Comm comm)

@@ -50,6 +50,9 @@ def lib():
         L.oracle_rsb_recursive_halving.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(vp), il,
                                                    i32, i32, i32]
         L.oracle_rsb_pairwise.argtypes = L.oracle_rsb_recursive_halving.argtypes
+        L.oracle_rs_recursive_halving.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(vp),
+                                                  ctypes.POINTER(il), i32, i32, i32]
+        L.oracle_rs_pairwise.argtypes = L.oracle_rs_recursive_halving.argtypes
         L.oracle_allreduce_rabenseifner.argtypes = L.oracle_rsb_recursive_halving.argtypes
         L.oracle_allreduce_recursive_doubling.argtypes = L.oracle_rsb_recursive_halving.argtypes
         L.oracle_wtime.restype = ctypes.c_double
@@ -133,6 +136,23 @@ def rsb_recursive_halving(sendbufs, recvcount, datatype, op, algorithm='recursiv
     rc = fn(sp, rp, recvcount, _i32(datatype), _i32(op), P)
     if rc:
         raise RuntimeError('oracle rsb failed: %d' % rc)
+    return recvs
+
+
+def rs_schedule(sendbufs, recvcounts, datatype, op, algorithm='recursive_halving'):
+    """Simulate MPI_Reduce_scatter (per-rank recvcounts) over P ranks in one
+    process with the reference's recursive halving or pairwise schedule."""
+    P = len(sendbufs)
+    ext = extent(datatype)
+    recvs = [np.zeros(max(1, c) * ext, np.uint8)[:c * ext] for c in recvcounts]
+    sp = (ctypes.c_void_p * P)(*[s.ctypes.data for s in sendbufs])
+    rp = (ctypes.c_void_p * P)(*[r.ctypes.data for r in recvs])
+    cn = (ctypes.c_long * P)(*recvcounts)
+    fn = lib().oracle_rs_pairwise if algorithm == 'pairwise' else \
+        lib().oracle_rs_recursive_halving
+    rc = fn(sp, rp, cn, _i32(datatype), _i32(op), P)
+    if rc:
+        raise RuntimeError('oracle reduce_scatter failed: %d' % rc)
     return recvs
 
 

@@ -200,6 +200,78 @@ def test_rsb_host_in_place(oracle, P, algo):
         assert bufs[r][:recvcount].tobytes() == exp[r].tobytes(), r
 
 
+def _ragged_counts(P, seed):
+    """per-rank recvcounts with zeros and uneven sizes"""
+    rng = np.random.default_rng(seed)
+    c = [int(x) for x in rng.integers(0, 700, P)]
+    if P > 2:
+        c[1] = 0
+    return c
+
+
+@pytest.mark.parametrize('algo', ['recursive_halving', 'pairwise', 'pairwise_sequential', 'auto'])
+@pytest.mark.parametrize('P', [1, 2, 3, 4, 5, 6, 7, 8])
+def test_reduce_scatter_host_matches_oracle(oracle, P, algo):
+    """MPI_Reduce_scatter with ragged recvcounts (zeros included) against the
+    oracle's simulation of reduce_scatter_intra_{recursive_halving,pairwise}.c,
+    plain and MPI_IN_PLACE"""
+    from mpich_amd import ccl
+    counts = _ragged_counts(P, 100 + P)
+    total = sum(counts)
+    sends = float_sends(P, total, 0x5EED0400)
+    comms = host_comms(P, oracle)
+    sim_algo = 'recursive_halving' if algo in ('recursive_halving', 'auto') and \
+        total * 4 < (512 << 10) else 'pairwise'
+    exp = oracle.rs_schedule([s.view(np.uint8) for s in sends], counts, MPI_FLOAT, MPI_SUM,
+                             sim_algo)
+    for in_place in (False, True):
+        bufs = [s.copy() if in_place else np.zeros(max(1, counts[r]), np.float32)
+                for r, s in enumerate(sends)]
+        rcs = run_ranks(comms, lambda r, c: ccl.reduce_scatter(
+            None if in_place else sends[r], bufs[r], counts, MPI_FLOAT, MPI_SUM, c, algo))
+        assert rcs == [0] * P
+        for r in range(P):
+            assert bufs[r][:counts[r]].tobytes() == exp[r].tobytes(), (in_place, r)
+    free_all(comms)
+
+
+@pytest.mark.parametrize('P', [4, 6, 8])
+def test_reduce_scatter_redscat_kats(oracle, P):
+    """redscat.c:40-55 (recvcounts 1) and redscat3.c:51-100 (1 Mi / P ints per
+    rank, then MPI_IN_PLACE): block i of rank r holds r + i, result P*r +
+    P(P-1)/2; the two simulations of the reference schedules agree on ragged
+    integer counts too (exact arithmetic: association-free)"""
+    from mpich_amd import ccl
+    comms = host_comms(P, oracle)
+    for mycount in (1, (1 << 20) // P):
+        counts = [mycount] * P
+        sends = [np.concatenate([np.full(mycount, r + i, np.int32) for i in range(P)])
+                 for r in range(P)]
+        for algo in ('recursive_halving', 'pairwise'):
+            outs = [np.full(mycount, -1, np.int32) for _ in range(P)]
+            rcs = run_ranks(comms, lambda r, c: ccl.reduce_scatter(sends[r], outs[r], counts,
+                                                                   MPI_INT, MPI_SUM, c, algo))
+            assert rcs == [0] * P
+            for r in range(P):
+                assert np.all(outs[r] == P * r + P * (P - 1) // 2), (mycount, algo, r)
+        bufs = [s.copy() for s in sends]
+        rcs = run_ranks(comms, lambda r, c: ccl.reduce_scatter(None, bufs[r], counts, MPI_INT,
+                                                               MPI_SUM, c))
+        assert rcs == [0] * P
+        for r in range(P):
+            assert np.all(bufs[r][:mycount] == P * r + P * (P - 1) // 2)
+    free_all(comms)
+    counts = _ragged_counts(P, 7)
+    rng = np.random.default_rng(3)
+    ints = [rng.integers(-1000, 1000, sum(counts)).astype(np.int32) for _ in range(P)]
+    rh = oracle.rs_schedule([x.view(np.uint8) for x in ints], counts, MPI_INT, MPI_SUM)
+    pw = oracle.rs_schedule([x.view(np.uint8) for x in ints], counts, MPI_INT, MPI_SUM, 'pairwise')
+    offs = np.concatenate([[0], np.cumsum(counts)])
+    for r in range(P):
+        closed = sum(x[offs[r]:offs[r + 1]] for x in ints).astype(np.int32)
+        assert rh[r].tobytes() == pw[r].tobytes() == closed.tobytes(), r
+
+
 def test_argument_errors(oracle):
     from mpich_amd import ccl
     from mpich_amd import handles as H
@@ -360,6 +432,30 @@ def test_async_on_caller_streams_back_to_back(oracle):
         assert outs[r][0].cpu().numpy().tobytes() == rh[r].tobytes()
         assert outs[r][1].cpu().numpy().tobytes() == pw[r].tobytes()
         assert outs[r][2].cpu().numpy().tobytes() == rh[r].tobytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('algo', ['recursive_halving', 'pairwise', 'pairwise_sequential'])
+@pytest.mark.parametrize('P', [3, 4, 7])
+def test_reduce_scatter_device_ragged(oracle, P, algo):
+    """MPI_Reduce_scatter on device buffers with ragged recvcounts (zeros
+    included), HIP combine, bit-identical to the oracle's simulation"""
+    import torch
+    from mpich_amd import ccl
+    counts = [c * 37 for c in _ragged_counts(P, 200 + P)]
+    sends = float_sends(P, sum(counts), 0x5EED0500)
+    dsend = [torch.from_numpy(s).cuda() for s in sends]
+    drecv = [torch.zeros(max(1, c), dtype=torch.float32, device='cuda') for c in counts]
+    torch.cuda.synchronize()
+    comms = _dev_comms(P)
+    rcs = run_ranks(comms, lambda r, c: ccl.reduce_scatter(dsend[r], drecv[r], counts, MPI_FLOAT,
+                                                           MPI_SUM, c, algo))
+    free_all(comms)
+    assert rcs == [0] * P
+    exp = oracle.rs_schedule([s.view(np.uint8) for s in sends], counts, MPI_FLOAT, MPI_SUM,
+                             'pairwise' if algo.startswith('pairwise') else 'recursive_halving')
+    for r in range(P):
+        assert drecv[r][:counts[r]].cpu().numpy().tobytes() == exp[r].tobytes(), r
 
 
 @pytest.mark.gpu
