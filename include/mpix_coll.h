@@ -129,6 +129,22 @@ int MPIX_Reduce_scatter_async(const void *sendbuf, void *recvbuf, const MPIX_Ain
                               MPIX_Datatype datatype, MPIX_Op op, MPIX_Comm comm, int algorithm,
                               void *workspace, size_t workspace_bytes, void *stream);
 
+/* ---- MPI_Reduce(sendbuf, recvbuf, count, datatype, op, root) ----
+ * (src/mpi/coll/reduce/reduce_intra_{binomial,reduce_scatter_gather}.c):
+ * recvbuf is significant at the root only; the root's sendbuf NULL =
+ * MPI_IN_PLACE.  Non-root ranks accumulate in the workspace (NULL: the
+ * communicator's scratch; else >= MPIX_Reduce_workspace() bytes). */
+#define MPIX_REDUCE_AUTO            0   /* generic.json:206-250: binomial up to 2 KiB or count < pof2 */
+#define MPIX_REDUCE_BINOMIAL        1
+#define MPIX_REDUCE_SCATTER_GATHER  2   /* Rabenseifner: reduce-scatter + binomial gather; count >= pof2 */
+size_t MPIX_Reduce_workspace(MPIX_Aint count, MPIX_Datatype datatype, int root, MPIX_Comm comm);
+int MPIX_Reduce(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Datatype datatype,
+                MPIX_Op op, int root, MPIX_Comm comm, int algorithm, void *workspace,
+                size_t workspace_bytes);
+int MPIX_Reduce_async(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Datatype datatype,
+                      MPIX_Op op, int root, MPIX_Comm comm, int algorithm, void *workspace,
+                      size_t workspace_bytes, void *stream);
+
 /* ---- MPI_Allreduce(sendbuf, recvbuf, count, datatype, op) ----
  * sendbuf NULL = MPI_IN_PLACE (recvbuf holds the input). */
 #define MPIX_ALLREDUCE_AUTO                 0   /* reduce-scatter+allgather if count >= pof2 */

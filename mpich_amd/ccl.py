@@ -61,6 +61,9 @@ def lib():
                                     i32),
             'MPIX_Reduce_scatter_async': ([vp, vp, ctypes.POINTER(aint), i32, i32, vp, i32, vp,
                                            sz, vp], i32),
+            'MPIX_Reduce_workspace': ([aint, i32, i32, vp], sz),
+            'MPIX_Reduce': ([vp, vp, aint, i32, i32, i32, vp, i32, vp, sz], i32),
+            'MPIX_Reduce_async': ([vp, vp, aint, i32, i32, i32, vp, i32, vp, sz, vp], i32),
             'MPIX_Allreduce_workspace': ([aint, i32, vp], sz),
             'MPIX_Allreduce': ([vp, vp, aint, i32, i32, vp, i32, vp, sz], i32),
             'MPIX_Allreduce_async': ([vp, vp, aint, i32, i32, vp, i32, vp, sz, vp], i32),
@@ -169,6 +172,24 @@ def reduce_scatter(sendbuf, recvbuf, recvcounts, datatype, op, comm, algorithm='
     return lib().MPIX_Reduce_scatter_async(_addr(sendbuf), _addr(recvbuf), cnts,
                                            H.as_c_int(datatype), H.as_c_int(op), comm.h, a, ws,
                                            wsb, redop._stream_ptr(stream))
+
+
+REDUCE_ALGORITHMS = {'auto': 0, 'binomial': 1, 'reduce_scatter_gather': 2}
+
+
+def reduce(sendbuf, recvbuf, count, datatype, op, root, comm, algorithm='auto', workspace=None,
+           stream=None, blocking=True):
+    """MPI_Reduce to `root` (the root's sendbuf None = MPI_IN_PLACE; recvbuf
+    only significant at the root); returns the MPI error class."""
+    a = REDUCE_ALGORITHMS[algorithm] if isinstance(algorithm, str) else algorithm
+    ws, wsb = (None, 0) if workspace is None else (_addr(workspace), workspace.numel() *
+                                                    workspace.element_size())
+    if blocking:
+        return lib().MPIX_Reduce(_addr(sendbuf), _addr(recvbuf), count, H.as_c_int(datatype),
+                                 H.as_c_int(op), root, comm.h, a, ws, wsb)
+    return lib().MPIX_Reduce_async(_addr(sendbuf), _addr(recvbuf), count, H.as_c_int(datatype),
+                                   H.as_c_int(op), root, comm.h, a, ws, wsb,
+                                   redop._stream_ptr(stream))
 
 
 def rs_workspace_bytes(recvcounts, datatype, comm, algorithm='auto'):

@@ -547,6 +547,12 @@ size_t rs_workspace(size_t total, size_t mine, size_t ext, int size, int algo)
     }
 }
 
+// MPI_Reduce: tmp_buf, plus the accumulator a non-root rank has no recvbuf for
+size_t reduce_workspace(size_t nb, bool is_root)
+{
+    return round256(nb) + (is_root ? 0 : round256(nb));
+}
+
 size_t rsb_workspace(size_t recvcount, size_t ext, int size, int algo)
 {
     return rs_workspace(recvcount * size, recvcount, ext, size, algo);
@@ -699,6 +705,196 @@ int allreduce_rd(char *rb, size_t count, MPIX_Datatype dt, MPIX_Op op, MPIX_Comm
             TRY(exchange(c, {rcv(rank + 1, rb, nb)}, s));
     }
     return MPIX_REDOP_SUCCESS;
+}
+
+// MPIR_Reduce_intra_binomial (reduce_intra_binomial.c:12-131) for the
+// predefined (commutative) ops: relative to the root, a rank receives from
+// relrank|mask for every mask below its lowest set bit, in increasing mask
+// order, folding each child in with MPIR_Reduce_local(tmp_buf, recvbuf), then
+// sends its result to relrank & ~mask.  acc: the root's recvbuf, or a
+// temporary on the other ranks; tmp: count elements.
+int reduce_binomial(char *acc, size_t count, MPIX_Datatype dt, MPIX_Op op, int root, MPIX_Comm c,
+                    char *tmp, hipStream_t s, size_t ext)
+{
+    const int rank = c->rank, size = c->size;
+    const size_t nb = count * ext;
+    const int relrank = (rank - root + size) % size;
+    for (int mask = 1; mask < size; mask <<= 1) {                           // :84-121
+        if ((mask & relrank) == 0) {
+            int source = relrank | mask;
+            if (source < size) {
+                TRY(exchange(c, {rcv((source + root) % size, tmp, nb)}, s));
+                TRY(combine(c, tmp, acc, (MPIX_Aint) count, dt, op, s));
+            }
+        } else {
+            TRY(exchange(c, {snd(((relrank & ~mask) + root) % size, acc, nb)}, s));
+            break;
+        }
+    }
+    return MPIX_REDOP_SUCCESS;
+}
+
+// MPIR_Reduce_intra_reduce_scatter_gather (reduce_intra_reduce_scatter_gather.c
+// :40-330): odd ranks below 2*rem fold into their EVEN left neighbour (the
+// opposite of the allreduce's pairing), a reduce-scatter by recursive halving
+// with increasing distance over blocks cnts[i] = count/pof2 (+1 for the first
+// count%pof2), then a binomial gather of the finished blocks to the root
+// (an excluded odd root takes block 0 from rank 0 and newrank 0's place).
+int reduce_rsg(char *acc, size_t count, MPIX_Datatype dt, MPIX_Op op, int root, MPIX_Comm c,
+               char *tmp, hipStream_t s, size_t ext)
+{
+    const int rank = c->rank, size = c->size;
+    const int pof2 = pof2_of(size), rem = size - pof2;
+    const size_t nb = count * ext;
+    int newrank;
+    if (rank < 2 * rem) {                                                   // :110-134
+        if (rank % 2) {
+            TRY(exchange(c, {snd(rank - 1, acc, nb)}, s));
+            newrank = -1;
+        } else {
+            TRY(exchange(c, {rcv(rank + 1, tmp, nb)}, s));
+            TRY(combine(c, tmp, acc, (MPIX_Aint) count, dt, op, s));
+            newrank = rank / 2;
+        }
+    } else {
+        newrank = rank - rem;
+    }
+    std::vector<size_t> cnts(pof2, count / pof2), disps(pof2, 0);
+    for (size_t i = 0; i < count % (size_t) pof2; ++i)
+        cnts[i] += 1;
+    for (int i = 1; i < pof2; ++i)
+        disps[i] = disps[i - 1] + cnts[i - 1];
+    auto sum = [&](int lo, int hi) {
+        size_t t = 0;
+        for (int i = lo; i < hi; ++i)
+            t += cnts[i];
+        return t;
+    };
+    int send_idx = 0, recv_idx = 0, last_idx = 0;
+    if (newrank != -1) {                                                    // :150-210
+        last_idx = pof2;
+        for (int mask = 1; mask < pof2;) {
+            int newdst = newrank ^ mask;
+            int dst = newdst < rem ? newdst * 2 : newdst + rem;
+            size_t send_cnt, recv_cnt;
+            if (newrank < newdst) {
+                send_idx = recv_idx + pof2 / (mask * 2);
+                send_cnt = sum(send_idx, last_idx);
+                recv_cnt = sum(recv_idx, send_idx);
+            } else {
+                recv_idx = send_idx + pof2 / (mask * 2);
+                send_cnt = sum(send_idx, recv_idx);
+                recv_cnt = sum(recv_idx, last_idx);
+            }
+            TRY(exchange(c, {snd(dst, acc + disps[send_idx] * ext, send_cnt * ext),
+                             rcv(dst, tmp + disps[recv_idx] * ext, recv_cnt * ext)}, s));
+            TRY(combine(c, tmp + disps[recv_idx] * ext, acc + disps[recv_idx] * ext,
+                        (MPIX_Aint) recv_cnt, dt, op, s));
+            send_idx = recv_idx;
+            mask <<= 1;
+            if (mask < pof2)
+                last_idx = recv_idx + pof2 / mask;
+        }
+    }
+    int newroot;                                                            // :215-250
+    if (root < 2 * rem) {
+        if (root % 2) {
+            if (rank == root) {
+                TRY(exchange(c, {rcv(0, acc, cnts[0] * ext)}, s));
+                newrank = 0;
+                send_idx = 0;
+                last_idx = 2;
+            } else if (newrank == 0) {
+                TRY(exchange(c, {snd(root, acc, cnts[0] * ext)}, s));
+                newrank = -1;
+            }
+            newroot = 0;
+        } else {
+            newroot = root / 2;
+        }
+    } else {
+        newroot = root - rem;
+    }
+    if (newrank != -1) {                                                    // :252-318
+        int j = 0, mask = 1;
+        while (mask < pof2) {
+            mask <<= 1;
+            ++j;
+        }
+        mask >>= 1;
+        --j;
+        while (mask > 0) {
+            int newdst = newrank ^ mask;
+            int dst = newdst < rem ? newdst * 2 : newdst + rem;
+            if (newdst == 0 && root < 2 * rem && root % 2)
+                dst = root;
+            const int newdst_tree_root = (newdst >> j) << j;
+            const int newroot_tree_root = (newroot >> j) << j;
+            size_t send_cnt, recv_cnt;
+            if (newrank < newdst) {
+                if (mask != pof2 / 2)
+                    last_idx = last_idx + pof2 / (mask * 2);
+                recv_idx = send_idx + pof2 / (mask * 2);
+                send_cnt = sum(send_idx, recv_idx);
+                recv_cnt = sum(recv_idx, last_idx);
+            } else {
+                recv_idx = send_idx - pof2 / (mask * 2);
+                send_cnt = sum(send_idx, last_idx);
+                recv_cnt = sum(recv_idx, send_idx);
+            }
+            if (newdst_tree_root == newroot_tree_root) {
+                TRY(exchange(c, {snd(dst, acc + disps[send_idx] * ext, send_cnt * ext)}, s));
+                break;
+            }
+            TRY(exchange(c, {rcv(dst, acc + disps[recv_idx] * ext, recv_cnt * ext)}, s));
+            if (newrank > newdst)
+                send_idx = recv_idx;
+            mask >>= 1;
+            --j;
+        }
+    }
+    return MPIX_REDOP_SUCCESS;
+}
+
+// MPI_Reduce(sendbuf, recvbuf, count, datatype, op, root).  The root's
+// sendbuf NULL = MPI_IN_PLACE; other ranks accumulate in the workspace.
+int reduce_entry(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Datatype dt, MPIX_Op op,
+                 int root, MPIX_Comm c, int algorithm, void *ws, size_t ws_bytes, void *stream,
+                 bool blocking)
+{
+    size_t ext;
+    if (!c)
+        return MPIX_REDOP_ERR_ARG;
+    if (root < 0 || root >= c->size)
+        return MPIX_REDOP_ERR_ARG;      // MPI_ERR_ROOT has no class in mpix_redop.h
+    const bool is_root = c->rank == root;
+    TRY(check_args(c, is_root ? recvbuf : sendbuf, count, dt, op, &ext));
+    if (algorithm < MPIX_REDUCE_AUTO || algorithm > MPIX_REDUCE_SCATTER_GATHER)
+        return MPIX_REDOP_ERR_ARG;
+    if (!count)
+        return MPIX_REDOP_SUCCESS;
+    if (!is_root && !sendbuf)
+        return MPIX_REDOP_ERR_BUFFER;
+    const int pof2 = pof2_of(c->size);
+    const size_t nb = (size_t) count * ext;
+    if (algorithm == MPIX_REDUCE_AUTO)  // generic.json:206-250 (intra, builtin op)
+        algorithm = (nb <= 2048 || (size_t) count < (size_t) pof2) ? MPIX_REDUCE_BINOMIAL
+                                                                   : MPIX_REDUCE_SCATTER_GATHER;
+    if (algorithm == MPIX_REDUCE_SCATTER_GATHER && (size_t) count < (size_t) pof2)
+        return MPIX_REDOP_ERR_COUNT;    // the reference asserts count >= pof2 (:86)
+    TRY(set_device(c));
+    hipStream_t s = stream_of(stream);
+    char *w;
+    TRY(workspace(c, ws, ws_bytes, reduce_workspace(nb, is_root), s, &w));
+    char *acc = is_root ? static_cast<char *>(recvbuf) : w + round256(nb);
+    if (!is_root || sendbuf)                                                // :43-47
+        TRY(copy(c, acc, sendbuf, nb, s));
+    int rc = MPIX_REDOP_SUCCESS;
+    if (c->size > 1)
+        rc = algorithm == MPIX_REDUCE_BINOMIAL
+                 ? reduce_binomial(acc, (size_t) count, dt, op, root, c, w, s, ext)
+                 : reduce_rsg(acc, (size_t) count, dt, op, root, c, w, s, ext);
+    return finish(c, release_scratch(c, w, rc, s), s, blocking);
 }
 
 // MPI_Reduce_scatter (cnts = recvcounts) and MPI_Reduce_scatter_block
@@ -1022,6 +1218,31 @@ int MPIX_Reduce_scatter_async(const void *sendbuf, void *recvbuf, const MPIX_Ain
     TRY(rs_counts(comm, recvcounts, &cnts));
     return rs_entry(sendbuf, recvbuf, cnts, datatype, op, comm, algorithm, workspace,
                     workspace_bytes, stream, false);
+}
+
+size_t MPIX_Reduce_workspace(MPIX_Aint count, MPIX_Datatype datatype, int root, MPIX_Comm comm)
+{
+    size_t ext = (size_t) MPIX_Datatype_extent(datatype);
+    if (!comm || !ext || count <= 0)
+        return 0;
+    return reduce_workspace((size_t) count * ext, comm->rank == root);
+}
+
+int MPIX_Reduce(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Datatype datatype,
+                MPIX_Op op, int root, MPIX_Comm comm, int algorithm, void *workspace,
+                size_t workspace_bytes)
+{
+    return reduce_entry(sendbuf, recvbuf, count, datatype, op, root, comm, algorithm, workspace,
+                        workspace_bytes,
+                        comm ? (comm->stream ? comm->stream : comm->own_stream) : 0, true);
+}
+
+int MPIX_Reduce_async(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Datatype datatype,
+                      MPIX_Op op, int root, MPIX_Comm comm, int algorithm, void *workspace,
+                      size_t workspace_bytes, void *stream)
+{
+    return reduce_entry(sendbuf, recvbuf, count, datatype, op, root, comm, algorithm, workspace,
+                        workspace_bytes, stream, false);
 }
 
 size_t MPIX_Allreduce_workspace(MPIX_Aint count, MPIX_Datatype datatype, MPIX_Comm comm)

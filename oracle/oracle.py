@@ -53,6 +53,8 @@ def lib():
         L.oracle_rs_recursive_halving.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(vp),
                                                   ctypes.POINTER(il), i32, i32, i32]
         L.oracle_rs_pairwise.argtypes = L.oracle_rs_recursive_halving.argtypes
+        L.oracle_reduce_binomial.argtypes = [ctypes.POINTER(vp), vp, il, i32, i32, i32, i32]
+        L.oracle_reduce_rsg.argtypes = L.oracle_reduce_binomial.argtypes
         L.oracle_allreduce_rabenseifner.argtypes = L.oracle_rsb_recursive_halving.argtypes
         L.oracle_allreduce_recursive_doubling.argtypes = L.oracle_rsb_recursive_halving.argtypes
         L.oracle_wtime.restype = ctypes.c_double
@@ -154,6 +156,20 @@ def rs_schedule(sendbufs, recvcounts, datatype, op, algorithm='recursive_halving
     if rc:
         raise RuntimeError('oracle reduce_scatter failed: %d' % rc)
     return recvs
+
+
+def reduce_schedule(sendbufs, count, datatype, op, root, algorithm='binomial'):
+    """Simulate MPI_Reduce to `root` over P ranks with the reference's
+    binomial or reduce_scatter_gather schedule; returns the root's vector."""
+    P = len(sendbufs)
+    out = np.zeros(max(1, count * extent(datatype)), np.uint8)
+    sp = (ctypes.c_void_p * P)(*[s.ctypes.data for s in sendbufs])
+    fn = lib().oracle_reduce_rsg if algorithm == 'reduce_scatter_gather' else \
+        lib().oracle_reduce_binomial
+    rc = fn(sp, out.ctypes.data, count, _i32(datatype), _i32(op), root, P)
+    if rc:
+        raise RuntimeError('oracle reduce failed: %d' % rc)
+    return out[:count * extent(datatype)]
 
 
 def rsb_pairwise(sendbufs, recvcount, datatype, op):

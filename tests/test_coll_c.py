@@ -1,6 +1,6 @@
-"""libmpix_coll.so -- the C++ restatement of MPICH's reduce-scatter and
-allreduce schedules (include/mpix_coll.h) -- driven with P in-process ranks,
-one thread each.
+"""libmpix_coll.so -- the C++ restatement of MPICH's reduce-scatter,
+allreduce and reduce schedules (include/mpix_coll.h) -- driven with P
+in-process ranks, one thread each.
 
 CPU: the host-memory transport with the oracle installed as the combine
 (the product has no CPU compute path), checked bit-for-bit against the
@@ -538,3 +538,104 @@ def test_rccl_communicator_single_rank():
     assert ccl.allreduce(x, z, 1000, MPI_FLOAT, MPI_SUM, c) == 0
     assert torch.equal(x, z)
     assert c.free() == 0
+
+
+# ------------------------------------------------------------ MPI_Reduce
+def _special_doubles(P, n, seed):
+    """values with ties, NaN and +-0 so that the operand order of every
+    MPIR_Reduce_local of the schedule shows in MAX's bits"""
+    rng = np.random.default_rng(seed)
+    out = []
+    for r in range(P):
+        x = rng.integers(-3, 4, n).astype(np.float64)
+        k = rng.random(n)
+        x[k < 0.05] = np.nan
+        x[(k >= 0.05) & (k < 0.15)] = -0.0
+        x[(k >= 0.15) & (k < 0.25)] = 0.0
+        out.append(x)
+    return out
+
+
+@pytest.mark.parametrize('algo', ['binomial', 'reduce_scatter_gather', 'auto'])
+@pytest.mark.parametrize('P', [1, 2, 3, 4, 5, 6, 7, 8])
+def test_reduce_host_matches_oracle(oracle, P, algo):
+    """MPI_Reduce with every root: fp32 SUM and fp64 MAX (NaN / +-0 operand
+    order) bit-identical to the oracle's simulation of
+    reduce_intra_{binomial,reduce_scatter_gather}.c, plus MPI_IN_PLACE at the root"""
+    from mpich_amd import ccl
+    count = 1031
+    comms = host_comms(P, oracle)
+    for dt, op, sends in ((MPI_FLOAT, MPI_SUM, float_sends(P, count, 0x5EED0600)),
+                          (MPI_DOUBLE, MPI_MAX, _special_doubles(P, count, 5))):
+        ext = sends[0].itemsize
+        sim_algo = 'binomial' if algo == 'binomial' or (algo == 'auto' and count * ext <= 2048) \
+            else 'reduce_scatter_gather'
+        for root in range(P):
+            exp = oracle.reduce_schedule([s.view(np.uint8) for s in sends], count, dt, op, root,
+                                         sim_algo)
+            for in_place in (False, True):
+                out = sends[root].copy() if in_place else np.zeros_like(sends[root])
+                rcs = run_ranks(comms, lambda r, c: ccl.reduce(
+                    None if (in_place and r == root) else sends[r], out if r == root else None,
+                    count, dt, op, root, c, algo))
+                assert rcs == [0] * P
+                assert out.view(np.uint8).tobytes() == exp.tobytes(), (dt, root, in_place)
+    free_all(comms)
+
+
+@pytest.mark.parametrize('P', [3, 5, 8])
+def test_reduce_kat(oracle, P):
+    """reduce.c:17-110 (testlist sizes 3, 5, 10): in[i] = i on every rank,
+    result i*P at every root, counts 1..2^16 doubling, with and without
+    MPI_IN_PLACE; the oracle's two simulations give the same closed form"""
+    from mpich_amd import ccl
+    comms = host_comms(P, oracle)
+    count = 1
+    while count < 130000:
+        src = np.arange(count, dtype=np.int32)
+        for algo in ('binomial', 'reduce_scatter_gather'):
+            if algo == 'reduce_scatter_gather' and count < (1 << (P.bit_length() - 1)):
+                continue
+            for root in (0, P - 1, P // 2):
+                out = np.full(count, -1, np.int32)
+                rcs = run_ranks(comms, lambda r, c: ccl.reduce(src, out if r == root else None,
+                                                               count, MPI_INT, MPI_SUM, root, c,
+                                                               algo))
+                assert rcs == [0] * P
+                assert np.array_equal(out, src * P), (count, algo, root)
+                inp = src.copy()
+                rcs = run_ranks(comms, lambda r, c: ccl.reduce(None if r == root else src,
+                                                               inp if r == root else None, count,
+                                                               MPI_INT, MPI_SUM, root, c, algo))
+                assert rcs == [0] * P
+                assert np.array_equal(inp, src * P), (count, algo, root, 'in place')
+                sim = oracle.reduce_schedule([src.view(np.uint8)] * P, count, MPI_INT, MPI_SUM,
+                                             root, algo)
+                assert sim.tobytes() == (src * P).tobytes()
+        count *= 8
+    free_all(comms)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('algo', ['binomial', 'reduce_scatter_gather'])
+@pytest.mark.parametrize('P', [3, 4, 6])
+def test_reduce_device_matches_oracle(oracle, P, algo):
+    """MPI_Reduce on device buffers (device transport, HIP combine), fp64 MAX
+    with NaN / +-0 and fp32 SUM, two roots, bit-identical to the oracle"""
+    import torch
+    from mpich_amd import ccl
+    count = 50021
+    comms = _dev_comms(P)
+    for dt, op, sends in ((MPI_DOUBLE, MPI_MAX, _special_doubles(P, count, 9)),
+                          (MPI_FLOAT, MPI_SUM, float_sends(P, count, 0x5EED0700))):
+        dsend = [torch.from_numpy(s).cuda() for s in sends]
+        for root in (0, P - 1):
+            out = torch.zeros_like(dsend[0])
+            torch.cuda.synchronize()
+            rcs = run_ranks(comms, lambda r, c: ccl.reduce(dsend[r], out if r == root else None,
+                                                           count, dt, op, root, c, algo))
+            assert rcs == [0] * P
+            exp = oracle.reduce_schedule([s.view(np.uint8) for s in sends], count, dt, op, root,
+                                         algo)
+            assert out.cpu().numpy().view(np.uint8).tobytes() == exp.tobytes(), (dt, root)
+    free_all(comms)
