@@ -635,6 +635,38 @@ def allreduce_bench(args, world, rank, dev, res):
                 ms=round(t * 1e3, 3), busbw_GBs=round(2 * (world - 1) / world * n * 4 / t / 1e9, 2))
         except Exception as e:
             res['c_reduce_scatter_allgather'] = dict(error='%s: %s' % (type(e).__name__, e))
+        # MPI_Reduce to rank 0 (reduce_scatter_gather, libmpix_coll over RCCL):
+        # reduce.c KAT first (in[i] = i on every rank, i*P at the root)
+        try:
+            m = 100003
+            x = torch.arange(m, dtype=torch.int32, device=dev)
+            y = torch.full_like(x, -1)
+            redop.check(ccl.reduce(x, y if rank == 0 else None, m, H.MPI_INT, H.MPI_SUM, 0, cc,
+                                   'reduce_scatter_gather'), 'MPIX_Reduce')
+            torch.cuda.synchronize()
+            ok = allreduce_scalar(1 if rank != 0 or bool(torch.all(y == x * world)) else 0,
+                                  dist.ReduceOp.MIN, dev)
+
+            def c_red():
+                redop.check(ccl.reduce(send, recv if rank == 0 else None, n, H.MPI_FLOAT,
+                                       H.MPI_SUM, 0, cc, 'reduce_scatter_gather'), 'MPIX_Reduce')
+            c_red()
+            reps = max(3, min(10, args.steps))
+            dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                c_red()
+            torch.cuda.synchronize()
+            dist.barrier()
+            t = (time.perf_counter() - t0) / reps
+            t = allreduce_scalar(t, dist.ReduceOp.MAX, dev)
+            res['c_reduce_to_root0'] = dict(
+                parity_reduce_c_all_ranks=bool(ok), ms=round(t * 1e3, 3),
+                busbw_GBs=round(n * 4 / t / 1e9, 2),   # nccl-tests: reduce busbw = algbw
+                algorithm='reduce_scatter_gather')
+        except Exception as e:
+            res['c_reduce_to_root0'] = dict(error='%s: %s' % (type(e).__name__, e))
     del send, recv, ws
     torch.cuda.empty_cache()
     return res
