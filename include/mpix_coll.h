@@ -1,5 +1,5 @@
 /*
- * mpix_coll.h -- C-ABI of the reduce-scatter / allreduce schedules that feed
+ * mpix_coll.h -- C-ABI of the reduce-scatter / allreduce / reduce schedules that feed
  * the MI355X local reduction (libmpix_coll.so, built from mpich_amd/csrc/).
  *
  * These are host-side C restatements of MPICH's collective schedules whose
@@ -20,6 +20,11 @@
  *                                  allreduce_intra_reduce_scatter_allgather.c:41-277
  *                                 and MPIR_Allreduce_intra_recursive_doubling
  *                                  allreduce_intra_recursive_doubling.c:24-150
+ *                                 and MPIR_Allreduce_intra_ring  allreduce_intra_ring.c:10-105
+ *   MPIX_Reduce                <- MPIR_Reduce_intra_binomial  src/mpi/coll/reduce/
+ *                                  reduce_intra_binomial.c:12-131
+ *                                 and MPIR_Reduce_intra_reduce_scatter_gather
+ *                                  reduce_intra_reduce_scatter_gather.c:40-330
  *   MPIX_Comm_create_ccl       <- MPIR_RCCLcomm_init  src/util/ccl/rccl.c:21-52
  *                                 (ncclCommInitRank with a unique id the caller
  *                                  broadcasts, as rccl.c:36 does with MPIR_Bcast)
@@ -147,10 +152,14 @@ int MPIX_Reduce_async(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_
 
 /* ---- MPI_Allreduce(sendbuf, recvbuf, count, datatype, op) ----
  * sendbuf NULL = MPI_IN_PLACE (recvbuf holds the input). */
-#define MPIX_ALLREDUCE_AUTO                 0   /* reduce-scatter+allgather if count >= pof2 */
+#define MPIX_ALLREDUCE_AUTO                 0   /* generic.json:99-135: recursive doubling up to
+                                                   8 bytes or below pof2 elements, else
+                                                   reduce-scatter+allgather */
 #define MPIX_ALLREDUCE_RECURSIVE_DOUBLING   1
 #define MPIX_ALLREDUCE_REDUCE_SCATTER_ALLGATHER 2  /* allgather as ONE group of direct exchanges */
 #define MPIX_ALLREDUCE_RSAG_RD_ALLGATHER    3   /* the reference's log2(P) allgather steps */
+#define MPIX_ALLREDUCE_RING                 4   /* allreduce_intra_ring.c: ring reduce-scatter
+                                                   (P-1 steps) + allgather of the blocks */
 size_t MPIX_Allreduce_workspace(MPIX_Aint count, MPIX_Datatype datatype, MPIX_Comm comm);
 int MPIX_Allreduce(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Datatype datatype,
                    MPIX_Op op, MPIX_Comm comm, int algorithm, void *workspace,

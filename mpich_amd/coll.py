@@ -550,13 +550,18 @@ def allreduce_recursive_doubling(sendbuf, recvbuf, count, datatype, op, group=No
 
 def allreduce_auto(sendbuf, recvbuf, count, datatype, op, group=None, **kw):
     """MPI_Allreduce algorithm choice: MPIR_CVAR_ALLREDUCE_INTRA_ALGORITHM
-    (`recursive_doubling` | `reduce_scatter_allgather`) or, by default, the
-    reduce-scatter + allgather schedule whenever count >= pof2 (the
-    condition the reference asserts for it, :127) and recursive doubling
-    below."""
+    (`recursive_doubling` | `reduce_scatter_allgather`) or, by default,
+    generic.json:99-135 for builtin ops: recursive doubling up to 8 bytes of
+    message or below pof2 elements (the reduce-scatter needs count >= pof2,
+    :127), the reduce-scatter + allgather schedule otherwise."""
     algo = os.environ.get('MPIR_CVAR_ALLREDUCE_INTRA_ALGORITHM', 'auto')
     if algo not in ('recursive_doubling', 'reduce_scatter_allgather'):
-        algo = 'reduce_scatter_allgather' if count >= _pof2(dist.get_world_size(group)) \
+        ext = kw.get('extent')
+        if ext is None:
+            from . import redop
+            ext = redop.datatype_extent(datatype)
+        algo = 'reduce_scatter_allgather' \
+            if count * ext > 8 and count >= _pof2(dist.get_world_size(group)) \
             else 'recursive_doubling'
     fn = allreduce if algo == 'reduce_scatter_allgather' else allreduce_recursive_doubling
     return fn(sendbuf, recvbuf, count, datatype, op, group=group, **kw)

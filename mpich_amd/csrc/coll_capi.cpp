@@ -897,6 +897,51 @@ int reduce_entry(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Datat
     return finish(c, release_scratch(c, w, rc, s), s, blocking);
 }
 
+// MPIR_Allreduce_intra_ring (allreduce_intra_ring.c:10-105): blocks of
+// ceil(count/P) (the last ones short or empty); in step i = 0..P-2 a rank
+// sends block (rank-1-i) to rank+1 and folds block (rank-2-i) received from
+// rank-1 into recvbuf.  The allgather only moves finished blocks, so it is
+// ONE group of direct exchanges here (every xGMI link at once) -- same bits
+// as the reference's ring allgatherv.
+int allreduce_ring(char *rb, size_t count, MPIX_Datatype dt, MPIX_Op op, MPIX_Comm c, char *tmp,
+                   hipStream_t s, size_t ext)
+{
+    const int rank = c->rank, size = c->size;
+    std::vector<size_t> cnts(size, 0), displs(size, 0);
+    size_t total = 0;
+    for (int i = 0; i < size; ++i) {                                        // :34-42
+        cnts[i] = (count + size - 1) / size;
+        if (total + cnts[i] > count) {
+            cnts[i] = count - total;
+            break;
+        }
+        total += cnts[i];
+    }
+    for (int i = 1; i < size; ++i)
+        displs[i] = displs[i - 1] + cnts[i - 1];
+    const int src = (size + rank - 1) % size, dst = (rank + 1) % size;
+    for (int i = 0; i < size - 1; ++i) {                                    // :57-76
+        const int recv_rank = (size + rank - 2 - i) % size;
+        const int send_rank = (size + rank - 1 - i) % size;
+        TRY(exchange(c, {rcv(src, tmp, cnts[recv_rank] * ext),
+                         snd(dst, rb + displs[send_rank] * ext, cnts[send_rank] * ext)}, s));
+        TRY(combine(c, tmp, rb + displs[recv_rank] * ext, (MPIX_Aint) cnts[recv_rank], dt, op,
+                    s));
+    }
+    // after step P-2 rank r has folded block r - P = r: that is its finished
+    // block, the one MPIR_Allgatherv_intra_ring then circulates (:79-81)
+    const int mine = rank;
+    std::vector<MPIX_P2p_op> ops;
+    for (int q = 0; q < size; ++q) {
+        if (q == rank)
+            continue;
+        const int theirs = q;
+        ops.push_back(snd(q, rb + displs[mine] * ext, cnts[mine] * ext));
+        ops.push_back(rcv(q, rb + displs[theirs] * ext, cnts[theirs] * ext));
+    }
+    return exchange(c, ops, s);
+}
+
 // MPI_Reduce_scatter (cnts = recvcounts) and MPI_Reduce_scatter_block
 // (equal cnts).  sendbuf NULL = MPI_IN_PLACE: recvbuf holds all ranks' inputs.
 int rs_entry(const void *sendbuf, void *recvbuf, const std::vector<size_t> &cnts, MPIX_Datatype dt,
@@ -961,7 +1006,7 @@ int allreduce_entry(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Da
 {
     size_t ext;
     TRY(check_args(c, recvbuf, count, dt, op, &ext));
-    if (algorithm < MPIX_ALLREDUCE_AUTO || algorithm > MPIX_ALLREDUCE_RSAG_RD_ALLGATHER)
+    if (algorithm < MPIX_ALLREDUCE_AUTO || algorithm > MPIX_ALLREDUCE_RING)
         return MPIX_REDOP_ERR_ARG;
     if (!count)
         return MPIX_REDOP_SUCCESS;
@@ -970,11 +1015,13 @@ int allreduce_entry(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Da
     char *rb = static_cast<char *>(recvbuf);
     const size_t nb = (size_t) count * ext;
     const int pof2 = pof2_of(c->size);
-    if (algorithm == MPIX_ALLREDUCE_AUTO)       // the reference's condition, :127
-        algorithm = (size_t) count >= (size_t) pof2 ? MPIX_ALLREDUCE_REDUCE_SCATTER_ALLGATHER
-                                                    : MPIX_ALLREDUCE_RECURSIVE_DOUBLING;
-    if (algorithm != MPIX_ALLREDUCE_RECURSIVE_DOUBLING && (size_t) count < (size_t) pof2)
-        return MPIX_REDOP_ERR_COUNT;
+    if (algorithm == MPIX_ALLREDUCE_AUTO)       // generic.json:99-135 (builtin ops)
+        algorithm = (nb > 8 && (size_t) count >= (size_t) pof2)
+                        ? MPIX_ALLREDUCE_REDUCE_SCATTER_ALLGATHER
+                        : MPIX_ALLREDUCE_RECURSIVE_DOUBLING;
+    if ((algorithm == MPIX_ALLREDUCE_REDUCE_SCATTER_ALLGATHER ||
+         algorithm == MPIX_ALLREDUCE_RSAG_RD_ALLGATHER) && (size_t) count < (size_t) pof2)
+        return MPIX_REDOP_ERR_COUNT;    // :127
     if (sendbuf)
         TRY(copy(c, rb, sendbuf, nb, s));
     if (c->size == 1)
@@ -983,6 +1030,8 @@ int allreduce_entry(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Da
     TRY(workspace(c, ws, ws_bytes, round256(nb), s, &tmp));
     int rc = algorithm == MPIX_ALLREDUCE_RECURSIVE_DOUBLING
                  ? allreduce_rd(rb, (size_t) count, dt, op, c, tmp, s, ext)
+             : algorithm == MPIX_ALLREDUCE_RING
+                 ? allreduce_ring(rb, (size_t) count, dt, op, c, tmp, s, ext)
                  : allreduce_rsag(rb, (size_t) count, dt, op, c, tmp, s, ext,
                                   algorithm == MPIX_ALLREDUCE_REDUCE_SCATTER_ALLGATHER);
     return finish(c, release_scratch(c, tmp, rc, s), s, blocking);

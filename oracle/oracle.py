@@ -57,6 +57,7 @@ def lib():
         L.oracle_reduce_rsg.argtypes = L.oracle_reduce_binomial.argtypes
         L.oracle_allreduce_rabenseifner.argtypes = L.oracle_rsb_recursive_halving.argtypes
         L.oracle_allreduce_recursive_doubling.argtypes = L.oracle_rsb_recursive_halving.argtypes
+        L.oracle_allreduce_ring.argtypes = L.oracle_rsb_recursive_halving.argtypes
         L.oracle_wtime.restype = ctypes.c_double
         _lib = L
     return _lib
@@ -185,8 +186,8 @@ def allreduce_rabenseifner(sendbufs, count, datatype, op, algorithm='reduce_scat
     recvs = [np.zeros(count * ext, np.uint8) for _ in range(P)]
     sp = (ctypes.c_void_p * P)(*[s.ctypes.data for s in sendbufs])
     rp = (ctypes.c_void_p * P)(*[r.ctypes.data for r in recvs])
-    fn = lib().oracle_allreduce_recursive_doubling if algorithm == 'recursive_doubling' else \
-        lib().oracle_allreduce_rabenseifner
+    fn = {'recursive_doubling': lib().oracle_allreduce_recursive_doubling,
+          'ring': lib().oracle_allreduce_ring}.get(algorithm, lib().oracle_allreduce_rabenseifner)
     rc = fn(sp, rp, count, _i32(datatype), _i32(op), P)
     if rc:
         raise RuntimeError('oracle allreduce failed: %d' % rc)

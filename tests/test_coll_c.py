@@ -107,7 +107,7 @@ def test_rsb_host_redscatblk3(oracle, P, algo):
 
 
 @pytest.mark.parametrize('algo', ['reduce_scatter_allgather', 'rsag_rd_allgather',
-                                  'recursive_doubling'])
+                                  'recursive_doubling', 'ring'])
 @pytest.mark.parametrize('P', [1, 2, 3, 4, 7, 8])
 def test_allreduce_host_matches_oracle_and_kats(oracle, P, algo):
     from mpich_amd import ccl
@@ -120,8 +120,7 @@ def test_allreduce_host_matches_oracle_and_kats(oracle, P, algo):
     assert rcs == [0] * P
     exp = oracle.allreduce_rabenseifner(
         [s.view(np.uint8) for s in sends], count, MPI_FLOAT, MPI_SUM,
-        algorithm='recursive_doubling' if algo == 'recursive_doubling' else
-        'reduce_scatter_allgather')
+        algorithm=algo if algo in ('recursive_doubling', 'ring') else 'reduce_scatter_allgather')
     for r in range(P):
         assert recvs[r].tobytes() == exp[r].tobytes(), r
     # the allred.c KATs generated for this world size, every op and type
@@ -130,7 +129,8 @@ def test_allreduce_host_matches_oracle_and_kats(oracle, P, algo):
     for case in gu.load_cases():
         if case['nranks'] != P or not case['name'].startswith('allred '):
             continue
-        if algo != 'recursive_doubling' and case['count'] < pof2:
+        if algo.startswith('r') and algo != 'recursive_doubling' and algo != 'ring' and \
+                case['count'] < pof2:
             continue
         ext = len(case['expected']) // case['count']
         outs = [np.zeros(case['count'] * ext, np.uint8) for _ in range(P)]
@@ -144,6 +144,40 @@ def test_allreduce_host_matches_oracle_and_kats(oracle, P, algo):
     free_all(comms)
     if P in (4, 7):
         assert ncase > 0
+
+
+@pytest.mark.parametrize('P', [2, 3, 5, 8])
+def test_allreduce_ring_ragged_and_auto_rule(oracle, P):
+    """the ring with counts that leave short and empty blocks (fp64 MAX over
+    NaN / +-0: every step's operand order shows), and the generic.json:114-117
+    rule: up to 8 bytes the auto choice is recursive doubling even at
+    count >= pof2"""
+    from mpich_amd import ccl
+    comms = host_comms(P, oracle)
+    for count in (1, P - 1, P + 1, 3 * P - 2, 1000):
+        sends = _special_doubles(P, count, count)
+        outs = [np.zeros(count) for _ in range(P)]
+        rcs = run_ranks(comms, lambda r, c: ccl.allreduce(sends[r], outs[r], count, MPI_DOUBLE,
+                                                           MPI_MAX, c, 'ring'))
+        assert rcs == [0] * P
+        exp = oracle.allreduce_rabenseifner([s.view(np.uint8) for s in sends], count, MPI_DOUBLE,
+                                            MPI_MAX, algorithm='ring')
+        for r in range(P):
+            assert outs[r].view(np.uint8).tobytes() == exp[r].tobytes(), (count, r)
+    pof2 = 1 << (P.bit_length() - 1)
+    for count in (max(1, 8 // 8), pof2):        # 8 bytes -> recursive doubling; > 8 -> RSAG
+        sends = _special_doubles(P, count, 77 + count)
+        outs = [np.zeros(count) for _ in range(P)]
+        rcs = run_ranks(comms, lambda r, c: ccl.allreduce(sends[r], outs[r], count, MPI_DOUBLE,
+                                                           MPI_MAX, c, 'auto'))
+        assert rcs == [0] * P
+        algo = 'recursive_doubling' if count * 8 <= 8 or count < pof2 else \
+            'reduce_scatter_allgather'
+        exp = oracle.allreduce_rabenseifner([s.view(np.uint8) for s in sends], count, MPI_DOUBLE,
+                                            MPI_MAX, algorithm=algo)
+        for r in range(P):
+            assert outs[r].view(np.uint8).tobytes() == exp[r].tobytes(), (count, r)
+    free_all(comms)
 
 
 def test_in_place_allreduce_and_workspace(oracle):
@@ -374,7 +408,7 @@ def test_rsb_device_local_types(oracle, dt, op, algo):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize('algo', ['reduce_scatter_allgather', 'rsag_rd_allgather',
-                                  'recursive_doubling'])
+                                  'recursive_doubling', 'ring'])
 @pytest.mark.parametrize('P', [2, 3, 4, 7, 8])
 def test_allreduce_device_local_matches_oracle(oracle, P, algo):
     import torch
@@ -392,8 +426,7 @@ def test_allreduce_device_local_matches_oracle(oracle, P, algo):
     free_all(comms)
     exp = oracle.allreduce_rabenseifner(
         [s.view(np.uint8) for s in sends], count, MPI_FLOAT, MPI_SUM,
-        algorithm='recursive_doubling' if algo == 'recursive_doubling' else
-        'reduce_scatter_allgather')
+        algorithm=algo if algo in ('recursive_doubling', 'ring') else 'reduce_scatter_allgather')
     for r in range(P):
         assert drecv[r].cpu().numpy().tobytes() == exp[r].tobytes(), r
 
