@@ -150,6 +150,23 @@ int MPIX_Reduce_async(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_
                       MPIX_Op op, int root, MPIX_Comm comm, int algorithm, void *workspace,
                       size_t workspace_bytes, void *stream);
 
+/* ---- MPI_Scan / MPI_Exscan(sendbuf, recvbuf, count, datatype, op) ----
+ * (src/mpi/coll/scan/scan_intra_recursive_doubling.c:60-150,
+ * src/mpi/coll/exscan/exscan_intra_recursive_doubling.c:60-160): sendbuf
+ * NULL = MPI_IN_PLACE; Exscan leaves rank 0's recvbuf untouched.  workspace:
+ * NULL or >= MPIX_Scan_workspace() bytes (partial scan + incoming buffer). */
+size_t MPIX_Scan_workspace(MPIX_Aint count, MPIX_Datatype datatype, MPIX_Comm comm);
+int MPIX_Scan(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Datatype datatype,
+              MPIX_Op op, MPIX_Comm comm, void *workspace, size_t workspace_bytes);
+int MPIX_Scan_async(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Datatype datatype,
+                    MPIX_Op op, MPIX_Comm comm, void *workspace, size_t workspace_bytes,
+                    void *stream);
+int MPIX_Exscan(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Datatype datatype,
+                MPIX_Op op, MPIX_Comm comm, void *workspace, size_t workspace_bytes);
+int MPIX_Exscan_async(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Datatype datatype,
+                      MPIX_Op op, MPIX_Comm comm, void *workspace, size_t workspace_bytes,
+                      void *stream);
+
 /* ---- MPI_Allreduce(sendbuf, recvbuf, count, datatype, op) ----
  * sendbuf NULL = MPI_IN_PLACE (recvbuf holds the input). */
 #define MPIX_ALLREDUCE_AUTO                 0   /* generic.json:99-135: recursive doubling up to

@@ -65,6 +65,11 @@ def lib():
             'MPIX_Reduce_workspace': ([aint, i32, i32, vp], sz),
             'MPIX_Reduce': ([vp, vp, aint, i32, i32, i32, vp, i32, vp, sz], i32),
             'MPIX_Reduce_async': ([vp, vp, aint, i32, i32, i32, vp, i32, vp, sz, vp], i32),
+            'MPIX_Scan_workspace': ([aint, i32, vp], sz),
+            'MPIX_Scan': ([vp, vp, aint, i32, i32, vp, vp, sz], i32),
+            'MPIX_Scan_async': ([vp, vp, aint, i32, i32, vp, vp, sz, vp], i32),
+            'MPIX_Exscan': ([vp, vp, aint, i32, i32, vp, vp, sz], i32),
+            'MPIX_Exscan_async': ([vp, vp, aint, i32, i32, vp, vp, sz, vp], i32),
             'MPIX_Allreduce_workspace': ([aint, i32, vp], sz),
             'MPIX_Allreduce': ([vp, vp, aint, i32, i32, vp, i32, vp, sz], i32),
             'MPIX_Allreduce_async': ([vp, vp, aint, i32, i32, vp, i32, vp, sz, vp], i32),
@@ -191,6 +196,21 @@ def reduce(sendbuf, recvbuf, count, datatype, op, root, comm, algorithm='auto', 
     return lib().MPIX_Reduce_async(_addr(sendbuf), _addr(recvbuf), count, H.as_c_int(datatype),
                                    H.as_c_int(op), root, comm.h, a, ws, wsb,
                                    redop._stream_ptr(stream))
+
+
+def scan(sendbuf, recvbuf, count, datatype, op, comm, exclusive=False, workspace=None,
+         stream=None, blocking=True):
+    """MPI_Scan, or MPI_Exscan with exclusive=True (sendbuf None =
+    MPI_IN_PLACE); returns the MPI error class."""
+    ws, wsb = (None, 0) if workspace is None else (_addr(workspace), workspace.numel() *
+                                                    workspace.element_size())
+    name = 'MPIX_Exscan' if exclusive else 'MPIX_Scan'
+    if blocking:
+        return getattr(lib(), name)(_addr(sendbuf), _addr(recvbuf), count, H.as_c_int(datatype),
+                                    H.as_c_int(op), comm.h, ws, wsb)
+    return getattr(lib(), name + '_async')(_addr(sendbuf), _addr(recvbuf), count,
+                                           H.as_c_int(datatype), H.as_c_int(op), comm.h, ws, wsb,
+                                           redop._stream_ptr(stream))
 
 
 def rs_workspace_bytes(recvcounts, datatype, comm, algorithm='auto'):

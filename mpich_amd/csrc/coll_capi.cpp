@@ -856,6 +856,65 @@ int reduce_rsg(char *acc, size_t count, MPIX_Datatype dt, MPIX_Op op, int root, 
     return MPIX_REDOP_SUCCESS;
 }
 
+// MPIR_Scan_intra_recursive_doubling (scan_intra_recursive_doubling.c:60-150)
+// and MPIR_Exscan_intra_recursive_doubling (exscan_intra_recursive_doubling.c
+// :60-160), commutative ops: partial_scan travels to rank ^ mask each step; a
+// rank above its partner folds the incoming partial into partial_scan and
+// into its result (Exscan: the first one is copied, not folded; rank 0's
+// result is left untouched), a rank below folds it into partial_scan only.
+// rb already holds the own contribution for Scan; ps = partial_scan.
+int scan_rd(char *rb, char *ps, size_t count, MPIX_Datatype dt, MPIX_Op op, MPIX_Comm c,
+            char *tmp, hipStream_t s, size_t ext, bool exclusive)
+{
+    const int rank = c->rank, size = c->size;
+    const size_t nb = count * ext;
+    bool flag = false;
+    for (int mask = 1; mask < size; mask <<= 1) {
+        const int dst = rank ^ mask;
+        if (dst >= size)
+            continue;
+        TRY(exchange(c, {snd(dst, ps, nb), rcv(dst, tmp, nb)}, s));
+        if (rank > dst) {
+            TRY(combine(c, tmp, ps, (MPIX_Aint) count, dt, op, s));
+            if (!exclusive) {
+                TRY(combine(c, tmp, rb, (MPIX_Aint) count, dt, op, s));
+            } else if (rank != 0) {
+                if (!flag)
+                    TRY(copy(c, rb, tmp, nb, s));
+                else
+                    TRY(combine(c, tmp, rb, (MPIX_Aint) count, dt, op, s));
+                flag = true;
+            }
+        } else {
+            TRY(combine(c, tmp, ps, (MPIX_Aint) count, dt, op, s));
+        }
+    }
+    return MPIX_REDOP_SUCCESS;
+}
+
+int scan_entry(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Datatype dt, MPIX_Op op,
+               MPIX_Comm c, void *ws, size_t ws_bytes, void *stream, bool blocking,
+               bool exclusive)
+{
+    size_t ext;
+    TRY(check_args(c, recvbuf, count, dt, op, &ext));
+    if (!count)
+        return MPIX_REDOP_SUCCESS;
+    TRY(set_device(c));
+    hipStream_t s = stream_of(stream);
+    char *rb = static_cast<char *>(recvbuf);
+    const size_t nb = (size_t) count * ext;
+    char *w;
+    TRY(workspace(c, ws, ws_bytes, 2 * round256(nb), s, &w));
+    char *ps = w, *tmp = w + round256(nb);
+    const void *own = sendbuf ? sendbuf : recvbuf;      // NULL = MPI_IN_PLACE
+    TRY(copy(c, ps, own, nb, s));
+    if (!exclusive && sendbuf)
+        TRY(copy(c, rb, sendbuf, nb, s));
+    int rc = scan_rd(rb, ps, (size_t) count, dt, op, c, tmp, s, ext, exclusive);
+    return finish(c, release_scratch(c, w, rc, s), s, blocking);
+}
+
 // MPI_Reduce(sendbuf, recvbuf, count, datatype, op, root).  The root's
 // sendbuf NULL = MPI_IN_PLACE; other ranks accumulate in the workspace.
 int reduce_entry(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Datatype dt, MPIX_Op op,
@@ -1292,6 +1351,44 @@ int MPIX_Reduce_async(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_
 {
     return reduce_entry(sendbuf, recvbuf, count, datatype, op, root, comm, algorithm, workspace,
                         workspace_bytes, stream, false);
+}
+
+size_t MPIX_Scan_workspace(MPIX_Aint count, MPIX_Datatype datatype, MPIX_Comm comm)
+{
+    size_t ext = (size_t) MPIX_Datatype_extent(datatype);
+    if (!comm || !ext || count <= 0)
+        return 0;
+    return 2 * round256((size_t) count * ext);
+}
+
+int MPIX_Scan(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Datatype datatype,
+              MPIX_Op op, MPIX_Comm comm, void *workspace, size_t workspace_bytes)
+{
+    return scan_entry(sendbuf, recvbuf, count, datatype, op, comm, workspace, workspace_bytes,
+                      comm ? (comm->stream ? comm->stream : comm->own_stream) : 0, true, false);
+}
+
+int MPIX_Scan_async(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Datatype datatype,
+                    MPIX_Op op, MPIX_Comm comm, void *workspace, size_t workspace_bytes,
+                    void *stream)
+{
+    return scan_entry(sendbuf, recvbuf, count, datatype, op, comm, workspace, workspace_bytes,
+                      stream, false, false);
+}
+
+int MPIX_Exscan(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Datatype datatype,
+                MPIX_Op op, MPIX_Comm comm, void *workspace, size_t workspace_bytes)
+{
+    return scan_entry(sendbuf, recvbuf, count, datatype, op, comm, workspace, workspace_bytes,
+                      comm ? (comm->stream ? comm->stream : comm->own_stream) : 0, true, true);
+}
+
+int MPIX_Exscan_async(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Datatype datatype,
+                      MPIX_Op op, MPIX_Comm comm, void *workspace, size_t workspace_bytes,
+                      void *stream)
+{
+    return scan_entry(sendbuf, recvbuf, count, datatype, op, comm, workspace, workspace_bytes,
+                      stream, false, true);
 }
 
 size_t MPIX_Allreduce_workspace(MPIX_Aint count, MPIX_Datatype datatype, MPIX_Comm comm)

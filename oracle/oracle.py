@@ -58,6 +58,7 @@ def lib():
         L.oracle_allreduce_rabenseifner.argtypes = L.oracle_rsb_recursive_halving.argtypes
         L.oracle_allreduce_recursive_doubling.argtypes = L.oracle_rsb_recursive_halving.argtypes
         L.oracle_allreduce_ring.argtypes = L.oracle_rsb_recursive_halving.argtypes
+        L.oracle_scan.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(vp), il, i32, i32, i32, i32]
         L.oracle_wtime.restype = ctypes.c_double
         _lib = L
     return _lib
@@ -171,6 +172,18 @@ def reduce_schedule(sendbufs, count, datatype, op, root, algorithm='binomial'):
     if rc:
         raise RuntimeError('oracle reduce failed: %d' % rc)
     return out[:count * extent(datatype)]
+
+
+def scan_schedule(sendbufs, recvbufs, count, datatype, op, exclusive=False):
+    """Simulate MPI_Scan / MPI_Exscan (recursive doubling) over P ranks;
+    recvbufs (uint8 arrays) are updated in place."""
+    P = len(sendbufs)
+    sp = (ctypes.c_void_p * P)(*[s.ctypes.data for s in sendbufs])
+    rp = (ctypes.c_void_p * P)(*[r.ctypes.data for r in recvbufs])
+    rc = lib().oracle_scan(sp, rp, count, _i32(datatype), _i32(op), P, int(exclusive))
+    if rc:
+        raise RuntimeError('oracle scan failed: %d' % rc)
+    return recvbufs
 
 
 def rsb_pairwise(sendbufs, recvcount, datatype, op):

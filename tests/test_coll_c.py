@@ -1,5 +1,5 @@
 """libmpix_coll.so -- the C++ restatement of MPICH's reduce-scatter,
-allreduce and reduce schedules (include/mpix_coll.h) -- driven with P
+allreduce, reduce and scan schedules (include/mpix_coll.h) -- driven with P
 in-process ranks, one thread each.
 
 CPU: the host-memory transport with the oracle installed as the combine
@@ -672,3 +672,85 @@ def test_reduce_device_matches_oracle(oracle, P, algo):
                                          algo)
             assert out.cpu().numpy().view(np.uint8).tobytes() == exp.tobytes(), (dt, root)
     free_all(comms)
+
+
+# ------------------------------------------------------- MPI_Scan / Exscan
+@pytest.mark.parametrize('exclusive', [False, True])
+@pytest.mark.parametrize('P', [1, 2, 3, 4, 5, 7, 8])
+def test_scan_host_matches_oracle(oracle, P, exclusive):
+    """recursive-doubling Scan / Exscan, fp64 MAX over NaN / +-0 (operand
+    order in the bits) and fp32 SUM, plain and MPI_IN_PLACE, against the
+    oracle's simulation"""
+    from mpich_amd import ccl
+    count = 777
+    comms = host_comms(P, oracle)
+    for dt, op, sends in ((MPI_DOUBLE, MPI_MAX, _special_doubles(P, count, 21)),
+                          (MPI_FLOAT, MPI_SUM, float_sends(P, count, 0x5EED0800))):
+        for in_place in (False, True):
+            prior = [np.full_like(s, 7) for s in sends]         # Exscan: rank 0 keeps these
+            outs = [s.copy() if in_place else p.copy() for s, p in zip(sends, prior)]
+            rcs = run_ranks(comms, lambda r, c: ccl.scan(None if in_place else sends[r], outs[r],
+                                                         count, dt, op, c, exclusive))
+            assert rcs == [0] * P
+            exp = [(s.copy() if in_place else p.copy()).view(np.uint8)
+                   for s, p in zip(sends, prior)]
+            oracle.scan_schedule([s.view(np.uint8) for s in sends], exp, count, dt, op,
+                                 exclusive)
+            for r in range(P):
+                assert outs[r].view(np.uint8).tobytes() == exp[r].tobytes(), (dt, in_place, r)
+    free_all(comms)
+
+
+@pytest.mark.parametrize('P', [4, 5, 10])
+def test_scan_exscan_kats(oracle, P):
+    """scantst.c:60-70 (data = rank, result sum 0..rank) and exscan.c:38-85
+    (counts 1..2^15, in[i] = rank + i*P, result rank*i*P + rank(rank-1)/2 on
+    rank > 0; MPI_IN_PLACE leaves rank 0's buffer as it was)"""
+    from mpich_amd import ccl
+    comms = host_comms(P, oracle)
+    outs = [np.full(1, -100, np.int32) for _ in range(P)]
+    rcs = run_ranks(comms, lambda r, c: ccl.scan(np.array([r], np.int32), outs[r], 1, MPI_INT,
+                                                 MPI_SUM, c))
+    assert rcs == [0] * P
+    assert [int(o[0]) for o in outs] == [r * (r + 1) // 2 for r in range(P)]
+    count = 1
+    while count < 65000:
+        i = np.arange(count)
+        sends = [(r + i * P).astype(np.int32) for r in range(P)]
+        outs = [np.full(count, -1, np.int32) for _ in range(P)]
+        rcs = run_ranks(comms, lambda r, c: ccl.scan(sends[r], outs[r], count, MPI_INT, MPI_SUM,
+                                                     c, exclusive=True))
+        assert rcs == [0] * P
+        for r in range(1, P):
+            assert np.array_equal(outs[r], r * i * P + r * (r - 1) // 2), (count, r)
+        bufs = [s.copy() for s in sends]
+        rcs = run_ranks(comms, lambda r, c: ccl.scan(None, bufs[r], count, MPI_INT, MPI_SUM, c,
+                                                     exclusive=True))
+        assert rcs == [0] * P
+        assert np.array_equal(bufs[0], sends[0])
+        for r in range(1, P):
+            assert np.array_equal(bufs[r], r * i * P + r * (r - 1) // 2), (count, r)
+        count *= 4
+    free_all(comms)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('exclusive', [False, True])
+def test_scan_device_matches_oracle(oracle, exclusive):
+    import torch
+    from mpich_amd import ccl
+    P, count = 6, 30011
+    sends = _special_doubles(P, count, 41)
+    dsend = [torch.from_numpy(s).cuda() for s in sends]
+    douts = [torch.full((count,), 7.0, dtype=torch.float64, device='cuda') for _ in range(P)]
+    torch.cuda.synchronize()
+    comms = _dev_comms(P)
+    rcs = run_ranks(comms, lambda r, c: ccl.scan(dsend[r], douts[r], count, MPI_DOUBLE, MPI_MAX,
+                                                 c, exclusive))
+    free_all(comms)
+    assert rcs == [0] * P
+    exp = [np.full(count, 7.0).view(np.uint8) for _ in range(P)]
+    oracle.scan_schedule([s.view(np.uint8) for s in sends], exp, count, MPI_DOUBLE, MPI_MAX,
+                         exclusive)
+    for r in range(P):
+        assert douts[r].cpu().numpy().view(np.uint8).tobytes() == exp[r].tobytes(), r
