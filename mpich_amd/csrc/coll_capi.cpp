@@ -510,8 +510,16 @@ int rs_pairwise(const char *sb, char *rb, const std::vector<size_t> &cnts, MPIX_
         if (cnts[rank])
             TRY(combine_multi(c, ins, acc, (MPIX_Aint) cnts[rank], dt, op, s));
     }
-    if (in_place && rank != 0)
-        TRY(copy(c, rb, acc, blk, s));
+    if (in_place && rank != 0) {
+        // with uneven counts the own block can overlap the front of recvbuf;
+        // device copies must not overlap, so go through the (free) workspace
+        if (disps[rank] * ext < blk && !c->host()) {
+            TRY(copy(c, ws, acc, blk, s));
+            TRY(copy(c, rb, ws, blk, s));
+        } else {
+            TRY(copy(c, rb, acc, blk, s));
+        }
+    }
     return MPIX_REDOP_SUCCESS;
 }
 

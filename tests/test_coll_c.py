@@ -493,6 +493,30 @@ def test_reduce_scatter_device_ragged(oracle, P, algo):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize('algo', ['recursive_halving', 'pairwise', 'pairwise_sequential'])
+def test_reduce_scatter_device_in_place_overlap(oracle, algo):
+    """MPI_IN_PLACE with uneven counts where a rank's own block overlaps the
+    front of recvbuf (counts [1, 4000, 3, 9000]: rank 1's block at offset 1
+    is moved to offset 0), device buffers"""
+    import torch
+    from mpich_amd import ccl
+    counts = [1, 4000, 3, 9000]
+    P = len(counts)
+    sends = float_sends(P, sum(counts), 0x5EED0900)
+    bufs = [torch.from_numpy(s.copy()).cuda() for s in sends]
+    torch.cuda.synchronize()
+    comms = _dev_comms(P)
+    rcs = run_ranks(comms, lambda r, c: ccl.reduce_scatter(None, bufs[r], counts, MPI_FLOAT,
+                                                           MPI_SUM, c, algo))
+    free_all(comms)
+    assert rcs == [0] * P
+    exp = oracle.rs_schedule([s.view(np.uint8) for s in sends], counts, MPI_FLOAT, MPI_SUM,
+                             'pairwise' if algo.startswith('pairwise') else 'recursive_halving')
+    for r in range(P):
+        assert bufs[r][:counts[r]].cpu().numpy().tobytes() == exp[r].tobytes(), r
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('algo', ['recursive_halving', 'pairwise', 'pairwise_sequential'])
 def test_rsb_device_in_place(oracle, algo):
     """MPI_IN_PLACE on device buffers: inputs in recvbuf, result in its
     first block, bit-identical to the oracle's simulation"""
