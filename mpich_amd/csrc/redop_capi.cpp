@@ -290,7 +290,26 @@ struct DevState {
     char *bounce_dev = nullptr; // its device mapping
     size_t bounce_half = 0;
 };
-thread_local DevState *t_dev = nullptr;   // array of kMaxDev, never freed implicitly
+// Per-thread device state (streams, flag word, scratch).  A thread that exits
+// hands its array to a process-wide pool and the next new thread takes it over
+// instead of creating streams of its own, so MPI_THREAD_MULTIPLE codes that
+// spawn and join worker threads keep a bounded set of HIP streams.  The hand-off
+// makes no HIP call (it may run at process exit); work still queued on the
+// streams stays ordered ahead of the next owner's.  MPIX_Redop_finalize frees
+// the caller's array and the pooled ones.
+std::mutex g_pool_mu;
+std::vector<DevState *> *g_pool = new std::vector<DevState *>();  // never destroyed
+struct DevHolder {
+    DevState *arr = nullptr;
+    ~DevHolder()
+    {
+        if (arr) {
+            std::lock_guard<std::mutex> l(g_pool_mu);
+            g_pool->push_back(arr);
+        }
+    }
+};
+thread_local DevHolder t_dev;
 
 int set_err(int e)
 {
@@ -311,9 +330,16 @@ DevState *dev_state(int dev)
 {
     if (dev < 0 || dev >= kMaxDev)
         return nullptr;
-    if (!t_dev)
-        t_dev = new DevState[kMaxDev];
-    DevState &d = t_dev[dev];
+    if (!t_dev.arr) {
+        std::lock_guard<std::mutex> l(g_pool_mu);
+        if (!g_pool->empty()) {
+            t_dev.arr = g_pool->back();
+            g_pool->pop_back();
+        } else {
+            t_dev.arr = new DevState[kMaxDev];
+        }
+    }
+    DevState &d = t_dev.arr[dev];
     if (!d.init) {
         for (int k = 0; k < 2; ++k)
             if (hipStreamCreateWithFlags(&d.s[k], hipStreamNonBlocking) != hipSuccess)
@@ -731,12 +757,10 @@ int MPIX_Redop_init(void)
     return set_err(dev_state(dev) ? MPIX_REDOP_SUCCESS : MPIX_REDOP_ERR_OTHER);
 }
 
-int MPIX_Redop_finalize(void)
+static void free_states(DevState *arr)
 {
-    if (!t_dev)
-        return MPIX_REDOP_SUCCESS;
     for (int i = 0; i < kMaxDev; ++i) {
-        DevState &d = t_dev[i];
+        DevState &d = arr[i];
         if (!d.init)
             continue;
         DeviceGuard g(i);
@@ -759,8 +783,21 @@ int MPIX_Redop_finalize(void)
             (void) hipHostFree(d.bounce);
         d = DevState();
     }
-    delete[] t_dev;
-    t_dev = nullptr;
+    delete[] arr;
+}
+
+int MPIX_Redop_finalize(void)
+{
+    std::vector<DevState *> pooled;
+    {
+        std::lock_guard<std::mutex> l(g_pool_mu);
+        pooled.swap(*g_pool);
+    }
+    if (t_dev.arr)
+        pooled.push_back(t_dev.arr);
+    t_dev.arr = nullptr;
+    for (DevState *arr : pooled)
+        free_states(arr);
     return MPIX_REDOP_SUCCESS;
 }
 

@@ -596,6 +596,33 @@ def test_concurrent_callers(R, H, oracle):
     assert np.all(host(y).view(np.float32) == 2)
 
 
+def test_thread_churn(R, H):
+    """Worker threads that exit without finalizing hand their streams to a
+    pool that later threads take over (redop_capi.cpp DevHolder): 96
+    short-lived threads, 8 at a time, each reducing its own slice."""
+    import threading
+    n, nthreads = 4099, 96
+    a = dev(np.arange(n * nthreads, dtype=np.int64))
+    b = dev(np.full(n * nthreads, 3, np.int64))
+    errs = []
+
+    def work(t):
+        torch.cuda.set_device(0)
+        off = t * n * 8
+        rc = R.MPI_Reduce_local(b[off:], a[off:], n, H.MPI_LONG, H.MPI_SUM)
+        if rc:
+            errs.append(rc)
+
+    for base in range(0, nthreads, 8):
+        th = [threading.Thread(target=work, args=(t,)) for t in range(base, base + 8)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+    assert not errs
+    assert np.array_equal(host(a).view(np.int64), np.arange(n * nthreads, dtype=np.int64) + 3)
+
+
 @pytest.mark.parametrize('dtname,opname', [('MPI_DOUBLE', 'MPI_SUM'), ('MPI_INT', 'MPI_BXOR'),
                                            ('MPI_C_FLOAT_COMPLEX', 'MPI_PROD'),
                                            ('MPI_SHORT', 'MPI_MIN')])
