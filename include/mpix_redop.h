@@ -148,7 +148,9 @@ typedef intptr_t MPIX_Aint;     /* MPI_Aint on LP64 */
 
 /* ---- library lifetime ----
  * init is optional (every entry point initialises lazily); finalize frees
- * the per-thread streams and the host-staging scratch. */
+ * the calling thread's streams and host-staging scratch, and those that
+ * exited threads left in the reuse pool (a thread that exits without
+ * finalizing hands its state to the next new thread). */
 int MPIX_Redop_init(void);
 int MPIX_Redop_finalize(void);
 

@@ -16,6 +16,7 @@
 #include <string.h>
 
 #include <atomic>
+#include <chrono>
 #include <mutex>
 #include <vector>
 
@@ -234,9 +235,11 @@ const Entry *gpu_entry(uint32_t opi, uint32_t it)
 std::atomic<long long> g_ftrue{1}, g_ffalse{0};
 std::atomic<int> g_block{256}, g_max_grid{0};
 // completion wait of the synchronous calls: 0 block (hipStreamSynchronize),
-// 1 spin on an event, 2 spin on a pinned host word the stream writes after the
-// kernel (hipStreamWriteValue32; default: 10.1 vs 13.2 us for a 1-element
-// call, profiles/r01_lat_probe.txt) -- MPIX_REDOP_SYNC=block|event|flag
+// 1 spin on an event, 2 spin on a pinned host word that a one-workgroup
+// contiguous kernel stores itself and the stream writes after any other
+// kernel (hipStreamWriteValue32; default), 3 the same word always written by
+// the stream (10.1 vs 13.2 us for a 1-element call against the event,
+// profiles/r01_lat_probe.txt) -- MPIX_REDOP_SYNC=block|event|flag|stream
 std::atomic<int> g_sync{2};
 std::atomic<bool> g_zero_copy{true}; // MPIX_REDOP_PINNED=stage stages pinned host memory too
 std::once_flag g_env_once;
@@ -257,7 +260,10 @@ void read_env()
     if (const char *s = getenv("MPIX_REDOP_MAXGRID"))
         g_max_grid = atoi(s) > 0 ? atoi(s) : 0;
     if (const char *s = getenv("MPIX_REDOP_SYNC"))
-        g_sync = strcmp(s, "block") == 0 ? 0 : (strcmp(s, "flag") == 0 ? 2 : 1);
+        g_sync = strcmp(s, "block") == 0 ? 0
+               : strcmp(s, "flag") == 0  ? 2
+               : strcmp(s, "stream") == 0 ? 3
+                                          : 1;
     if (const char *s = getenv("MPIX_REDOP_PINNED"))
         g_zero_copy = strcmp(s, "stage") != 0;
     if (const char *s = getenv("MPIX_REDOP_STAGE_CHUNK")) {
@@ -280,6 +286,7 @@ struct DevState {
     hipStream_t s[2] = {nullptr, nullptr};
     hipEvent_t done = nullptr;          // completion marker for the spin wait
     volatile uint32_t *flag = nullptr;  // pinned host word for MPIX_REDOP_SYNC=flag
+    uint32_t *flag_ctr = nullptr;       // device word: workgroups done (Params::done_ctr)
     uint32_t seq = 0;
     void *scratch = nullptr;    // 2 slots x (in chunk + inout chunk)
     size_t scratch_bytes = 0;
@@ -350,6 +357,13 @@ DevState *dev_state(int dev)
         if (hipHostMalloc(&f, 64, hipHostMallocCoherent) == hipSuccess) {
             d.flag = (volatile uint32_t *) f;
             *d.flag = 0;
+            void *c = nullptr;
+            if (hipMalloc(&c, 256) == hipSuccess) {
+                if (hipMemset(c, 0, 256) == hipSuccess)
+                    d.flag_ctr = (uint32_t *) c;
+                else
+                    (void) hipFree(c);
+            }
         }
         d.init = true;
     }
@@ -375,7 +389,7 @@ int wait_stream(DevState *d, hipStream_t s)
     if (mode == 0)
         return hip_err(hipStreamSynchronize(s));
     hipError_t e;
-    if (mode == 2 && d->flag) {
+    if ((mode == 2 || mode == 3) && d->flag) {
         uint32_t seq = ++d->seq;
         e = hipStreamWriteValue32(s, (void *) d->flag, seq, 0);
         if (e != hipSuccess)
@@ -467,9 +481,15 @@ int validate(const void *in, const void *io, MPIX_Aint count, uint32_t dt, uint3
 }
 
 // Enqueue on a stream; both buffers device-accessible, arguments validated.
+// done/seq (synchronous callers): on success with *signalled set, seq will be
+// stored to *done once the result is complete (Params::done; ctr: its
+// workgroup counter, NULL = one workgroup only).
 int enqueue(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext, uint32_t op,
-            hipStream_t s)
+            hipStream_t s, uint32_t *done = nullptr, uint32_t *ctr = nullptr, uint32_t seq = 0,
+            bool *signalled = nullptr)
 {
+    if (signalled)
+        *signalled = false;
     uint32_t opi = op & 0xf;
     if (opi == 14)      // MPI_NO_OP
         return MPIX_REDOP_SUCCESS;
@@ -481,16 +501,46 @@ int enqueue(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext,
     const Entry *e = gpu_entry(opi, it);
     if (!e)
         return MPIX_REDOP_ERR_TYPE;
-    return hip_err(e->contig(in, io, count, params(), launch_cfg(), s));
+    Params prm = params();
+    prm.done = done;
+    prm.done_ctr = ctr;
+    prm.done_seq = seq;
+    int rc = hip_err(e->contig(in, io, count, prm, launch_cfg(), s));
+    if (signalled)
+        *signalled = done && rc == MPIX_REDOP_SUCCESS;
+    return rc;
 }
 
 // Synchronous combine of device-accessible operands on the library stream.
-// (A one-workgroup kernel that writes the completion word itself was
-// measured no faster than the stream write -- 10.9 vs 9.9 us per 1-element
-// call, profiles/r01_latency_small_kernel.json -- the floor is the dispatch.)
+// With the default flag wait, the contiguous launcher signals completion
+// itself (a kernel of at most kSignalMaxGrid workgroups stores the word,
+// saving the end-of-kernel and stream-packet round trip:
+// profiles/r01_sync_latency.txt); other ops and the other wait modes go
+// through wait_stream.
 int run_sync(DevState *d, const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext,
              uint32_t op)
 {
+    launch_cfg();       // environment read before g_sync is consulted
+    if (g_sync.load() == 2 && d->flag) {
+        const uint32_t seq = ++d->seq;
+        bool signalled = false;
+        int rc = enqueue(in, io, count, it, ext, op, d->s[0], (uint32_t *) d->flag, d->flag_ctr,
+                         seq, &signalled);
+        if (signalled) {
+            // an idle stream also means done, so the wait cannot outlive the
+            // kernel even if the word were never stored; the stream is only
+            // queried after 20 ms (a query inside the spin costs latency)
+            const auto t0 = std::chrono::steady_clock::now();
+            for (uint32_t spins = 1; __atomic_load_n(d->flag, __ATOMIC_ACQUIRE) != seq; ++spins)
+                if ((spins & 0xfff) == 0 &&
+                    std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20) &&
+                    hipStreamQuery(d->s[0]) == hipSuccess)
+                    break;
+            return MPIX_REDOP_SUCCESS;
+        }
+        int rc2 = wait_stream(d, d->s[0]);
+        return rc ? rc : rc2;
+    }
     int rc = enqueue(in, io, count, it, ext, op, d->s[0]);
     int rc2 = wait_stream(d, d->s[0]);
     return rc ? rc : rc2;
@@ -771,6 +821,8 @@ static void free_states(DevState *arr)
             (void) hipEventDestroy(d.done);
         if (d.flag)
             (void) hipHostFree((void *) d.flag);
+        if (d.flag_ctr)
+            (void) hipFree(d.flag_ctr);
         if (d.scratch)
             (void) hipFree(d.scratch);
         if (d.iov_done) {

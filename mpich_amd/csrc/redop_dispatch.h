@@ -9,11 +9,21 @@
 namespace mpix {
 
 // Runtime parameters some combiners need (Fortran .TRUE./.FALSE.,
-// src/include/mpii_fortlogical.h:15,28).
+// src/include/mpii_fortlogical.h:15,28), and the completion word of a
+// synchronous call: when `done` is set, the contiguous launcher guarantees
+// that done_seq is stored to it once the combine is complete and visible to
+// the host -- by the kernel itself when it runs as at most kSignalMaxGrid
+// workgroups (the last one to finish, counted on done_ctr, stores it: no
+// end-of-kernel + stream-packet round trip), else by a stream write after it.
 struct Params {
     long long ftrue;
     long long ffalse;
+    uint32_t *done = nullptr;       // pinned, fine-grained host word
+    uint32_t *done_ctr = nullptr;   // device word, 0 between launches
+    uint32_t done_seq = 0;
 };
+
+constexpr unsigned kSignalMaxGrid = 4;
 
 struct LaunchCfg {
     int block;          // threads per block (multiple of 64)

@@ -121,6 +121,23 @@ k_contig(const typename C::unit *__restrict__ in, typename C::unit *__restrict__
         for (uint64_t t = threadIdx.x; t < ntail; t += nt)
             io[tail_start + t] = C::apply(io[tail_start + t], in[tail_start + t], prm);
     }
+    if (prm.done) {     // small synchronous call (launch_contig sets it)
+        __threadfence();            // every wave: its stores complete
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            bool last = true;
+            if (gridDim.x > 1) {    // the last workgroup to arrive signals
+                last = atomicAdd(prm.done_ctr, 1u) == gridDim.x - 1;
+                if (last)
+                    *prm.done_ctr = 0;
+            }
+            if (last) {
+                __threadfence_system();     // L2 written back for the host
+                __hip_atomic_store(prm.done, prm.done_seq, __ATOMIC_RELEASE,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+    }
 }
 
 // Multi-input combine: inout = OP(...OP(OP(inout, in[0]), in[1])..., in[k-1]),
@@ -317,6 +334,7 @@ hipError_t launch_contig(const void *in, void *io, uint64_t count, const Params 
     constexpr uint64_t E = 16 / sizeof(T);
     const T *tin = static_cast<const T *>(in);
     T *tio = static_cast<T *>(io);
+    bool signalled = false;
     uintptr_t ai = reinterpret_cast<uintptr_t>(in), ao = reinterpret_cast<uintptr_t>(io);
     if ((ao % sizeof(T)) == 0 && (ai % sizeof(T)) == 0) {
         uint64_t head = ((16 - (ao & 15)) & 15) / sizeof(T);
@@ -327,19 +345,28 @@ hipError_t launch_contig(const void *in, void *io, uint64_t count, const Params 
         uint32_t ntail = (uint32_t) (count - tail_start);
         const uint64_t tile = (uint64_t) cfg.block * MPIX_REDOP_UNROLL;
         unsigned grid = grid_for(tile, npk, cfg.max_grid);
+        // up to kSignalMaxGrid workgroups (64 KiB at the defaults): the
+        // kernel stores the completion word itself (Params::done)
+        Params p = prm;
+        if (grid > (prm.done_ctr ? kSignalMaxGrid : 1u))
+            p.done = nullptr;
+        signalled = p.done != nullptr;
         if ((ai & 15) == (ao & 15))
             hipLaunchKernelGGL(
                 (k_contig<C, MPIX_REDOP_UNROLL, MPIX_REDOP_NT_LOAD, MPIX_REDOP_NT_STORE, true>),
-                dim3(grid), dim3(cfg.block), 0, s, tin, tio, head, npk, tail_start, ntail, prm);
+                dim3(grid), dim3(cfg.block), 0, s, tin, tio, head, npk, tail_start, ntail, p);
         else
             hipLaunchKernelGGL(
                 (k_contig<C, MPIX_REDOP_UNROLL, MPIX_REDOP_NT_LOAD, MPIX_REDOP_NT_STORE, false>),
-                dim3(grid), dim3(cfg.block), 0, s, tin, tio, head, npk, tail_start, ntail, prm);
+                dim3(grid), dim3(cfg.block), 0, s, tin, tio, head, npk, tail_start, ntail, p);
     } else {
         unsigned grid = grid_for((uint64_t) cfg.block * 4, count, cfg.max_grid);
         hipLaunchKernelGGL((k_elem<C>), dim3(grid), dim3(cfg.block), 0, s, tin, tio, count, prm);
     }
-    return hipGetLastError();
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess && prm.done && !signalled)
+        e = hipStreamWriteValue32(s, (void *) prm.done, prm.done_seq, 0);
+    return e;
 }
 
 template <class C>

@@ -596,6 +596,36 @@ def test_concurrent_callers(R, H, oracle):
     assert np.all(host(y).view(np.float32) == 2)
 
 
+@pytest.mark.parametrize('n', [1, 7, 4096, 4100, 8192, 65536, 65540, 65600, 300000])
+@pytest.mark.parametrize('off', [0, 4, 2])
+def test_sync_result_visible_on_return(R, H, n, off):
+    """The synchronous call returns when the completion word arrives -- for
+    small launches the kernel stores it itself (Params::done, up to 4
+    workgroups, the last one counted on a device word).  The result must be
+    complete then: copied on torch's stream (not ordered after the library's
+    stream) and read from zero-copy pinned memory with no synchronisation at
+    all.  off = 2 bytes: int32 not element-aligned, the element-wise kernel
+    (stream-written word); off = 4: the packet kernel with a head."""
+    rng = np.random.default_rng(n + off)
+    a = rng.integers(-1000, 1000, n, dtype=np.int32)
+    b = rng.integers(-1000, 1000, n, dtype=np.int32)
+    exp = a + b
+    pad = np.zeros(off, np.uint8)
+    da = dev(np.concatenate([pad, a.view(np.uint8)]))
+    db = dev(b)
+    for rep in range(3):
+        if rep:     # inout back to a, then a full device sync
+            da[off:] = dev(a)
+            torch.cuda.synchronize()
+        assert R.MPI_Reduce_local(db, da[off:], n, H.MPI_INT, H.MPI_SUM) == 0
+        snap = da[off:].clone()             # torch stream, no wait on the library's
+        assert np.array_equal(host(snap).view(np.int32), exp)
+    # zero-copy pinned inout, read by the host right after the call
+    hio = torch.from_numpy(a.copy()).pin_memory()
+    assert R.MPI_Reduce_local(db, hio, n, H.MPI_INT, H.MPI_SUM) == 0
+    assert np.array_equal(hio.numpy(), exp)
+
+
 def test_thread_churn(R, H):
     """Worker threads that exit without finalizing hand their streams to a
     pool that later threads take over (redop_capi.cpp DevHolder): 96

@@ -6,6 +6,9 @@
 //            spin on hipEventQuery
 //   extsync  the same, hipEventSynchronize
 //   ev       launch, hipEventRecord, spin on hipEventQuery
+//   kflag    a plain element-wise kernel whose last block (device-scope counter)
+//            stores the sequence number to the pinned word itself, against
+//            the same kernel followed by hipStreamWriteValue32 (kwv)
 // Usage: sync_probe [reps_small=2000] [reps_big=50]
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
@@ -23,6 +26,31 @@ using C = FSum<float>;
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
     fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); exit(1); } } while (0)
+
+__global__ void k_plain(const float *in, float *io, uint64_t n)
+{
+    for (uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t) gridDim.x * blockDim.x)
+        io[i] += in[i];
+}
+
+__global__ void k_flag(const float *in, float *io, uint64_t n, uint32_t *flag, uint32_t *counter,
+                       uint32_t seq)
+{
+    for (uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t) gridDim.x * blockDim.x)
+        io[i] += in[i];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        uint32_t old = atomicAdd(counter, 1u);
+        if (old == gridDim.x - 1) {
+            *counter = 0;
+            __threadfence_system();
+            __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
 
 static double med_us(const std::function<void()> &f, int reps)
 {
@@ -59,6 +87,29 @@ int main(int argc, char **argv)
     uint32_t seq = 0;
     const Params prm{1, 0};
 
+    uint32_t *counter;
+    CK(hipMalloc(&counter, 4));
+    CK(hipMemset(counter, 0, 4));
+    for (uint64_t count : {(uint64_t) 1, (uint64_t) 4096, (uint64_t) 65536, (uint64_t) 1 << 20}) {
+        const unsigned g = (unsigned) std::min<uint64_t>((count + 1023) / 1024, 1024);
+        double t_kwv = med_us([&] {
+            ++seq;
+            hipLaunchKernelGGL(k_plain, dim3(g), dim3(256), 0, s, b, a, count);
+            hipStreamWriteValue32(s, (void *) flag, seq, 0);
+            while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq) {
+            }
+        }, reps_small);
+        double t_kflag = med_us([&] {
+            ++seq;
+            hipLaunchKernelGGL(k_flag, dim3(g), dim3(256), 0, s, b, a, count, (uint32_t *) flag,
+                               counter, seq);
+            while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq) {
+            }
+        }, reps_small);
+        CK(hipStreamSynchronize(s));
+        printf("plain kernel count %llu grid %u: kwv %.1f us  kflag %.1f us\n",
+               (unsigned long long) count, g, t_kwv, t_kflag);
+    }
     for (uint64_t count : {(uint64_t) 4, n}) {
         const uint64_t npk = count / 4;
         const unsigned grid = grid_for(256ull * 4, npk, 0);
