@@ -70,7 +70,7 @@ def float_sends(P, n, seed=0x5EED0100):
 
 # ------------------------------------------------------------------ CPU
 @pytest.mark.parametrize('algo', ['recursive_halving', 'pairwise', 'pairwise_sequential'])
-@pytest.mark.parametrize('P', [1, 2, 3, 4, 5, 7, 8])
+@pytest.mark.parametrize('P', [1, 2, 3, 4, 5, 7, 8, 13, 16])
 def test_rsb_host_matches_oracle_schedule(oracle, P, algo):
     from mpich_amd import ccl
     recvcount = 1001
@@ -108,7 +108,7 @@ def test_rsb_host_redscatblk3(oracle, P, algo):
 
 @pytest.mark.parametrize('algo', ['reduce_scatter_allgather', 'rsag_rd_allgather',
                                   'recursive_doubling', 'ring'])
-@pytest.mark.parametrize('P', [1, 2, 3, 4, 7, 8])
+@pytest.mark.parametrize('P', [1, 2, 3, 4, 7, 8, 12, 16])
 def test_allreduce_host_matches_oracle_and_kats(oracle, P, algo):
     from mpich_amd import ccl
     count = 1037
@@ -244,7 +244,7 @@ def _ragged_counts(P, seed):
 
 
 @pytest.mark.parametrize('algo', ['recursive_halving', 'pairwise', 'pairwise_sequential', 'auto'])
-@pytest.mark.parametrize('P', [1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize('P', [1, 2, 3, 4, 5, 6, 7, 8, 11, 16])
 def test_reduce_scatter_host_matches_oracle(oracle, P, algo):
     """MPI_Reduce_scatter with ragged recvcounts (zeros included) against the
     oracle's simulation of reduce_scatter_intra_{recursive_halving,pairwise}.c,
@@ -614,7 +614,7 @@ def _special_doubles(P, n, seed):
 
 
 @pytest.mark.parametrize('algo', ['binomial', 'reduce_scatter_gather', 'auto'])
-@pytest.mark.parametrize('P', [1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize('P', [1, 2, 3, 4, 5, 6, 7, 8, 11, 16])
 def test_reduce_host_matches_oracle(oracle, P, algo):
     """MPI_Reduce with every root: fp32 SUM and fp64 MAX (NaN / +-0 operand
     order) bit-identical to the oracle's simulation of
@@ -700,7 +700,7 @@ def test_reduce_device_matches_oracle(oracle, P, algo):
 
 # ------------------------------------------------------- MPI_Scan / Exscan
 @pytest.mark.parametrize('exclusive', [False, True])
-@pytest.mark.parametrize('P', [1, 2, 3, 4, 5, 7, 8])
+@pytest.mark.parametrize('P', [1, 2, 3, 4, 5, 7, 8, 11, 16])
 def test_scan_host_matches_oracle(oracle, P, exclusive):
     """recursive-doubling Scan / Exscan, fp64 MAX over NaN / +-0 (operand
     order in the bits) and fp32 SUM, plain and MPI_IN_PLACE, against the
