@@ -498,7 +498,7 @@ def rsb_bench(args, world, rank, dev, out):
     # the same schedules as C++ host code (libmpix_coll.so) on their own RCCL
     # communicator: no Python between the steps
     cc = ccl_comm() if p2p_ok else None
-    for algo in ('recursive_halving', 'pairwise'):
+    for algo in ('recursive_halving', 'pairwise', 'pairwise_pipelined'):
         key = 'c_' + algo
         if cc is None:
             out[key] = dict(skipped='no RCCL communicator (%s)' % _CCL.get('error', 'gloo'))

@@ -108,6 +108,10 @@ int MPIX_Comm_free(MPIX_Comm comm);
 #define MPIX_RSB_RECURSIVE_HALVING  1
 #define MPIX_RSB_PAIRWISE           2   /* the P-1 exchanges in ONE group + one multi-input combine */
 #define MPIX_RSB_PAIRWISE_SEQUENTIAL 3  /* the reference's loop: P-1 sendrecv + combine steps */
+#define MPIX_RSB_PAIRWISE_PIPELINED 4   /* PAIRWISE cut into 2..8 chunks (>= 4 MiB of the
+                                           largest block each; below 8 MiB it is PAIRWISE):
+                                           chunk k's combine, on a second stream, overlaps
+                                           chunk k+1's group; same bits as PAIRWISE */
 size_t MPIX_Reduce_scatter_block_workspace(MPIX_Aint recvcount, MPIX_Datatype datatype,
                                            MPIX_Comm comm, int algorithm);
 int MPIX_Reduce_scatter_block(const void *sendbuf, void *recvbuf, MPIX_Aint recvcount,

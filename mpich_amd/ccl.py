@@ -21,8 +21,10 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libmpix_col
 UNIQUE_ID_BYTES = 128
 
 RSB_AUTO, RSB_RECURSIVE_HALVING, RSB_PAIRWISE, RSB_PAIRWISE_SEQUENTIAL = 0, 1, 2, 3
+RSB_PAIRWISE_PIPELINED = 4
 RSB_ALGORITHMS = {'auto': RSB_AUTO, 'recursive_halving': RSB_RECURSIVE_HALVING,
-                  'pairwise': RSB_PAIRWISE, 'pairwise_sequential': RSB_PAIRWISE_SEQUENTIAL}
+                  'pairwise': RSB_PAIRWISE, 'pairwise_sequential': RSB_PAIRWISE_SEQUENTIAL,
+                  'pairwise_pipelined': RSB_PAIRWISE_PIPELINED}
 AR_AUTO, AR_RECURSIVE_DOUBLING, AR_RSAG, AR_RSAG_RD, AR_RING = 0, 1, 2, 3, 4
 AR_ALGORITHMS = {'auto': AR_AUTO, 'recursive_doubling': AR_RECURSIVE_DOUBLING,
                  'reduce_scatter_allgather': AR_RSAG, 'rsag_rd_allgather': AR_RSAG_RD,

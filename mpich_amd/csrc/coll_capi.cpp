@@ -84,6 +84,8 @@ struct MPIX_Comm_s {
     void *scratch = nullptr;
     size_t scratch_bytes = 0;
     hipEvent_t scratch_ev = nullptr;   // recorded after the last collective that used scratch
+    hipStream_t aux = nullptr;         // combine stream of the pipelined pairwise schedule
+    std::vector<hipEvent_t> pipe_ev;   // its hand-off events (chunk k arrived, combines done)
     std::vector<uint64_t> send_seq, recv_seq;
     bool host() const { return kind == K_LOCAL_HOST || (kind == K_CUSTOM && device < 0); }
 };
@@ -523,6 +525,77 @@ int rs_pairwise(const char *sb, char *rb, const std::vector<size_t> &cnts, MPIX_
     return MPIX_REDOP_SUCCESS;
 }
 
+// rs_pairwise with `concurrent`, cut into chunks: chunk k of every one of the
+// P-1 messages moves in one exchange group on the collective's stream while
+// the combine of chunk k-1 runs on the communicator's second stream, so the
+// multi-input combine hides behind the transfer.  A chunk is the same element
+// range [k*q, ...) of a message on both sides (q from the receiver's count),
+// every element still folds its P-1 inputs in the same order: same bits.
+int rs_pairwise_pipelined(const char *sb, char *rb, const std::vector<size_t> &cnts,
+                          MPIX_Datatype dt, MPIX_Op op, MPIX_Comm c, char *ws, hipStream_t s,
+                          size_t ext)
+{
+    const int rank = c->rank, size = c->size;
+    const size_t blk = cnts[rank] * ext;
+    // the chunk count must be the same on every rank (both ends of a message
+    // cut it alike), so it follows the largest block: chunks of >= 4 MiB of
+    // it, at most kPipeChunks
+    size_t maxblk = 0;
+    for (size_t n : cnts)
+        maxblk = n * ext > maxblk ? n * ext : maxblk;
+    if (c->host() || c->combine || size == 1 || maxblk < (size_t(8) << 20))
+        return rs_pairwise(sb, rb, cnts, dt, op, c, ws, s, ext, true);
+    constexpr size_t kPipeChunks = 8;
+    size_t nch = maxblk >> 22;
+    if (nch > kPipeChunks)
+        nch = kPipeChunks;
+    if (!c->aux)
+        HTRY(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+    while (c->pipe_ev.size() < nch + 1) {
+        hipEvent_t e;
+        HTRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        c->pipe_ev.push_back(e);
+    }
+    std::vector<size_t> disps(size, 0);
+    for (int i = 1; i < size; ++i)
+        disps[i] = disps[i - 1] + cnts[i - 1];
+    const size_t sstride = round256(blk);
+    const bool in_place = sb == rb;
+    char *acc = in_place ? rb + disps[rank] * ext : rb;
+    if (!in_place)
+        TRY(copy(c, rb, sb + disps[rank] * ext, blk, s));
+    auto lo = [nch](size_t n, size_t k) { return n * k / nch; };    // chunk k: [lo(k), lo(k+1))
+    for (size_t k = 0; k < nch; ++k) {
+        std::vector<MPIX_P2p_op> ops;
+        std::vector<const void *> ins;
+        const size_t r0 = lo(cnts[rank], k), r1 = lo(cnts[rank], k + 1);
+        for (int i = 1; i < size; ++i) {
+            const int dst = (rank + i) % size, src = (rank - i + size) % size;
+            const size_t s0 = lo(cnts[dst], k), s1 = lo(cnts[dst], k + 1);
+            ops.push_back(snd(dst, sb + (disps[dst] + s0) * ext, (s1 - s0) * ext));
+            ops.push_back(rcv(src, ws + (i - 1) * sstride + r0 * ext, (r1 - r0) * ext));
+            ins.push_back(ws + (i - 1) * sstride + r0 * ext);
+        }
+        TRY(exchange(c, ops, s));
+        // chunk k (and, for k = 0, the own-block copy) is in: hand it over
+        HTRY(hipEventRecord(c->pipe_ev[k], s));
+        HTRY(hipStreamWaitEvent(c->aux, c->pipe_ev[k], 0));
+        if (r1 > r0)
+            TRY(combine_multi(c, ins, acc + r0 * ext, (MPIX_Aint) (r1 - r0), dt, op, c->aux));
+    }
+    HTRY(hipEventRecord(c->pipe_ev[nch], c->aux));
+    HTRY(hipStreamWaitEvent(s, c->pipe_ev[nch], 0));
+    if (in_place && rank != 0) {
+        if (disps[rank] * ext < blk) {
+            TRY(copy(c, ws, acc, blk, s));
+            TRY(copy(c, rb, ws, blk, s));
+        } else {
+            TRY(copy(c, rb, acc, blk, s));
+        }
+    }
+    return MPIX_REDOP_SUCCESS;
+}
+
 // generic.json:277-291 / :316-341: recursive halving below 512 KiB of total
 // message, pairwise above (commutative ops)
 int rs_choose(int algorithm, size_t total_bytes)
@@ -547,6 +620,7 @@ size_t rs_workspace(size_t total, size_t mine, size_t ext, int size, int algo)
         case MPIX_RSB_RECURSIVE_HALVING:
             return 2 * round256(total * ext);
         case MPIX_RSB_PAIRWISE:
+        case MPIX_RSB_PAIRWISE_PIPELINED:
             return (size - 1) * round256(mine * ext);
         case MPIX_RSB_PAIRWISE_SEQUENTIAL:
             return round256(mine * ext);
@@ -1019,7 +1093,7 @@ int rs_entry(const void *sendbuf, void *recvbuf, const std::vector<size_t> &cnts
     for (size_t n : cnts)
         total += n;
     TRY(check_args(c, recvbuf, (MPIX_Aint) cnts[c->rank], dt, op, &ext));
-    if (algorithm < MPIX_RSB_AUTO || algorithm > MPIX_RSB_PAIRWISE_SEQUENTIAL)
+    if (algorithm < MPIX_RSB_AUTO || algorithm > MPIX_RSB_PAIRWISE_PIPELINED)
         return MPIX_REDOP_ERR_ARG;
     if (!total)
         return MPIX_REDOP_SUCCESS;
@@ -1037,7 +1111,9 @@ int rs_entry(const void *sendbuf, void *recvbuf, const std::vector<size_t> &cnts
     TRY(workspace(c, ws, ws_bytes, rs_workspace(total, cnts[c->rank], ext, c->size, algo), s, &w));
     int rc = algo == MPIX_RSB_RECURSIVE_HALVING
                  ? rs_recursive_halving(sb, rb, cnts, dt, op, c, w, s, ext)
-                 : rs_pairwise(sb, rb, cnts, dt, op, c, w, s, ext, algo == MPIX_RSB_PAIRWISE);
+                 : algo == MPIX_RSB_PAIRWISE_PIPELINED
+                       ? rs_pairwise_pipelined(sb, rb, cnts, dt, op, c, w, s, ext)
+                       : rs_pairwise(sb, rb, cnts, dt, op, c, w, s, ext, algo == MPIX_RSB_PAIRWISE);
     return finish(c, release_scratch(c, w, rc, s), s, blocking);
 }
 
@@ -1266,6 +1342,13 @@ int MPIX_Comm_free(MPIX_Comm comm)
             (void) hipEventDestroy(comm->scratch_ev);
         if (comm->own_stream)
             (void) hipStreamDestroy(comm->own_stream);
+        if (comm->aux) {
+            if (hipStreamSynchronize(comm->aux) != hipSuccess)
+                rc = MPIX_REDOP_ERR_OTHER;
+            (void) hipStreamDestroy(comm->aux);
+        }
+        for (hipEvent_t e : comm->pipe_ev)
+            (void) hipEventDestroy(e);
     } else {
         free(comm->scratch);
     }

@@ -243,7 +243,8 @@ def _ragged_counts(P, seed):
     return c
 
 
-@pytest.mark.parametrize('algo', ['recursive_halving', 'pairwise', 'pairwise_sequential', 'auto'])
+@pytest.mark.parametrize('algo', ['recursive_halving', 'pairwise', 'pairwise_sequential',
+                                  'pairwise_pipelined', 'auto'])
 @pytest.mark.parametrize('P', [1, 2, 3, 4, 5, 6, 7, 8, 11, 16])
 def test_reduce_scatter_host_matches_oracle(oracle, P, algo):
     """MPI_Reduce_scatter with ragged recvcounts (zeros included) against the
@@ -489,6 +490,45 @@ def test_reduce_scatter_device_ragged(oracle, P, algo):
                              'pairwise' if algo.startswith('pairwise') else 'recursive_halving')
     for r in range(P):
         assert drecv[r][:counts[r]].cpu().numpy().tobytes() == exp[r].tobytes(), r
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('P', [2, 3, 4])
+def test_reduce_scatter_device_pipelined(oracle, P):
+    """MPIX_RSB_PAIRWISE_PIPELINED with blocks large enough to be cut into
+    chunks (>= 4 MiB each, up to 8): chunk k's combine runs on the
+    communicator's second stream while chunk k+1 moves.  Bit-identical to the
+    pairwise simulation: equal blocks, ragged blocks (one below the 4 MiB
+    cut, one empty), MPI_IN_PLACE, and two collectives back to back on one
+    communicator (the hand-off events are reused)."""
+    import torch
+    from mpich_amd import ccl
+    big = (3 << 20) + 7                     # 12 MiB fp32 blocks -> 3 chunks
+    for counts in ([big] * P, [big + 5 * r for r in range(P)][:-1] + [1000],
+                   [0] + [(9 << 20) + 3] * (P - 1)):
+        total = sum(counts)
+        sends = float_sends(P, total, 0x5EED0900 + len(counts))
+        exp = oracle.rs_schedule([s.view(np.uint8) for s in sends], counts, MPI_FLOAT, MPI_SUM,
+                                 'pairwise')
+        comms = _dev_comms(P)
+        for in_place in (False, True):
+            dsend = [torch.from_numpy(s).cuda() for s in sends]
+            bufs = [d.clone() if in_place else torch.zeros(max(1, counts[r]), device='cuda')
+                    for r, d in enumerate(dsend)]
+            torch.cuda.synchronize()
+            for rep in range(2):
+                if rep and in_place:
+                    for b, d in zip(bufs, dsend):
+                        b.copy_(d)
+                    torch.cuda.synchronize()
+                rcs = run_ranks(comms, lambda r, c: ccl.reduce_scatter(
+                    None if in_place else dsend[r], bufs[r], counts, MPI_FLOAT, MPI_SUM, c,
+                    'pairwise_pipelined'))
+                assert rcs == [0] * P
+                for r in range(P):
+                    got = bufs[r][:counts[r]].cpu().numpy()
+                    assert got.tobytes() == exp[r].tobytes(), (counts[r], in_place, rep, r)
+        free_all(comms)
 
 
 @pytest.mark.gpu

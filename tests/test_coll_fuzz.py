@@ -53,7 +53,8 @@ def _inputs(P, n, case, seed):
 
 @SETTINGS
 @given(P=st.integers(1, 12), case=st.sampled_from(CASES),
-       algo=st.sampled_from(['recursive_halving', 'pairwise', 'pairwise_sequential']),
+       algo=st.sampled_from(['recursive_halving', 'pairwise', 'pairwise_sequential',
+                             'pairwise_pipelined']),
        in_place=st.booleans(), data=st.data(), seed=st.integers(0, 2**31))
 def test_reduce_scatter_random(oracle, P, case, algo, in_place, data, seed):
     from mpich_amd import ccl
@@ -154,7 +155,8 @@ def _dev(a):
 @pytest.mark.gpu
 @GPU_SETTINGS
 @given(P=st.integers(2, 8), case=st.sampled_from(CASES),
-       algo=st.sampled_from(['recursive_halving', 'pairwise', 'pairwise_sequential']),
+       algo=st.sampled_from(['recursive_halving', 'pairwise', 'pairwise_sequential',
+                             'pairwise_pipelined']),
        in_place=st.booleans(), data=st.data(), seed=st.integers(0, 2**31))
 def test_reduce_scatter_random_device(oracle, P, case, algo, in_place, data, seed):
     import torch
