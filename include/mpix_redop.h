@@ -191,7 +191,10 @@ int MPIX_Reduce_local_vector(const void *inbuf, void *inoutbuf, MPIX_Aint count,
  * with the next seg_counts[s] elements of inbuf.  Offsets may be negative
  * (lb < 0) and need only the 4-byte alignment of the element loads (2 for
  * 2-byte types); runs must not overlap (MPI accumulate targets).  The
- * tables are host arrays, read before the call returns.  Device buffers. */
+ * tables are host arrays, read before the call returns (the run table is
+ * uploaded through pinned memory, asynchronously on `stream`; a call waits
+ * only for the previous iov call's kernels, whose table it replaces).
+ * Device buffers. */
 int MPIX_Reduce_local_iov_async(const void *inbuf, void *inoutbuf, MPIX_Aint nseg,
                                 const MPIX_Aint *seg_offsets, const MPIX_Aint *seg_counts,
                                 MPIX_Datatype basic_type, MPIX_Op op, void *stream);

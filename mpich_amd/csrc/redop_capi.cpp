@@ -291,7 +291,8 @@ struct DevState {
     void *scratch = nullptr;    // 2 slots x (in chunk + inout chunk)
     size_t scratch_bytes = 0;
     int64_t *iov_tab = nullptr; // device copy of the last iov run table
-    size_t iov_cap = 0;         // its capacity in int64 entries
+    int64_t *iov_host = nullptr;    // its pinned host staging copy
+    size_t iov_cap = 0;         // capacity of both in int64 entries
     hipEvent_t iov_done = nullptr;  // recorded after the launches that read iov_tab
     char *bounce = nullptr;     // pinned host: in half + inout half, bounce_half bytes each
     char *bounce_dev = nullptr; // its device mapping
@@ -771,19 +772,24 @@ int enqueue_runs(const void *inbuf, void *inoutbuf, const std::vector<Run> &runs
     if (d->iov_cap < need) {
         if (d->iov_tab)
             (void) hipFree(d->iov_tab);
+        if (d->iov_host)
+            (void) hipHostFree(d->iov_host);
         d->iov_tab = nullptr;
+        d->iov_host = nullptr;
         d->iov_cap = 0;
         if (hipMalloc((void **) &d->iov_tab, need * sizeof(int64_t)) != hipSuccess)
             return MPIX_REDOP_ERR_OTHER;
+        if (hipHostMalloc((void **) &d->iov_host, need * sizeof(int64_t), hipHostMallocDefault) !=
+            hipSuccess)
+            return MPIX_REDOP_ERR_OTHER;
         d->iov_cap = need;
     }
-    // pageable source: hipMemcpyAsync stages it, and the sync makes the
-    // host vector free to go; stream order keeps the new table behind
-    // earlier kernels that still read the old one
-    rc = hip_err(hipMemcpyAsync(d->iov_tab, tab.data(), need * sizeof(int64_t),
+    // the table goes through a pinned copy, so the upload is a true async
+    // copy on s (no wait on the caller's stream); both copies are free for
+    // reuse once iov_done, recorded after the launches below, has fired
+    memcpy(d->iov_host, tab.data(), need * sizeof(int64_t));
+    rc = hip_err(hipMemcpyAsync(d->iov_tab, d->iov_host, need * sizeof(int64_t),
                                 hipMemcpyHostToDevice, s));
-    if (rc == MPIX_REDOP_SUCCESS)
-        rc = hip_err(hipStreamSynchronize(s));
     for (size_t g = 0; g < groups.size() && rc == MPIX_REDOP_SUCCESS; ++g) {
         const int64_t n = (int64_t) groups[g].size();
         const int64_t *t = d->iov_tab + base[g];
@@ -831,6 +837,8 @@ static void free_states(DevState *arr)
         }
         if (d.iov_tab)
             (void) hipFree(d.iov_tab);
+        if (d.iov_host)
+            (void) hipHostFree(d.iov_host);
         if (d.bounce)
             (void) hipHostFree(d.bounce);
         d = DevState();
