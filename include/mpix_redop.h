@@ -192,8 +192,9 @@ int MPIX_Reduce_local_vector(const void *inbuf, void *inoutbuf, MPIX_Aint count,
  * (lb < 0) and need only the 4-byte alignment of the element loads (2 for
  * 2-byte types); runs must not overlap (MPI accumulate targets).  The
  * tables are host arrays, read before the call returns (the run table is
- * uploaded through pinned memory, asynchronously on `stream`; a call waits
- * only for the previous iov call's kernels, whose table it replaces).
+ * uploaded through pinned memory, asynchronously on `stream`; two table
+ * slots are used in turn, so a call waits only for the kernels of the iov
+ * call before the previous one, whose slot it takes over).
  * Device buffers. */
 int MPIX_Reduce_local_iov_async(const void *inbuf, void *inoutbuf, MPIX_Aint nseg,
                                 const MPIX_Aint *seg_offsets, const MPIX_Aint *seg_counts,

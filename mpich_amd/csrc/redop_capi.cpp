@@ -290,10 +290,15 @@ struct DevState {
     uint32_t seq = 0;
     void *scratch = nullptr;    // 2 slots x (in chunk + inout chunk)
     size_t scratch_bytes = 0;
-    int64_t *iov_tab = nullptr; // device copy of the last iov run table
-    int64_t *iov_host = nullptr;    // its pinned host staging copy
-    size_t iov_cap = 0;         // capacity of both in int64 entries
-    hipEvent_t iov_done = nullptr;  // recorded after the launches that read iov_tab
+    // iov run tables, two slots used in turn, so back-to-back iov calls only
+    // wait for the call before the previous one
+    struct IovSlot {
+        int64_t *tab = nullptr;     // device copy of the run table
+        int64_t *host = nullptr;    // its pinned host staging copy
+        size_t cap = 0;             // capacity of both in int64 entries
+        hipEvent_t done = nullptr;  // recorded after the launches that read it
+    } iov[2];
+    uint32_t iov_next = 0;
     char *bounce = nullptr;     // pinned host: in half + inout half, bounce_half bytes each
     char *bounce_dev = nullptr; // its device mapping
     size_t bounce_half = 0;
@@ -762,41 +767,41 @@ int enqueue_runs(const void *inbuf, void *inoutbuf, const std::vector<Run> &runs
     DevState *d = dev_state(dev);
     if (!d)
         return MPIX_REDOP_ERR_OTHER;
-    if (!d->iov_done && hipEventCreateWithFlags(&d->iov_done, hipEventDisableTiming) != hipSuccess)
+    DevState::IovSlot &sl = d->iov[d->iov_next++ & 1];
+    if (!sl.done && hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess)
         return MPIX_REDOP_ERR_OTHER;
-    // the previous table may still be read by kernels queued on any stream
-    // (this thread may have used another one last time): wait for them
-    rc = hip_err(hipEventSynchronize(d->iov_done));
+    // the slot's previous table may still be read by kernels queued on any
+    // stream (this thread may have used another one then): wait for them
+    rc = hip_err(hipEventSynchronize(sl.done));
     if (rc != MPIX_REDOP_SUCCESS)
         return rc;
-    if (d->iov_cap < need) {
-        if (d->iov_tab)
-            (void) hipFree(d->iov_tab);
-        if (d->iov_host)
-            (void) hipHostFree(d->iov_host);
-        d->iov_tab = nullptr;
-        d->iov_host = nullptr;
-        d->iov_cap = 0;
-        if (hipMalloc((void **) &d->iov_tab, need * sizeof(int64_t)) != hipSuccess)
+    if (sl.cap < need) {
+        if (sl.tab)
+            (void) hipFree(sl.tab);
+        if (sl.host)
+            (void) hipHostFree(sl.host);
+        sl.tab = nullptr;
+        sl.host = nullptr;
+        sl.cap = 0;
+        if (hipMalloc((void **) &sl.tab, need * sizeof(int64_t)) != hipSuccess)
             return MPIX_REDOP_ERR_OTHER;
-        if (hipHostMalloc((void **) &d->iov_host, need * sizeof(int64_t), hipHostMallocDefault) !=
+        if (hipHostMalloc((void **) &sl.host, need * sizeof(int64_t), hipHostMallocDefault) !=
             hipSuccess)
             return MPIX_REDOP_ERR_OTHER;
-        d->iov_cap = need;
+        sl.cap = need;
     }
-    // the table goes through a pinned copy, so the upload is a true async
+    // the table goes through the pinned copy, so the upload is a true async
     // copy on s (no wait on the caller's stream); both copies are free for
-    // reuse once iov_done, recorded after the launches below, has fired
-    memcpy(d->iov_host, tab.data(), need * sizeof(int64_t));
-    rc = hip_err(hipMemcpyAsync(d->iov_tab, d->iov_host, need * sizeof(int64_t),
-                                hipMemcpyHostToDevice, s));
+    // reuse once sl.done, recorded after the launches below, has fired
+    memcpy(sl.host, tab.data(), need * sizeof(int64_t));
+    rc = hip_err(hipMemcpyAsync(sl.tab, sl.host, need * sizeof(int64_t), hipMemcpyHostToDevice, s));
     for (size_t g = 0; g < groups.size() && rc == MPIX_REDOP_SUCCESS; ++g) {
         const int64_t n = (int64_t) groups[g].size();
-        const int64_t *t = d->iov_tab + base[g];
+        const int64_t *t = sl.tab + base[g];
         rc = hip_err(en->iov(inbuf, (char *) inoutbuf + resid[g], t, t + n, t + 2 * n + 1, n,
                              (uint64_t) gtotal[g], params(), launch_cfg(), s));
     }
-    int rc2 = hip_err(hipEventRecord(d->iov_done, s));
+    int rc2 = hip_err(hipEventRecord(sl.done, s));
     return rc ? rc : rc2;
 }
 
@@ -831,14 +836,16 @@ static void free_states(DevState *arr)
             (void) hipFree(d.flag_ctr);
         if (d.scratch)
             (void) hipFree(d.scratch);
-        if (d.iov_done) {
-            (void) hipEventSynchronize(d.iov_done);
-            (void) hipEventDestroy(d.iov_done);
+        for (DevState::IovSlot &sl : d.iov) {
+            if (sl.done) {
+                (void) hipEventSynchronize(sl.done);
+                (void) hipEventDestroy(sl.done);
+            }
+            if (sl.tab)
+                (void) hipFree(sl.tab);
+            if (sl.host)
+                (void) hipHostFree(sl.host);
         }
-        if (d.iov_tab)
-            (void) hipFree(d.iov_tab);
-        if (d.iov_host)
-            (void) hipHostFree(d.iov_host);
         if (d.bounce)
             (void) hipHostFree(d.bounce);
         d = DevState();

@@ -276,13 +276,13 @@ def test_replace_keeps_padding_on_gpu(R, oracle, dt):
 
 @pytest.mark.gpu
 def test_iov_tables_on_two_streams(R, oracle):
-    """back-to-back iov calls on two different streams from one thread: the
-    second call's run table must not overwrite the first one's while its
-    kernel still reads it"""
+    """back-to-back iov calls on different streams from one thread: a call's
+    run table must not overwrite one a queued kernel still reads (two table
+    slots used in turn: the third call reuses the first call's slot)"""
     import torch
     rng = np.random.default_rng(4242)
     jobs = []
-    for j in range(2):
+    for j in range(3):
         nseg = 400000 - 150000 * j
         cnts = rng.integers(1, 5, nseg)
         offs, pos = [], 0
@@ -293,7 +293,7 @@ def test_iov_tables_on_two_streams(R, oracle):
         src = rng.uniform(-1, 1, int(cnts.sum()))
         dst = rng.uniform(-1, 1, pos + 1)
         jobs.append((offs, [int(c) for c in cnts], src, dst))
-    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()]
     devs = [(_dev(dst), _dev(src)) for _, _, src, dst in jobs]
     for (offs, cnts, _, _), (dd, ds), st in zip(jobs, devs, streams):
         assert R.reduce_local_iov_async(ds, dd, offs, cnts, MPI_DOUBLE, SUM, st) == 0
