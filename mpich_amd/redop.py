@@ -77,15 +77,48 @@ def lib():
 
 
 def _addr(buf):
+    """base address of a buffer: a raw int pointer is passed through; a
+    tensor or array must be contiguous (an MPI buffer is one span)"""
     if buf is None:
         return None
     if isinstance(buf, int):
         return buf
     if isinstance(buf, torch.Tensor):
+        if not buf.is_contiguous():
+            raise ValueError('non-contiguous tensor: an MPI buffer is one contiguous span')
         return buf.data_ptr()
     if hasattr(buf, 'ctypes'):          # numpy
+        if not buf.flags['C_CONTIGUOUS']:
+            raise ValueError('non-contiguous array: an MPI buffer is one contiguous span')
         return buf.ctypes.data
     raise TypeError('unsupported buffer type %r' % type(buf))
+
+
+def _nbytes(buf):
+    if isinstance(buf, torch.Tensor):
+        return buf.numel() * buf.element_size()
+    if hasattr(buf, 'nbytes'):
+        return buf.nbytes
+    return None                         # raw pointer: the caller vouches for the span
+
+
+def _span_check(count, datatype, op, *bufs):
+    """count elements of `datatype` must fit every tensor / array operand: a
+    short buffer would be an out-of-bounds access on the device, not an MPI
+    error the C call could report.  Calls the C side rejects anyway (bad
+    count, type or op) go through, so they return their MPI error class."""
+    if not isinstance(count, int) or count <= 0:
+        return
+    if not lib().MPIX_Redop_is_supported(H.as_c_int(op), count, H.as_c_int(datatype)):
+        return
+    ext = lib().MPIX_Datatype_extent(H.as_c_int(datatype))
+    if ext <= 0:
+        return                          # the C call reports MPI_ERR_TYPE
+    for b in bufs:
+        nb = _nbytes(b)
+        if nb is not None and nb < count * ext:
+            raise ValueError('buffer of %d bytes is too small for %d elements of extent %d'
+                             % (nb, count, ext))
 
 
 def _stream_ptr(stream):
@@ -101,12 +134,14 @@ def MPI_Reduce_local(inbuf, inoutbuf, count, datatype, op):
 
     Device buffers must be ready (the caller orders its own streams, as an
     MPI caller does); host buffers are staged through the device."""
+    _span_check(count, datatype, op, inbuf, inoutbuf)
     return lib().MPIX_Reduce_local(_addr(inbuf), _addr(inoutbuf), count, H.as_c_int(datatype),
                                    H.as_c_int(op))
 
 
 def reduce_local_async(inbuf, inoutbuf, count, datatype, op, stream=None):
     """Enqueue the combine on `stream` (default: torch's current stream)."""
+    _span_check(count, datatype, op, inbuf, inoutbuf)
     return lib().MPIX_Reduce_local_async(_addr(inbuf), _addr(inoutbuf), count,
                                          H.as_c_int(datatype), H.as_c_int(op),
                                          _stream_ptr(stream))
@@ -148,6 +183,7 @@ def reduce_local_iovec_async(inbuf, inoutbuf, iov_offsets, iov_lens, basic_type,
 
 def reduce_local_multi_async(inbufs, inoutbuf, count, datatype, op, stream=None):
     """inoutbuf = (...((inoutbuf OP in[0]) OP in[1])...) OP in[k-1], one pass."""
+    _span_check(count, datatype, op, inoutbuf, *inbufs)
     arr = (ctypes.c_void_p * len(inbufs))(*[_addr(b) for b in inbufs])
     return lib().MPIX_Reduce_local_multi_async(arr, len(inbufs), _addr(inoutbuf), count,
                                                H.as_c_int(datatype), H.as_c_int(op),

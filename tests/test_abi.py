@@ -154,3 +154,22 @@ def test_launch_knobs(R):
     assert R.set_launch(100, 0) == 12
     assert R.set_launch(cfg['block'], cfg['max_grid']) == 0
     assert 'gfx950' in R.build_info()
+
+
+def test_python_mirror_rejects_bad_spans():
+    """the Python mirror checks what the raw C-ABI cannot: a tensor / array
+    operand must be one contiguous span holding count elements (a short or
+    strided buffer would be an out-of-bounds device access, not an MPI error)"""
+    import numpy as np
+    from mpich_amd import handles as H
+    from mpich_amd import redop
+    a = np.zeros(64, np.float32)
+    with pytest.raises(ValueError, match='non-contiguous'):
+        redop.MPI_Reduce_local(a[::2], a[:32].copy(), 32, H.MPI_FLOAT, H.MPI_SUM)
+    with pytest.raises(ValueError, match='too small'):
+        redop.MPI_Reduce_local(a, np.zeros(16, np.float32), 32, H.MPI_FLOAT, H.MPI_SUM)
+    with pytest.raises(ValueError, match='too small'):      # pairs: extent, not value size
+        redop.reduce_local_async(np.zeros(4, np.int32), np.zeros(4, np.int32), 3, H.MPI_2INT,
+                                 H.MPI_MAXLOC, stream=0)
+    with pytest.raises(ValueError, match='too small'):
+        redop.reduce_local_multi_async([a, a[:8].copy()], a, 32, H.MPI_FLOAT, H.MPI_SUM, stream=0)
