@@ -88,6 +88,22 @@ def _addr(buf):
     return redop._addr(buf)
 
 
+def _ws(workspace):
+    """(address, bytes) of an optional workspace tensor / array"""
+    if workspace is None:
+        return None, 0
+    nb = redop._nbytes(workspace)
+    return _addr(workspace), (nb if nb is not None else 0)
+
+
+def _fits(datatype, op, *pairs):
+    """every (buffer, element count) pair: the tensor / array holds that many
+    elements (redop._span_check; None buffers and raw pointers pass)"""
+    for buf, n in pairs:
+        if buf is not None:
+            redop._span_check(int(n), datatype, op, buf)
+
+
 class Comm:
     """One rank's handle of a libmpix_coll communicator."""
 
@@ -155,8 +171,9 @@ def reduce_scatter_block(sendbuf, recvbuf, recvcount, datatype, op, comm, algori
                          workspace=None, stream=None, blocking=True):
     """MPI_Reduce_scatter_block; returns the MPI error class."""
     a = RSB_ALGORITHMS[algorithm] if isinstance(algorithm, str) else algorithm
-    ws, wsb = (None, 0) if workspace is None else (_addr(workspace), workspace.numel() *
-                                                    workspace.element_size())
+    ws, wsb = _ws(workspace)
+    total = recvcount * comm.size
+    _fits(datatype, op, (sendbuf, total), (recvbuf, total if sendbuf is None else recvcount))
     if blocking:
         return lib().MPIX_Reduce_scatter_block(_addr(sendbuf), _addr(recvbuf), recvcount,
                                                H.as_c_int(datatype), H.as_c_int(op), comm.h, a,
@@ -171,9 +188,12 @@ def reduce_scatter(sendbuf, recvbuf, recvcounts, datatype, op, comm, algorithm='
     """MPI_Reduce_scatter with per-rank recvcounts (sendbuf None =
     MPI_IN_PLACE); returns the MPI error class."""
     a = RSB_ALGORITHMS[algorithm] if isinstance(algorithm, str) else algorithm
-    ws, wsb = (None, 0) if workspace is None else (_addr(workspace), workspace.numel() *
-                                                    workspace.element_size())
+    ws, wsb = _ws(workspace)
     cnts = (ctypes.c_ssize_t * len(recvcounts))(*recvcounts)
+    if len(recvcounts) == comm.size and all(c >= 0 for c in recvcounts):
+        total = sum(recvcounts)
+        _fits(datatype, op, (sendbuf, total),
+              (recvbuf, total if sendbuf is None else recvcounts[comm.rank]))
     if blocking:
         return lib().MPIX_Reduce_scatter(_addr(sendbuf), _addr(recvbuf), cnts,
                                          H.as_c_int(datatype), H.as_c_int(op), comm.h, a, ws, wsb)
@@ -190,8 +210,8 @@ def reduce(sendbuf, recvbuf, count, datatype, op, root, comm, algorithm='auto', 
     """MPI_Reduce to `root` (the root's sendbuf None = MPI_IN_PLACE; recvbuf
     only significant at the root); returns the MPI error class."""
     a = REDUCE_ALGORITHMS[algorithm] if isinstance(algorithm, str) else algorithm
-    ws, wsb = (None, 0) if workspace is None else (_addr(workspace), workspace.numel() *
-                                                    workspace.element_size())
+    ws, wsb = _ws(workspace)
+    _fits(datatype, op, (sendbuf, count), (recvbuf if comm.rank == root else None, count))
     if blocking:
         return lib().MPIX_Reduce(_addr(sendbuf), _addr(recvbuf), count, H.as_c_int(datatype),
                                  H.as_c_int(op), root, comm.h, a, ws, wsb)
@@ -204,9 +224,9 @@ def scan(sendbuf, recvbuf, count, datatype, op, comm, exclusive=False, workspace
          stream=None, blocking=True):
     """MPI_Scan, or MPI_Exscan with exclusive=True (sendbuf None =
     MPI_IN_PLACE); returns the MPI error class."""
-    ws, wsb = (None, 0) if workspace is None else (_addr(workspace), workspace.numel() *
-                                                    workspace.element_size())
+    ws, wsb = _ws(workspace)
     name = 'MPIX_Exscan' if exclusive else 'MPIX_Scan'
+    _fits(datatype, op, (sendbuf, count), (recvbuf, count))
     if blocking:
         return getattr(lib(), name)(_addr(sendbuf), _addr(recvbuf), count, H.as_c_int(datatype),
                                     H.as_c_int(op), comm.h, ws, wsb)
@@ -225,8 +245,8 @@ def allreduce(sendbuf, recvbuf, count, datatype, op, comm, algorithm='auto', wor
               stream=None, blocking=True):
     """MPI_Allreduce (sendbuf None = MPI_IN_PLACE); returns the MPI error class."""
     a = AR_ALGORITHMS[algorithm] if isinstance(algorithm, str) else algorithm
-    ws, wsb = (None, 0) if workspace is None else (_addr(workspace), workspace.numel() *
-                                                    workspace.element_size())
+    ws, wsb = _ws(workspace)
+    _fits(datatype, op, (sendbuf, count), (recvbuf, count))
     if blocking:
         return lib().MPIX_Allreduce(_addr(sendbuf), _addr(recvbuf), count, H.as_c_int(datatype),
                                     H.as_c_int(op), comm.h, a, ws, wsb)

@@ -173,3 +173,30 @@ def test_python_mirror_rejects_bad_spans():
                                  H.MPI_MAXLOC, stream=0)
     with pytest.raises(ValueError, match='too small'):
         redop.reduce_local_multi_async([a, a[:8].copy()], a, 32, H.MPI_FLOAT, H.MPI_SUM, stream=0)
+
+
+def test_python_collective_wrappers_reject_short_buffers(oracle):
+    """mpich_amd.ccl checks tensor / array spans the same way before the C
+    call: sendbuf P*recvcount, recvbuf recvcount (all of it for MPI_IN_PLACE)"""
+    import numpy as np
+    from mpich_amd import ccl
+    from mpich_amd import handles as H
+    comms = ccl.comm_create_local(2)
+    try:
+        for c in comms:
+            c.set_combine(oracle.combine_fn_address())
+        c0 = comms[0]
+        with pytest.raises(ValueError, match='too small'):
+            ccl.reduce_scatter_block(np.zeros(10, np.float32), np.zeros(8, np.float32), 8,
+                                     H.MPI_FLOAT, H.MPI_SUM, c0)
+        with pytest.raises(ValueError, match='too small'):
+            ccl.reduce_scatter_block(None, np.zeros(8, np.float32), 8, H.MPI_FLOAT, H.MPI_SUM, c0)
+        with pytest.raises(ValueError, match='too small'):
+            ccl.allreduce(np.zeros(8, np.float32), np.zeros(4, np.float32), 8, H.MPI_FLOAT,
+                          H.MPI_SUM, c0)
+        with pytest.raises(ValueError, match='non-contiguous'):
+            ccl.scan(np.zeros(16, np.float32)[::2], np.zeros(8, np.float32), 8, H.MPI_FLOAT,
+                     H.MPI_SUM, c0)
+    finally:
+        for c in comms:
+            assert c.free() == 0
