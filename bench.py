@@ -69,7 +69,31 @@ def bench_lib():
     L = ctypes.CDLL(path)
     L.mpix_bench_triad.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                    ctypes.c_float, ctypes.c_uint64, ctypes.c_void_p]
+    L.mpix_bench_call_latency.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          ctypes.POINTER(ctypes.c_double),
+                                          ctypes.POINTER(ctypes.c_double)]
     return L
+
+
+def sync_call_latency(B, dev, counts=(1, 4096, 1 << 20), reps=2000):
+    """per-call host time of the synchronous MPIX_Reduce_local (fp32 SUM,
+    device-resident), timed in C by libmpix_bench (no binding overhead);
+    checked: after the warm-up + reps calls on zeros with in = 1, inout = reps+1"""
+    fn = ctypes.cast(redop.lib().MPIX_Reduce_local, ctypes.c_void_p).value
+    out = []
+    for n in counts:
+        xin = torch.ones(n, dtype=torch.float32, device=dev)
+        xio = torch.zeros(n, dtype=torch.float32, device=dev)
+        torch.cuda.synchronize()
+        med, p90 = ctypes.c_double(), ctypes.c_double()
+        rc = B.mpix_bench_call_latency(fn, xin.data_ptr(), xio.data_ptr(), n,
+                                       H.as_c_int(H.MPI_FLOAT), H.as_c_int(H.MPI_SUM), reps,
+                                       ctypes.byref(med), ctypes.byref(p90))
+        ok = rc == 0 and bool(torch.all(xio == reps + 1))
+        out.append(dict(count=n, median_us=round(med.value, 2), p90_us=round(p90.value, 2),
+                        checked=ok))
+    return out
 
 
 def event_time_per_launch(launch, reps, stream, rounds=3):
@@ -269,6 +293,11 @@ def main():
             result['roofline']['triad_measured_GBs'] = round(triad, 1)
             result['roofline']['frac_of_triad'] = round(achieved / triad, 4)
             del a3
+            # small-message regime of the same entry point: per-call latency
+            try:
+                result['sync_call_latency'] = sync_call_latency(B, dev)
+            except Exception as e:      # secondary figure: never lose the headline line
+                result['sync_call_latency'] = dict(error='%s: %s' % (type(e).__name__, e))
         except OSError as e:
             result['roofline']['triad_measured_GBs'] = None
             result['roofline']['triad_error'] = str(e)

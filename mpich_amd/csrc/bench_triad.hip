@@ -6,6 +6,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+#include <chrono>
+#include <vector>
+
 typedef float f4 __attribute__((ext_vector_type(4)));
 
 template <int U>
@@ -40,4 +44,33 @@ extern "C" int mpix_bench_triad(float *a, const float *b, const float *c, float 
     hipLaunchKernelGGL((k_triad<U>), dim3((unsigned) grid), dim3(T), 0, (hipStream_t) stream,
                        (f4 *) a, (const f4 *) b, (const f4 *) c, q, n4);
     return hipGetLastError() == hipSuccess ? 0 : 15;
+}
+
+// Per-call host time of a synchronous reduce entry point (passed as a
+// function pointer, e.g. MPIX_Reduce_local), median over `reps` calls after
+// one warm-up, timed in C so the figure carries no binding overhead.
+typedef int (*sync_reduce_fn)(const void *, void *, int64_t, int, int);
+
+extern "C" int mpix_bench_call_latency(void *fn, const void *in, void *io, int64_t count, int dt,
+                                       int op, int reps, double *median_us, double *p90_us)
+{
+    if (!fn || reps < 1 || !median_us || !p90_us)
+        return 12;
+    sync_reduce_fn f = (sync_reduce_fn) fn;
+    int rc = f(in, io, count, dt, op);
+    if (rc)
+        return rc;
+    std::vector<double> t(reps);
+    for (int i = 0; i < reps; ++i) {
+        auto a = std::chrono::steady_clock::now();
+        rc = f(in, io, count, dt, op);
+        auto b = std::chrono::steady_clock::now();
+        if (rc)
+            return rc;
+        t[i] = std::chrono::duration<double, std::micro>(b - a).count();
+    }
+    std::sort(t.begin(), t.end());
+    *median_us = t[reps / 2];
+    *p90_us = t[(reps * 9) / 10];
+    return 0;
 }
