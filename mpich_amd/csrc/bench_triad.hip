@@ -74,3 +74,38 @@ extern "C" int mpix_bench_call_latency(void *fn, const void *in, void *io, int64
     *p90_us = t[(reps * 9) / 10];
     return 0;
 }
+
+// The chunked regime of a pipelined collective (one combine per arriving
+// chunk), issued from C: `count` elements of `elem_size` bytes cut into
+// chunks of `chunk` elements, each enqueued through the stream-ordered entry
+// point (e.g. MPIX_Reduce_local_async) back to back on `stream`, timed from
+// the first issue to the stream draining.  *issue_s is the host time of the
+// issue loop alone (per-call launch cost), *total_s the whole interval.
+typedef int (*async_reduce_fn)(const void *, void *, int64_t, int, int, void *);
+
+extern "C" int mpix_bench_chunked_async(void *fn, const void *in, void *io, int64_t count,
+                                        int64_t chunk, int elem_size, int dt, int op, void *stream,
+                                        double *issue_s, double *total_s)
+{
+    if (!fn || chunk < 1 || count < chunk || elem_size < 1 || !issue_s || !total_s)
+        return 12;
+    async_reduce_fn f = (async_reduce_fn) fn;
+    hipStream_t s = (hipStream_t) stream;
+    if (hipStreamSynchronize(s) != hipSuccess)
+        return 15;
+    const int64_t nch = count / chunk;
+    auto a = std::chrono::steady_clock::now();
+    for (int64_t k = 0; k < nch; ++k) {
+        const int64_t off = k * chunk * elem_size;
+        int rc = f((const char *) in + off, (char *) io + off, chunk, dt, op, stream);
+        if (rc)
+            return rc;
+    }
+    auto b = std::chrono::steady_clock::now();
+    if (hipStreamSynchronize(s) != hipSuccess)
+        return 15;
+    auto c = std::chrono::steady_clock::now();
+    *issue_s = std::chrono::duration<double>(b - a).count();
+    *total_s = std::chrono::duration<double>(c - a).count();
+    return 0;
+}
