@@ -755,3 +755,37 @@ def test_equal_op(R, H, oracle, nbytes):
             assert oracle.reduce_local(b.copy(), exp, nbytes, H.MPI_BYTE, 0x5800000f) == 0
             assert np.array_equal(host(da), exp)
     assert R.MPI_Reduce_local(dev(base), dev(base), nbytes, H.MPI_INT, 0x5800000f) != 0
+
+
+@pytest.mark.parametrize('dtname,opname,npdt', [('MPI_DOUBLE', 'MPI_SUM', np.float64),
+                                               ('MPI_FLOAT', 'MPI_PROD', np.float32),
+                                               ('MPI_INT', 'MPI_BXOR', np.int32)])
+def test_chunked_pipeline_ragged(R, H, oracle, dtname, opname, npdt):
+    """the per-chunk pattern of a pipelined collective: three incoming
+    vectors, each combined into the result as ragged chunks (odd offsets,
+    one-element and empty-free pieces) by back-to-back async calls on one
+    stream; bit-equal to the oracle applying the three inputs in order"""
+    rng = np.random.default_rng(0x5EED0C)
+    n = 1_000_003
+    dt, op = getattr(H, dtname), getattr(H, opname)
+    if npdt is np.int32:
+        ins = [rng.integers(-2**31, 2**31, n, dtype=np.int64).astype(np.int32) for _ in range(3)]
+        acc = rng.integers(-2**31, 2**31, n, dtype=np.int64).astype(np.int32)
+    else:
+        ins = [rng.uniform(0.5, 1.5, n).astype(npdt) for _ in range(3)]
+        acc = rng.uniform(-1, 1, n).astype(npdt)
+    cuts = np.unique(np.concatenate([[0, 1, 2, n - 1, n], rng.integers(3, n - 1, 37)]))
+    d_acc = torch.from_numpy(acc.copy()).cuda()
+    d_ins = [torch.from_numpy(x).cuda() for x in ins]
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for x in d_ins:
+            for lo, hi in zip(cuts[:-1], cuts[1:]):
+                assert R.reduce_local_async(x[lo:hi], d_acc[lo:hi], int(hi - lo), dt, op, s) == 0
+    s.synchronize()
+    exp = acc.copy()
+    for x in ins:
+        oracle.reduce_local(x, exp, n, dt, op)
+    got = d_acc.cpu().numpy()
+    assert np.array_equal(got.view(np.uint8), exp.view(np.uint8))
