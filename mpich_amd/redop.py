@@ -102,6 +102,25 @@ def _nbytes(buf):
     return None                         # raw pointer: the caller vouches for the span
 
 
+_extent_cache = {}
+
+
+def _checked_extent(op, datatype):
+    """extent of `datatype` when (op, datatype) is a supported pair, else 0.
+    Both answers are fixed by the compiled op table (MPIX_Redop_is_supported
+    ignores count), so they are looked up once per pair: the Python mirror's
+    per-call cost is part of every synchronous call it times."""
+    key = (op, datatype)
+    ext = _extent_cache.get(key)
+    if ext is None:
+        cop, cdt = H.as_c_int(op), H.as_c_int(datatype)
+        ext = 0
+        if lib().MPIX_Redop_is_supported(cop, 1, cdt):
+            ext = max(0, lib().MPIX_Datatype_extent(cdt))
+        _extent_cache[key] = ext
+    return ext
+
+
 def _span_check(count, datatype, op, *bufs):
     """count elements of `datatype` must fit every tensor / array operand: a
     short buffer would be an out-of-bounds access on the device, not an MPI
@@ -109,11 +128,9 @@ def _span_check(count, datatype, op, *bufs):
     count, type or op) go through, so they return their MPI error class."""
     if not isinstance(count, int) or count <= 0:
         return
-    if not lib().MPIX_Redop_is_supported(H.as_c_int(op), count, H.as_c_int(datatype)):
-        return
-    ext = lib().MPIX_Datatype_extent(H.as_c_int(datatype))
+    ext = _checked_extent(op, datatype)
     if ext <= 0:
-        return                          # the C call reports MPI_ERR_TYPE
+        return                          # the C call reports MPI_ERR_OP / MPI_ERR_TYPE
     for b in bufs:
         nb = _nbytes(b)
         if nb is not None and nb < count * ext:
