@@ -294,6 +294,17 @@ const char *MPIX_Redop_error_string(int code);
 int MPIX_Redop_set_launch(int block_threads, int max_grid);
 int MPIX_Redop_get_launch(int *block_threads, int *unroll, int *max_grid);
 
+/* ---- large pageable host operands (performance knob) ----
+ * threads > 0: operands of at least 2 * threads * chunk_bytes bytes go
+ * through that many host workers, which copy chunks into pinned slots of
+ * their own, each combined by a zero-copy kernel; smaller ones, and all of
+ * them with threads = 0, are staged through device scratch with
+ * hipMemcpyAsync.  Same bits either way.  Defaults 8 workers x 16 MiB (env
+ * MPIX_REDOP_PAGEABLE_THREADS / MPIX_REDOP_PAGEABLE_CHUNK at first use);
+ * threads 0..16, chunk 64 KiB..256 MiB. */
+int MPIX_Redop_set_pageable(int threads, MPIX_Aint chunk_bytes);
+int MPIX_Redop_get_pageable(int *threads, MPIX_Aint *chunk_bytes);
+
 /* Build identification: the gfx target the code object was compiled for. */
 const char *MPIX_Redop_build_info(void);
 

@@ -18,6 +18,7 @@
 #include <atomic>
 #include <chrono>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "mpix_redop.h"
@@ -249,6 +250,15 @@ size_t g_stage_chunk = (size_t) 64 << 20;
 // pageable hipMemcpy calls (each a driver-side bounce of its own);
 // MPIX_REDOP_BOUNCE_BYTES, 0 disables
 size_t g_bounce_bytes = (size_t) 1 << 20;
+// pageable operands of at least two chunks per worker: this many host
+// workers, each copying chunks of g_pipe_chunk bytes into a pinned slot of its
+// own that a zero-copy kernel then combines (MPIX_REDOP_PAGEABLE_THREADS, 0 =
+// always stream the chunks through device scratch with hipMemcpyAsync;
+// MPIX_REDOP_PAGEABLE_CHUNK).  8 x 16 MiB: 60 GiB/s end to end at 1 GiB
+// against 52 staged; with fewer chunks than that the workers cannot overlap
+// and staging is faster (profiles/r01_pageable_sweep.txt)
+std::atomic<int> g_pipe_threads{8};
+std::atomic<size_t> g_pipe_chunk{(size_t) 16 << 20};
 
 void read_env()
 {
@@ -270,6 +280,16 @@ void read_env()
         long long c = atoll(s);
         if (c >= 4096)
             g_stage_chunk = (size_t) c;
+    }
+    if (const char *s = getenv("MPIX_REDOP_PAGEABLE_THREADS")) {
+        int t = atoi(s);
+        if (t >= 0 && t <= 16)
+            g_pipe_threads = t;
+    }
+    if (const char *s = getenv("MPIX_REDOP_PAGEABLE_CHUNK")) {
+        long long c = atoll(s);
+        if (c >= 65536 && c <= (256ll << 20))
+            g_pipe_chunk = (size_t) c;
     }
     if (const char *s = getenv("MPIX_REDOP_BOUNCE_BYTES")) {
         long long c = atoll(s);
@@ -302,6 +322,13 @@ struct DevState {
     char *bounce = nullptr;     // pinned host: in half + inout half, bounce_half bytes each
     char *bounce_dev = nullptr; // its device mapping
     size_t bounce_half = 0;
+    // large pageable operands: one stream + pinned slot pair per host worker
+    struct PipeSlot {
+        hipStream_t s = nullptr;
+        char *host = nullptr;   // in half + inout half, pipe_half bytes each
+        char *dev = nullptr;    // its device mapping
+    } pipe[16];
+    size_t pipe_half = 0;       // slot half size; slots [0, threads) hold host != nullptr
 };
 // Per-thread device state (streams, flag word, scratch).  A thread that exits
 // hands its array to a process-wide pool and the next new thread takes it over
@@ -646,6 +673,99 @@ int bounced(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext,
     return rc;
 }
 
+// Large pageable operand(s): W host workers take chunks k = w, w + W, ...; per
+// chunk a worker memcpys the pageable operand(s) into its pinned slot, runs one
+// zero-copy kernel over the slot's device mapping on its own stream (a pinned
+// or device operand is used in place), waits for it and memcpys the result
+// back.  The workers' host copies overlap each other's PCIe transfers, where
+// hipMemcpyAsync from pageable memory serialises through the runtime's own
+// bounce.  Each element is combined exactly once, by the same kernel, so the
+// bits equal every other path's.  Returns -1 when the slots cannot be had
+// (caller stages).
+int pipelined(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext, uint32_t op,
+              bool in_pg, bool io_pg, int dev, int nthreads)
+{
+    DevState *d = dev_state(dev);
+    if (!d)
+        return MPIX_REDOP_ERR_OTHER;
+    const size_t half = (g_pipe_chunk.load() + 255) & ~(size_t) 255;
+    bool ready = d->pipe_half >= half;
+    for (int w = 0; ready && w < nthreads; ++w)
+        ready = d->pipe[w].host != nullptr;
+    if (!ready) {
+        // (re)allocate every worker's slot at the current chunk size
+        for (DevState::PipeSlot &sl : d->pipe) {
+            if (sl.s)
+                (void) hipStreamSynchronize(sl.s);
+            if (sl.host)
+                (void) hipHostFree(sl.host);
+            sl.host = sl.dev = nullptr;
+        }
+        d->pipe_half = 0;
+        for (int w = 0; w < nthreads; ++w) {
+            DevState::PipeSlot &sl = d->pipe[w];
+            if (!sl.s && hipStreamCreateWithFlags(&sl.s, hipStreamNonBlocking) != hipSuccess)
+                return -1;
+            void *h = nullptr, *hd = nullptr;
+            if (hipHostMalloc(&h, 2 * half, hipHostMallocDefault) != hipSuccess)
+                return -1;
+            if (hipHostGetDevicePointer(&hd, h, 0) != hipSuccess) {
+                (void) hipHostFree(h);
+                return -1;
+            }
+            sl.host = (char *) h;
+            sl.dev = (char *) hd;
+        }
+        d->pipe_half = half;
+    }
+    uint64_t chunk = half / ext;
+    if (chunk == 0)
+        return -1;
+    const uint64_t nchunks = (count + chunk - 1) / chunk;
+    const int W = (int) std::min<uint64_t>((uint64_t) nthreads, nchunks);
+    std::atomic<int> err{MPIX_REDOP_SUCCESS};
+    auto work = [&](int w) {
+        DevState::PipeSlot &sl = d->pipe[w];
+        if (hipSetDevice(dev) != hipSuccess) {
+            int z = MPIX_REDOP_SUCCESS;
+            err.compare_exchange_strong(z, MPIX_REDOP_ERR_OTHER);
+            return;
+        }
+        for (uint64_t k = (uint64_t) w; k < nchunks && err.load() == MPIX_REDOP_SUCCESS;
+             k += (uint64_t) W) {
+            const uint64_t off = k * chunk;
+            const uint64_t n = std::min(chunk, count - off);
+            const size_t bytes = (size_t) (n * ext);
+            const char *src_in = (const char *) in + off * ext;
+            char *dst_io = (char *) io + off * ext;
+            if (in_pg)
+                memcpy(sl.host, src_in, bytes);
+            if (io_pg)
+                memcpy(sl.host + half, dst_io, bytes);
+            const void *kin = in_pg ? (const void *) sl.dev : (const void *) src_in;
+            void *kio = io_pg ? (void *) (sl.dev + half) : (void *) dst_io;
+            int rc = enqueue(kin, kio, n, it, ext, op, sl.s);
+            if (rc == MPIX_REDOP_SUCCESS)
+                rc = hip_err(hipStreamSynchronize(sl.s));
+            if (rc != MPIX_REDOP_SUCCESS) {
+                int z = MPIX_REDOP_SUCCESS;
+                err.compare_exchange_strong(z, rc);
+                return;
+            }
+            if (io_pg)
+                memcpy(dst_io, sl.host + half, bytes);
+        }
+    };
+    std::vector<std::thread> pool;
+    pool.reserve(W > 0 ? W - 1 : 0);
+    for (int w = 1; w < W; ++w)
+        pool.emplace_back(work, w);
+    work(0);
+    for (std::thread &t : pool)
+        t.join();
+    return err.load();
+}
+
 struct DeviceGuard {
     int prev = -1;
     explicit DeviceGuard(int dev)
@@ -848,6 +968,12 @@ static void free_states(DevState *arr)
         }
         if (d.bounce)
             (void) hipHostFree(d.bounce);
+        for (DevState::PipeSlot &sl : d.pipe) {
+            if (sl.s)
+                (void) hipStreamDestroy(sl.s);
+            if (sl.host)
+                (void) hipHostFree(sl.host);
+        }
         d = DevState();
     }
     delete[] arr;
@@ -912,6 +1038,18 @@ int MPIX_Reduce_local(const void *inbuf, void *inoutbuf, MPIX_Aint count, MPIX_D
         rc = bounced(win == Where::Pageable ? inbuf : pin,
                      wio == Where::Pageable ? inoutbuf : (void *) pio, (uint64_t) count, it, ext,
                      (uint32_t) op, win == Where::Pageable, wio == Where::Pageable, dev);
+        if (rc >= 0)
+            return set_err(rc);
+    }
+    const int pipe_threads = g_pipe_threads.load();
+    if (pageable && zc && pipe_threads > 0 &&
+        (uint64_t) count * ext >= 2 * (uint64_t) pipe_threads * g_pipe_chunk.load()) {
+        // pageable operands through the workers' pinned slots; a pinned
+        // operand is used through its device mapping
+        rc = pipelined(win == Where::Pageable ? inbuf : pin,
+                       wio == Where::Pageable ? inoutbuf : (void *) pio, (uint64_t) count, it, ext,
+                       (uint32_t) op, win == Where::Pageable, wio == Where::Pageable, dev,
+                       pipe_threads);
         if (rc >= 0)
             return set_err(rc);
     }
@@ -1192,6 +1330,26 @@ int MPIX_Redop_set_launch(int block_threads, int max_grid)
         return MPIX_REDOP_ERR_ARG;
     g_block = block_threads;
     g_max_grid = max_grid;
+    return MPIX_REDOP_SUCCESS;
+}
+
+int MPIX_Redop_set_pageable(int threads, MPIX_Aint chunk_bytes)
+{
+    launch_cfg();
+    if (threads < 0 || threads > 16 || chunk_bytes < 65536 || chunk_bytes > ((MPIX_Aint) 256 << 20))
+        return MPIX_REDOP_ERR_ARG;
+    g_pipe_threads = threads;
+    g_pipe_chunk = (size_t) chunk_bytes;
+    return MPIX_REDOP_SUCCESS;
+}
+
+int MPIX_Redop_get_pageable(int *threads, MPIX_Aint *chunk_bytes)
+{
+    launch_cfg();
+    if (threads)
+        *threads = g_pipe_threads.load();
+    if (chunk_bytes)
+        *chunk_bytes = (MPIX_Aint) g_pipe_chunk.load();
     return MPIX_REDOP_SUCCESS;
 }
 

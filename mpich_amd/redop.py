@@ -64,6 +64,8 @@ def lib():
             'MPIX_Redop_set_fortran_booleans': ([i32, i32], i32),
             'MPIX_Redop_set_launch': ([i32, i32], i32),
             'MPIX_Redop_get_launch': ([ctypes.POINTER(i32)] * 3, i32),
+            'MPIX_Redop_set_pageable': ([i32, aint], i32),
+            'MPIX_Redop_get_pageable': ([ctypes.POINTER(i32), ctypes.POINTER(aint)], i32),
             'MPIX_Redop_last_error': ([], i32),
             'MPIX_Redop_error_string': ([i32], ctypes.c_char_p),
             'MPIX_Redop_build_info': ([], ctypes.c_char_p),
@@ -261,6 +263,18 @@ def datatype_size(datatype):
 
 def set_fortran_booleans(true_value, false_value):
     return lib().MPIX_Redop_set_fortran_booleans(true_value, false_value)
+
+
+def set_pageable(threads, chunk_bytes=16 << 20):
+    """host workers (0 = hipMemcpyAsync staging) and chunk size for large
+    pageable operands of the synchronous call; returns an MPI error class"""
+    return lib().MPIX_Redop_set_pageable(threads, chunk_bytes)
+
+
+def get_pageable():
+    t, c = ctypes.c_int(), ctypes.c_ssize_t()
+    check(lib().MPIX_Redop_get_pageable(ctypes.byref(t), ctypes.byref(c)))
+    return dict(threads=t.value, chunk_bytes=c.value)
 
 
 def set_launch(block_threads=256, max_grid=0):

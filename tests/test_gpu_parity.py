@@ -789,3 +789,74 @@ def test_chunked_pipeline_ragged(R, H, oracle, dtname, opname, npdt):
         oracle.reduce_local(x, exp, n, dt, op)
     got = d_acc.cpu().numpy()
     assert np.array_equal(got.view(np.uint8), exp.view(np.uint8))
+
+
+@pytest.mark.parametrize('threads,chunk', [(1, 65536), (4, 65536), (8, 256 << 10), (16, 128 << 10)])
+@pytest.mark.parametrize('place', ['both_host', 'host_in', 'host_inout', 'pinned_in'])
+def test_pageable_worker_pipeline(R, H, oracle, threads, chunk, place):
+    """large pageable operands through the host workers' pinned slots
+    (MPIX_Redop_set_pageable): ragged last chunk, mixed placements, fp32 SUM
+    and MPI_2INT MAXLOC with ties; bit-equal to the oracle and to the
+    hipMemcpyAsync staging path"""
+    prev = R.get_pageable()
+    rng = np.random.default_rng(0x5EED0F + threads)
+    n = (1 << 21) + 77
+    a = rng.uniform(-1, 1, n).astype(np.float32)
+    b = rng.uniform(-1, 1, n).astype(np.float32)
+    m = (1 << 20) + 3
+    p = rng.integers(0, 4, (m, 2)).astype(np.int32)
+    q = rng.integers(0, 4, (m, 2)).astype(np.int32)
+    exp_f = a.copy()
+    oracle.reduce_local(b, exp_f, n, H.MPI_FLOAT, H.MPI_SUM)
+    exp_p = p.copy()
+    oracle.reduce_local(q, exp_p, m, H.MPI_2INT, H.MPI_MAXLOC)
+
+    def place_ops(x_in, x_io):
+        if place == 'host_in':
+            return x_in, torch.from_numpy(x_io.copy()).cuda()
+        if place == 'host_inout':
+            return torch.from_numpy(x_in).cuda(), x_io
+        if place == 'pinned_in':
+            return torch.from_numpy(x_in.copy()).pin_memory(), x_io
+        return x_in, x_io
+
+    try:
+        for mode in (threads, 0):
+            assert R.set_pageable(mode, chunk) == 0
+            for x_in, x_io, cnt, dt, op, exp in ((b, a, n, H.MPI_FLOAT, H.MPI_SUM, exp_f),
+                                                 (q, p, m, H.MPI_2INT, H.MPI_MAXLOC, exp_p)):
+                i_op, io_op = place_ops(x_in, x_io.copy())
+                torch.cuda.synchronize()
+                assert R.MPI_Reduce_local(i_op, io_op, cnt, dt, op) == 0
+                got = io_op.cpu().numpy() if isinstance(io_op, torch.Tensor) else io_op
+                assert np.array_equal(got, exp), (mode, dt)
+    finally:
+        R.set_pageable(prev['threads'], prev['chunk_bytes'])
+
+
+def test_pageable_knob_errors(R):
+    prev = R.get_pageable()
+    assert R.set_pageable(-1, 1 << 20) == 12
+    assert R.set_pageable(17, 1 << 20) == 12
+    assert R.set_pageable(4, 1024) == 12
+    assert R.get_pageable() == prev
+
+
+def test_pageable_slots_after_shrink(R, H, oracle):
+    """regression: slots re-allocated for fewer workers at a larger chunk,
+    then more workers at a smaller chunk again (every worker needs a slot)"""
+    prev = R.get_pageable()
+    rng = np.random.default_rng(0x5EED10)
+    n = (1 << 21) + 5
+    a = rng.uniform(-1, 1, n).astype(np.float32)
+    b = rng.uniform(-1, 1, n).astype(np.float32)
+    exp = a.copy()
+    oracle.reduce_local(b, exp, n, H.MPI_FLOAT, H.MPI_SUM)
+    try:
+        for threads, chunk in ((16, 128 << 10), (4, 512 << 10), (16, 128 << 10), (2, 64 << 10)):
+            assert R.set_pageable(threads, chunk) == 0
+            got = a.copy()
+            assert R.MPI_Reduce_local(b, got, n, H.MPI_FLOAT, H.MPI_SUM) == 0
+            assert np.array_equal(got, exp), (threads, chunk)
+    finally:
+        R.set_pageable(prev['threads'], prev['chunk_bytes'])
