@@ -860,3 +860,37 @@ def test_pageable_slots_after_shrink(R, H, oracle):
             assert np.array_equal(got, exp), (threads, chunk)
     finally:
         R.set_pageable(prev['threads'], prev['chunk_bytes'])
+
+
+def test_pageable_workers_concurrent_callers(R, H, oracle):
+    """two application threads in the pageable worker path at once (each
+    caller has its own slots and streams); both results bit-equal"""
+    import threading
+    prev = R.get_pageable()
+    rng = np.random.default_rng(0x5EED11)
+    n = (1 << 21) + 9
+    ops = []
+    for _ in range(2):
+        a = rng.uniform(-1, 1, n).astype(np.float64)
+        b = rng.uniform(-1, 1, n).astype(np.float64)
+        e = a.copy()
+        oracle.reduce_local(b, e, n, H.MPI_DOUBLE, H.MPI_SUM)
+        ops.append((b, a, e))
+    rcs = [None, None]
+
+    def run(i):
+        b, a, _ = ops[i]
+        rcs[i] = [R.MPI_Reduce_local(b, a, n, H.MPI_DOUBLE, H.MPI_SUM) for _ in range(1)]
+
+    try:
+        assert R.set_pageable(4, 256 << 10) == 0
+        ts = [threading.Thread(target=run, args=(i,)) for i in range(2)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=60)
+        assert rcs == [[0], [0]]
+        for b, a, e in ops:
+            assert np.array_equal(a, e)
+    finally:
+        R.set_pageable(prev['threads'], prev['chunk_bytes'])
