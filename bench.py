@@ -29,6 +29,7 @@ import os
 import sys
 import time
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -355,6 +356,28 @@ def main():
                                          note='pinned host buffers: the kernel reads and writes '
                                               'them over PCIe (zero-copy); never `value`')
         del hin, hio
+        # the same from pageable (numpy) buffers: host workers feeding pinned
+        # slots (the default above 256 MiB), and the hipMemcpyAsync staging
+        try:
+            pin_ = np.random.default_rng(0x5EED0007 + rank).random(hn, dtype=np.float32)
+            pio_ = np.random.default_rng(0x5EED0008 + rank).random(hn, dtype=np.float32)
+            prev = redop.get_pageable()
+            pg = {}
+            for label, threads in (('workers', prev['threads'] or 8), ('staged', 0)):
+                redop.check(redop.set_pageable(threads, prev['chunk_bytes']))
+                redop.check(redop.MPI_Reduce_local(pin_, pio_, hn, H.MPI_FLOAT, H.MPI_SUM))
+                t0 = time.perf_counter()
+                for _ in range(reps):
+                    redop.check(redop.MPI_Reduce_local(pin_, pio_, hn, H.MPI_FLOAT, H.MPI_SUM))
+                tp = (time.perf_counter() - t0) / reps
+                pg[label] = dict(gibs=round(3 * hn * 4 / GIB / tp, 2), ms_per_call=round(tp * 1e3, 2))
+            redop.check(redop.set_pageable(prev['threads'], prev['chunk_bytes']))
+            pg['workers_x_chunk'] = '%d x %d MiB' % (prev['threads'] or 8, prev['chunk_bytes'] >> 20)
+            pg['note'] = 'pageable (numpy) host buffers; never `value`'
+            result['end_to_end_pageable'] = pg
+            del pin_, pio_
+        except Exception as e:      # secondary figure
+            result['end_to_end_pageable'] = dict(error='%s: %s' % (type(e).__name__, e))
 
     if args.sweep and rank == 0:
         sweep = []
