@@ -1,26 +1,29 @@
 #!/usr/bin/env python3
-"""Benchmark: device-resident MPI_Reduce_local (fp32 SUM, 1 GiB) on MI355X.
+"""Benchmark of the MI355X-native local reduction and the reduce-scatter it feeds.
 
-BASELINE.json metric "GiB/s device-resident MPI_Reduce_local (fp32 SUM,
-1 GiB) vs HBM roofline", on configs[1]: count = 2^28 MPI_FLOAT per operand,
-both operands resident in HBM before the timed region.  One step = one
-MPIX_Reduce_local call (the synchronous MPIR_Reduce_local drop-in) over the
-whole buffer; GiB/s = algorithmic bytes 3 * count * 4 (read in, read inout,
-write inout) / wall time.
+N = 1 (BASELINE.json metric "GiB/s device-resident MPI_Reduce_local (fp32
+SUM, 1 GiB) vs HBM roofline", configs[1] at 1 GiB): one step = one
+synchronous MPIX_Reduce_local call (the MPIR_Reduce_local drop-in) over
+count = 2^28 MPI_FLOAT per operand, both operands resident in HBM before the
+timed region; GiB/s = algorithmic bytes 3 * count * 4 (read in, read inout,
+write inout) / wall time.  `roofline` is the kernel alone (HIP events on its
+stream), `cpu_baseline` the oracle (clean-room C restatement of MPICH's
+op_fns.c loop) on a bounded sample of the same workload on this host's cores,
+`host_crossover` where the GPU path starts to beat one core on host-resident
+operands (the floor of MPIX_Redop_is_supported_buffers).
 
-N > 1 (torchrun, one rank per GPU): every rank reduces its own 1 GiB shard
-(no data-path collective: the path is element-wise), value = all ranks'
-bytes / max-over-ranks time ("weak" scaling).  Those runs also time the
-MPI_Reduce_scatter_block schedules (BASELINE config 4: recursive halving
-with a per-step breakdown, pairwise, fused IPC pull) and the allreduce as
-secondary figures.
-
-Also reported (not `value`): kernel-only rate from HIP events on the launch
-stream -> `roofline`; a measured STREAM triad on the same GPU; the
-host-resident end-to-end rate (pinned host operands, the kernel reads and
-writes them over PCIe); and the `cpu_baseline` -- the oracle (clean-room C
-restatement of MPICH's op loop) timed on this host's cores on a bounded
-sample of the same 1 GiB workload, plus BASELINE config 1 (16 MiB) beside it.
+N > 1 (torchrun, one rank per GPU; BASELINE configs[3] and north_star's
+"1/2/4/8-GPU reduce-scatter throughput ... absolute GB/s and fraction of
+roofline"): one step = one MPI_Reduce_scatter_block (fp32 SUM, a 4 GiB vector
+per rank, recvcount = 2^30 / N) by the reference's recursive-halving schedule
+(reduce_scatter_block_intra_recursive_halving.c:38-260) in libmpix_coll's C++
+host code over its own RCCL communicator, every received half combined by the
+HIP kernel; `value` = bus bandwidth (N-1)/N * 4 GiB / max-over-ranks time
+(nccl-tests' reduce-scatter convention, GB/s), checked bit for bit against a
+numpy restatement of the schedule's association before timing.  The N
+independent 1 GiB local reductions of round 1 are reported as an extra
+(`reduce_local_replicas`); the pairwise, pipelined, fused-pull schedules and
+the allreduce are secondary figures under a watchdog.
 """
 import argparse
 import ctypes
@@ -40,7 +43,10 @@ from mpich_amd import handles as H  # noqa: E402
 from mpich_amd import redop  # noqa: E402
 
 METRIC = "GiB/s device-resident MPI_Reduce_local (fp32 SUM, 1 GiB) vs HBM roofline"
+METRIC_RSB = ("GB/s MPI_Reduce_scatter_block bus bandwidth (fp32 SUM, 4 GiB vector per rank, "
+              "recursive halving over RCCL/xGMI, HIP combine)")
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+XGMI_LINK_GBS = 153.0       # one xGMI link, one direction (task brief: 7 x ~153 GB/s per GPU)
 GIB = float(1 << 30)
 
 
@@ -54,13 +60,12 @@ def parse():
                    help='bounded CPU-baseline sample duration per leg')
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--no-extras', action='store_true',
-                   help='skip triad / end-to-end / sweep side measurements')
+                   help='skip triad / end-to-end / crossover / secondary collective figures')
     p.add_argument('--sweep', action='store_true', help='config 2 chunk/size sweep')
-    p.add_argument('--rsb', action='store_true', help='time reduce_scatter_block even at N=1')
     p.add_argument('--rsb-bytes', type=int, default=4 << 30, help='RSB vector bytes per rank')
     p.add_argument('--extras-timeout', type=float, default=300.0,
-                   help='watchdog (s) over the N>1 collective figures and teardown')
-    p.add_argument('--pmc', default=os.path.join(ROOT, 'profiles', 'r01_pmc_summary.json'),
+                   help='watchdog (s) over the N>1 secondary collective figures and teardown')
+    p.add_argument('--pmc', default=os.path.join(ROOT, 'profiles', 'r02_pmc_summary.json'),
                    help='PMC traffic summary (from tools/pmc_summary.py) to quote as traffic')
     return p.parse_args()
 
@@ -82,6 +87,17 @@ def bench_lib():
     return L
 
 
+def c_call_median_us(B, fn_addr, inp, io, n, reps):
+    """median host time (us) of a synchronous C reduce function with the
+    MPIR_Reduce_local signature, timed in C by libmpix_bench"""
+    med, p90 = ctypes.c_double(), ctypes.c_double()
+    rc = B.mpix_bench_call_latency(fn_addr, inp, io, n, H.as_c_int(H.MPI_FLOAT),
+                                   H.as_c_int(H.MPI_SUM), reps, ctypes.byref(med), ctypes.byref(p90))
+    if rc:
+        raise RuntimeError('call latency loop failed: MPI error class %d' % rc)
+    return med.value
+
+
 def chunked_async_c(B, inb, inout, n, stream, chunk_bytes):
     """1 GiB (n fp32) combined as back-to-back MPIX_Reduce_local_async calls of
     chunk_bytes each, issued and timed in C by libmpix_bench (the loop a
@@ -98,8 +114,7 @@ def chunked_async_c(B, inb, inout, n, stream, chunk_bytes):
                                         H.as_c_int(H.MPI_FLOAT), H.as_c_int(H.MPI_SUM),
                                         stream.cuda_stream, ctypes.byref(issue), ctypes.byref(total))
         if rc:
-            out.append(dict(chunk_bytes=ck, error=rc))
-            continue
+            raise RuntimeError('chunked async loop failed: MPI error class %d' % rc)
         out.append(dict(chunk_bytes=ck, calls=nch, GiBs=round(3 * nch * ck / total.value / GIB, 1),
                         us_per_call=round(1e6 * total.value / nch, 2),
                         issue_us_per_call=round(1e6 * issue.value / nch, 2)))
@@ -121,9 +136,51 @@ def sync_call_latency(B, dev, counts=(1, 4096, 1 << 20), reps=2000):
                                        H.as_c_int(H.MPI_FLOAT), H.as_c_int(H.MPI_SUM), reps,
                                        ctypes.byref(med), ctypes.byref(p90))
         ok = rc == 0 and bool(torch.all(xio == reps + 1))
+        if not ok:
+            raise RuntimeError('sync call latency check failed at count %d (rc %d)' % (n, rc))
         out.append(dict(count=n, median_us=round(med.value, 2), p90_us=round(p90.value, 2),
                         checked=ok))
     return out
+
+
+CROSSOVER_BYTES = (4 << 10, 16 << 10, 64 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20,
+                   64 << 20, 256 << 20, 1 << 30)
+
+
+def _reps_for(nbytes):
+    return max(3, min(2000, (256 << 20) // max(nbytes, 1)))
+
+
+def host_crossover_gpu(B):
+    """GPU side of the host-resident crossover: MPIX_Reduce_local on pageable
+    (numpy) and page-locked (torch pin_memory) operands of each size, timed
+    in C (median us per call)"""
+    fn = ctypes.cast(redop.lib().MPIX_Reduce_local, ctypes.c_void_p).value
+    out = []
+    for nb in CROSSOVER_BYTES:
+        n = nb // 4
+        rng = np.random.default_rng(0x5EED0009)
+        a = rng.uniform(-1, 1, n).astype(np.float32)
+        b = rng.uniform(-1, 1, n).astype(np.float32)
+        reps = _reps_for(nb)
+        pg = c_call_median_us(B, fn, a.ctypes.data, b.ctypes.data, n, reps)
+        ta, tb = torch.from_numpy(a).pin_memory(), torch.from_numpy(b).pin_memory()
+        pn = c_call_median_us(B, fn, ta.data_ptr(), tb.data_ptr(), n, reps)
+        out.append(dict(bytes=nb, gpu_pageable_us=round(pg, 2), gpu_pinned_us=round(pn, 2)))
+        del a, b, ta, tb
+    return out
+
+
+def crossover_from(rows, key):
+    """smallest size from which the GPU path is faster than one core at
+    every larger size too (None: the CPU wins at every measured size)"""
+    best = None
+    for r in reversed(rows):
+        if r[key] < r['cpu_1core_us']:
+            best = r['bytes']
+        else:
+            break
+    return best
 
 
 def event_time_per_launch(launch, reps, stream, rounds=3):
@@ -159,14 +216,14 @@ def allreduce_scalar(x, op, dev):
     return t.item()
 
 
-def cpu_baseline(seconds, count):
+def cpu_baseline(seconds, count, crossover_rows):
     """The oracle (clean-room C restatement of MPICH's op_fns.c loop) on a
     bounded sample of the SAME workload: MPI_Reduce_local(MPI_SUM, MPI_FLOAT)
     on `count`-element (1 GiB) host operands, repeated for ~seconds/2 on one
     core (MPICH's path is one thread per rank) and ~seconds/2 on all cores
     of this process's share.  BASELINE config 1 (16 MiB, cache-resident on
-    this host) is reported beside it."""
-    import numpy as np
+    this host) is reported beside it, and one core's time per call at each
+    host-crossover size (timed in C, like the GPU side) fills crossover_rows."""
     from oracle import oracle as orc
     orc.build()
     ncores = len(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') else os.cpu_count()
@@ -187,9 +244,19 @@ def cpu_baseline(seconds, count):
         return dict(gibs=round(3 * n * 4 / GIB / med, 3), best=round(3 * n * 4 / GIB / t_list[0], 3),
                     reps=len(t_list), threads=nth)
 
-    one = leg(count, 1, seconds * 0.45)
-    allc = leg(count, threads_all, seconds * 0.35)
-    c1 = leg(4194304, 1, seconds * 0.2)
+    one = leg(count, 1, seconds * 0.4)
+    allc = leg(count, threads_all, seconds * 0.3)
+    c1 = leg(4194304, 1, seconds * 0.15)
+    if crossover_rows:
+        B = bench_lib()
+        fn = ctypes.cast(orc.lib().oracle_reduce_local, ctypes.c_void_p).value
+        for r in crossover_rows:
+            n = r['bytes'] // 4
+            rng = np.random.default_rng(0x5EED0009)
+            a = rng.uniform(-1, 1, n).astype(np.float32)
+            b = rng.uniform(-1, 1, n).astype(np.float32)
+            r['cpu_1core_us'] = round(c_call_median_us(B, fn, a.ctypes.data, b.ctypes.data, n,
+                                                       _reps_for(r['bytes'])), 2)
     model = ''
     try:
         for line in open('/proc/cpuinfo'):
@@ -213,40 +280,23 @@ def cpu_baseline(seconds, count):
 
 
 def load_pmc(path, count):
-    try:
-        with open(path) as f:
-            d = json.load(f)
-    except (OSError, ValueError):
-        return None
-    k = d.get('kernels', {}).get('reduce_local_fp32_sum')
-    if not k or k.get('count') != count:
-        return None
-    return k.get('hbm_bytes_per_launch')
+    for p in (path, os.path.join(ROOT, 'profiles', 'r01_pmc_summary.json')):
+        try:
+            with open(p) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        k = d.get('kernels', {}).get('reduce_local_fp32_sum')
+        if k and k.get('count') == count:
+            return k.get('hbm_bytes_per_launch')
+    return None
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
-    # rehearsal knobs for a 1-GPU box (not used by the driver): every rank on
-    # device 0 and a gloo control plane; RCCL-transport figures then error out
-    # (caught) and only the flow, the replicas and the IPC pull are exercised
-    if os.environ.get('MPIX_BENCH_SAME_DEVICE') == '1':
-        local = 0
-    backend = os.environ.get('MPIX_BENCH_BACKEND', 'nccl')
-    if world > 1:
-        torch.cuda.set_device(local)
-        if backend == 'nccl':
-            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
-        else:
-            dist.init_process_group(backend)
-    dev = torch.device('cuda', local)
-    torch.cuda.set_device(dev)
-    assert redop.lib().MPIX_Redop_init() == 0
-
+# ------------------------------------------------------------------ N = 1
+def reduce_local_leg(args, world, rank, dev):
+    """the headline loop: synchronous MPIX_Reduce_local over 1 GiB operands,
+    barrier + synchronize around exactly `steps` calls, max over ranks"""
     n = args.count
-    nbytes_alg = 3 * n * 4
     inout = torch.empty(n, dtype=torch.float32, device=dev)
     inb = torch.empty(n, dtype=torch.float32, device=dev)
     fill_uniform(inout, 0x5EED0001 + 2 * rank)
@@ -270,200 +320,387 @@ def main():
     t = time.perf_counter() - t0
     if world > 1:
         t = allreduce_scalar(t, dist.ReduceOp.MAX, dev)
-    ms_per_step = 1e3 * t / args.steps
-    value = world * nbytes_alg * args.steps / t / GIB
-
-    # kernel-only: the same launch, async on torch's stream, timed by events
     stream = torch.cuda.current_stream()
     kreps = max(10, min(args.steps, 50))
     k_avg, k_med, k_min = event_time_per_launch(
         lambda: redop.check(redop.reduce_local_async(inb, inout, n, H.MPI_FLOAT, H.MPI_SUM,
                                                      stream)), kreps, stream)
-    achieved = nbytes_alg / (k_avg * 1e-3) / 1e9
+    return dict(t=t, k_avg=k_avg, k_med=k_med, k_min=k_min, kreps=kreps, inb=inb, inout=inout,
+                stream=stream)
+
+
+def single_gpu(args, dev):
+    n = args.count
+    nbytes_alg = 3 * n * 4
+    leg = reduce_local_leg(args, 1, 0, dev)
+    inb, inout, stream, kreps = leg['inb'], leg['inout'], leg['stream'], leg['kreps']
+    achieved = nbytes_alg / (leg['k_avg'] * 1e-3) / 1e9
     result = {
         'metric': METRIC,
-        'value': round(value, 2),
+        'value': round(nbytes_alg * args.steps / leg['t'] / GIB, 2),
         'unit': 'GiB/s',
-        'n_gpus': world,
+        'n_gpus': 1,
         'steps': args.steps,
         'warmup': args.warmup,
-        'ms_per_step': round(ms_per_step, 4),
+        'ms_per_step': round(1e3 * leg['t'] / args.steps, 4),
         'higher_is_better': True,
         'scaling': 'weak',
         'vs_baseline': None,
         'dtype': 'f32',
-        'data': 'synthetic (uniform [-1,1), seeded per rank)',
+        'data': 'synthetic (uniform [-1,1), seeded)',
         'config': {
             'workload': 'MPI_Reduce_local(MPI_SUM, MPI_FLOAT) device-resident, BASELINE configs[1] '
                         'at its 1 GiB point',
             'count': n, 'bytes_per_operand': 4 * n, 'algorithmic_bytes_per_step': nbytes_alg,
-            'parallelism': 'replicas' if world == 1 else 'dp%d shards (no collective)' % world,
+            'parallelism': 'single GPU',
             'launch': redop.get_launch(),
         },
         'roofline': {
             'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
             'frac': round(achieved / HBM_PEAK_GBS, 4),
             'traffic': load_pmc(args.pmc, n),
-            'kernel_ms_avg': round(k_avg, 4), 'kernel_ms_median_batch': round(k_med, 4),
-            'kernel_ms_min_batch': round(k_min, 4), 'kernel_launches_timed': 3 * kreps,
+            'kernel_ms_avg': round(leg['k_avg'], 4), 'kernel_ms_median_batch': round(leg['k_med'], 4),
+            'kernel_ms_min_batch': round(leg['k_min'], 4), 'kernel_launches_timed': 3 * kreps,
             'algorithmic_bytes_per_launch': nbytes_alg,
         },
     }
-
-    if not args.no_extras and rank == 0:
+    crossover = None
+    if not args.no_extras:
+        B = bench_lib()
         # STREAM triad on the same GPU (three separate 1 GiB fp32 arrays)
-        try:
-            B = bench_lib()
-            a3 = torch.empty(n, dtype=torch.float32, device=dev)
-            tri_avg, tri_med, _ = event_time_per_launch(
-                lambda: B.mpix_bench_triad(a3.data_ptr(), inb.data_ptr(), inout.data_ptr(),
-                                           ctypes.c_float(0.5), n, stream.cuda_stream),
-                kreps, stream)
-            triad = nbytes_alg / (tri_avg * 1e-3) / 1e9
-            result['roofline']['triad_measured_GBs'] = round(triad, 1)
-            result['roofline']['frac_of_triad'] = round(achieved / triad, 4)
-            del a3
-            # small-message regime of the same entry point: per-call latency
-            try:
-                result['sync_call_latency'] = sync_call_latency(B, dev)
-            except Exception as e:      # secondary figure: never lose the headline line
-                result['sync_call_latency'] = dict(error='%s: %s' % (type(e).__name__, e))
-            try:
-                result['chunked_async_c'] = chunked_async_c(
-                    B, inb, inout, n, stream,
-                    (64 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20, 64 << 20) if args.sweep
-                    else (64 << 10, 1 << 20, 16 << 20))
-            except Exception as e:      # secondary figure
-                result['chunked_async_c'] = dict(error='%s: %s' % (type(e).__name__, e))
-        except OSError as e:
-            result['roofline']['triad_measured_GBs'] = None
-            result['roofline']['triad_error'] = str(e)
-        # host-resident end-to-end: pinned host in/inout -> MPIX_Reduce_local
-        # stages H2D + kernel + D2H (3 x 1 GiB over PCIe)
-        hn = n
-        hin = torch.empty(hn, dtype=torch.float32).pin_memory()
-        hio = torch.empty(hn, dtype=torch.float32).pin_memory()
-        hin.uniform_(-1, 1)
-        hio.uniform_(-1, 1)
-        redop.check(redop.MPI_Reduce_local(hin, hio, hn, H.MPI_FLOAT, H.MPI_SUM))
-        reps = 3
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            redop.check(redop.MPI_Reduce_local(hin, hio, hn, H.MPI_FLOAT, H.MPI_SUM))
-        te = (time.perf_counter() - t0) / reps
-        result['end_to_end_host'] = dict(gibs=round(3 * hn * 4 / GIB / te, 2),
-                                         ms_per_call=round(te * 1e3, 2),
-                                         note='pinned host buffers: the kernel reads and writes '
-                                              'them over PCIe (zero-copy); never `value`')
-        del hin, hio
-        # the same from pageable (numpy) buffers: host workers feeding pinned
-        # slots (the default above 256 MiB), and the hipMemcpyAsync staging
-        try:
-            pin_ = np.random.default_rng(0x5EED0007 + rank).random(hn, dtype=np.float32)
-            pio_ = np.random.default_rng(0x5EED0008 + rank).random(hn, dtype=np.float32)
-            prev = redop.get_pageable()
-            pg = {}
-            for label, threads in (('workers', prev['threads'] or 8), ('staged', 0)):
-                redop.check(redop.set_pageable(threads, prev['chunk_bytes']))
-                redop.check(redop.MPI_Reduce_local(pin_, pio_, hn, H.MPI_FLOAT, H.MPI_SUM))
-                t0 = time.perf_counter()
-                for _ in range(reps):
-                    redop.check(redop.MPI_Reduce_local(pin_, pio_, hn, H.MPI_FLOAT, H.MPI_SUM))
-                tp = (time.perf_counter() - t0) / reps
-                pg[label] = dict(gibs=round(3 * hn * 4 / GIB / tp, 2), ms_per_call=round(tp * 1e3, 2))
-            redop.check(redop.set_pageable(prev['threads'], prev['chunk_bytes']))
-            pg['workers_x_chunk'] = '%d x %d MiB' % (prev['threads'] or 8, prev['chunk_bytes'] >> 20)
-            pg['note'] = 'pageable (numpy) host buffers; never `value`'
-            result['end_to_end_pageable'] = pg
-            del pin_, pio_
-        except Exception as e:      # secondary figure
-            result['end_to_end_pageable'] = dict(error='%s: %s' % (type(e).__name__, e))
-
-    if args.sweep and rank == 0:
-        sweep = []
-        for mib in (16, 32, 64, 128, 256, 512, 1024):
-            m = mib * (1 << 20) // 4
-            if m > n:
-                break
-            avg, _, _ = event_time_per_launch(
-                lambda: redop.check(redop.reduce_local_async(inb, inout, m, H.MPI_FLOAT,
-                                                             H.MPI_SUM, stream)), 20, stream)
-            sweep.append(dict(mib=mib, kernel_ms=round(avg, 4),
-                              GBs=round(3 * m * 4 / (avg * 1e-3) / 1e9, 1)))
-        chunks = []
-        for ck in (64 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20, 64 << 20, 256 << 20, 1 << 30):
-            m = ck // 4
-            nch = n // m
-            t0 = time.perf_counter()
-            torch.cuda.synchronize()
-            for k in range(nch):
-                redop.check(redop.reduce_local_async(inb[k * m:], inout[k * m:], m, H.MPI_FLOAT,
-                                                     H.MPI_SUM, stream))
-            torch.cuda.synchronize()
-            tt = time.perf_counter() - t0
-            chunks.append(dict(chunk_bytes=ck, calls=nch, GiBs=round(nbytes_alg / tt / GIB, 1)))
-        # the same chunked sweep replayed from a HIP graph (torch.cuda.graph):
-        # the launch-bound small chunks lose the per-call host launch cost
-        graphed = []
-        gs = torch.cuda.Stream()
-        for ck in (64 << 10, 256 << 10, 1 << 20, 4 << 20):
-            m = ck // 4
-            nch = min(n // m, 4096)
-            g = torch.cuda.CUDAGraph()
-            gs.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(gs):
-                with torch.cuda.graph(g, stream=gs):
-                    for k in range(nch):
-                        redop.check(redop.reduce_local_async(inb[k * m:], inout[k * m:], m,
-                                                             H.MPI_FLOAT, H.MPI_SUM, gs))
-            torch.cuda.synchronize()
-            g.replay()
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            g.replay()
-            torch.cuda.synchronize()
-            tt = time.perf_counter() - t0
-            graphed.append(dict(chunk_bytes=ck, calls=nch, GiBs=round(3 * m * 4 * nch / tt / GIB, 1)))
-            del g
-        result['sweep'] = dict(size_kernel=sweep, chunked_1gib_async=chunks,
-                               chunked_hipgraph_replay=graphed)
-
+        a3 = torch.empty(n, dtype=torch.float32, device=dev)
+        tri_avg, _, _ = event_time_per_launch(
+            lambda: B.mpix_bench_triad(a3.data_ptr(), inb.data_ptr(), inout.data_ptr(),
+                                       ctypes.c_float(0.5), n, stream.cuda_stream), kreps, stream)
+        triad = nbytes_alg / (tri_avg * 1e-3) / 1e9
+        result['roofline']['triad_measured_GBs'] = round(triad, 1)
+        result['roofline']['frac_of_triad'] = round(achieved / triad, 4)
+        del a3
+        result['sync_call_latency'] = sync_call_latency(B, dev)
+        result['chunked_async_c'] = chunked_async_c(
+            B, inb, inout, n, stream,
+            (64 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20, 64 << 20) if args.sweep
+            else (64 << 10, 1 << 20, 16 << 20))
+        end_to_end(result, n)
+        crossover = host_crossover_gpu(B)
+    if args.sweep:
+        result['sweep'] = size_sweep(inb, inout, n, stream, nbytes_alg)
     del inout, inb
     torch.cuda.empty_cache()
+    if not args.no_cpu_baseline:
+        result['cpu_baseline'] = cpu_baseline(args.cpu_seconds, args.count, crossover)
+        if crossover:
+            sup = redop.get_support()
+            result['host_crossover'] = dict(
+                rows=crossover,
+                pageable_crossover_bytes=crossover_from(crossover, 'gpu_pageable_us'),
+                pinned_crossover_bytes=crossover_from(crossover, 'gpu_pinned_us'),
+                library_floors=dict(pageable=sup['host_floor_bytes'],
+                                    pinned=sup['pinned_floor_bytes']),
+                note='bytes per operand; GPU = synchronous MPIX_Reduce_local on host operands, '
+                     'CPU = the oracle loop on one core, both median per call timed in C; the '
+                     'crossover is the smallest size from which the GPU path wins at every larger '
+                     'size (the MPIX_Redop_is_supported_buffers floor)')
+    print(json.dumps(result, default=str), flush=True)
 
-    # The headline is complete here.  Everything after it (collective
-    # figures, teardown) runs under a watchdog: if a secondary collective
-    # hangs on some rank, rank 0 still prints the line (with what it has)
-    # and every rank leaves, instead of the job dying silently at the
-    # driver's limit.
-    emit = _Emitter(rank, result)
-    dog = None
-    if world > 1 or args.rsb:
-        dog = _watchdog(args.extras_timeout, emit)
-        result['extras_timeout_s'] = args.extras_timeout
-        if os.environ.get('MPIX_BENCH_STALL_RANK') == str(rank):
-            time.sleep(1e6)     # rehearsal knob: a rank that never arrives
-        # filled in place, so a watchdog line carries the figures already taken
-        for key, fn in (('reduce_scatter_block', rsb_bench), ('allreduce', allreduce_bench)):
-            part = result[key] = {}
-            try:
-                fn(args, world, rank, dev, part)
-            except Exception as e:  # secondary figure: never lose the headline line
-                part['error'] = '%s: %s' % (type(e).__name__, e)
 
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result['cpu_baseline'] = cpu_baseline(args.cpu_seconds, args.count)
-    emit.emit()
-    if world > 1:
-        try:
-            dist.barrier()
-            if _CCL.get('comm') is not None:
-                _CCL.pop('comm').free()
-            dist.destroy_process_group()
-        except Exception as e:  # a peer already left (its error is in the line)
-            print('teardown: %s: %s' % (type(e).__name__, e), file=sys.stderr, flush=True)
-    if dog is not None:
-        dog.cancel()
+def end_to_end(result, n):
+    """host-resident end to end (never `value`): pinned operands read and
+    written by the kernel over PCIe; pageable operands through the host
+    workers and through hipMemcpyAsync staging"""
+    hin = torch.empty(n, dtype=torch.float32).pin_memory()
+    hio = torch.empty(n, dtype=torch.float32).pin_memory()
+    hin.uniform_(-1, 1)
+    hio.uniform_(-1, 1)
+    redop.check(redop.MPI_Reduce_local(hin, hio, n, H.MPI_FLOAT, H.MPI_SUM))
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        redop.check(redop.MPI_Reduce_local(hin, hio, n, H.MPI_FLOAT, H.MPI_SUM))
+    te = (time.perf_counter() - t0) / reps
+    result['end_to_end_host'] = dict(gibs=round(3 * n * 4 / GIB / te, 2),
+                                     ms_per_call=round(te * 1e3, 2),
+                                     note='pinned host buffers: the kernel reads and writes '
+                                          'them over PCIe (zero-copy); never `value`')
+    del hin, hio
+    pin_ = np.random.default_rng(0x5EED0007).random(n, dtype=np.float32)
+    pio_ = np.random.default_rng(0x5EED0008).random(n, dtype=np.float32)
+    prev = redop.get_pageable()
+    pg = {}
+    try:
+        for label, threads in (('workers', prev['threads'] or 8), ('staged', 0)):
+            redop.check(redop.set_pageable(threads, prev['chunk_bytes']))
+            redop.check(redop.MPI_Reduce_local(pin_, pio_, n, H.MPI_FLOAT, H.MPI_SUM))
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                redop.check(redop.MPI_Reduce_local(pin_, pio_, n, H.MPI_FLOAT, H.MPI_SUM))
+            tp = (time.perf_counter() - t0) / reps
+            pg[label] = dict(gibs=round(3 * n * 4 / GIB / tp, 2), ms_per_call=round(tp * 1e3, 2))
+    finally:
+        redop.check(redop.set_pageable(prev['threads'], prev['chunk_bytes']))
+    pg['workers_x_chunk'] = '%d x %d MiB' % (prev['threads'] or 8, prev['chunk_bytes'] >> 20)
+    pg['note'] = 'pageable (numpy) host buffers; never `value`'
+    result['end_to_end_pageable'] = pg
+
+
+def size_sweep(inb, inout, n, stream, nbytes_alg):
+    sweep = []
+    for mib in (16, 32, 64, 128, 256, 512, 1024):
+        m = mib * (1 << 20) // 4
+        if m > n:
+            break
+        avg, _, _ = event_time_per_launch(
+            lambda: redop.check(redop.reduce_local_async(inb, inout, m, H.MPI_FLOAT,
+                                                         H.MPI_SUM, stream)), 20, stream)
+        sweep.append(dict(mib=mib, kernel_ms=round(avg, 4),
+                          GBs=round(3 * m * 4 / (avg * 1e-3) / 1e9, 1)))
+    # the chunked sweep replayed from a HIP graph: the launch-bound small
+    # chunks lose the per-call host launch cost
+    graphed = []
+    gs = torch.cuda.Stream()
+    for ck in (64 << 10, 256 << 10, 1 << 20, 4 << 20):
+        m = ck // 4
+        nch = min(n // m, 4096)
+        g = torch.cuda.CUDAGraph()
+        gs.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(gs):
+            with torch.cuda.graph(g, stream=gs):
+                for k in range(nch):
+                    redop.check(redop.reduce_local_async(inb[k * m:], inout[k * m:], m,
+                                                         H.MPI_FLOAT, H.MPI_SUM, gs))
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        g.replay()
+        torch.cuda.synchronize()
+        tt = time.perf_counter() - t0
+        graphed.append(dict(chunk_bytes=ck, calls=nch, GiBs=round(3 * m * 4 * nch / tt / GIB, 1)))
+        del g
+    return dict(size_kernel=sweep, chunked_hipgraph_replay=graphed)
+
+
+# ------------------------------------------------------------------ N > 1
+def rh_expected_block(sends, rank, recvcount):
+    """rank's block of MPI_Reduce_scatter_block by recursive halving, as the
+    reference schedule associates it (…recursive_halving.c:110-229): the
+    non-power-of-two fold (odd rank 2i+1 adds rank 2i's vector), then per
+    step with mask = pof2/2 .. 1 every new rank adds its partner's partial
+    (one IEEE fp32 add each, so the tree alone fixes the bits)"""
+    P = len(sends)
+    pof2 = 1
+    while pof2 * 2 <= P:
+        pof2 *= 2
+    rem = P - pof2
+    parts = [sends[2 * i + 1] + sends[2 * i] for i in range(rem)] + \
+        [sends[r] for r in range(2 * rem, P)]
+    m = pof2 // 2
+    while m:
+        parts = [parts[q] + parts[q ^ m] for q in range(pof2)]
+        m //= 2
+    owner = rank // 2 if rank < 2 * rem else rank - rem
+    return parts[owner][rank * recvcount:(rank + 1) * recvcount]
+
+
+def rsb_inputs_host(r, P, recvcount):
+    return np.random.default_rng(0x5EED0100 + r).uniform(-1, 1, P * recvcount).astype(np.float32)
+
+
+def multi_gpu(args, world, rank, dev):
+    from mpich_amd import ccl
+    result = {'metric': METRIC_RSB, 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
+              'unit': 'GB/s', 'higher_is_better': True, 'scaling': 'strong', 'vs_baseline': None,
+              'dtype': 'f32', 'data': 'synthetic (uniform [-1,1), seeded per rank)'}
+    # the round-1 figure, kept as an extra: N independent 1 GiB local reductions
+    leg = reduce_local_leg(args, world, rank, dev)
+    n = args.count
+    result['reduce_local_replicas'] = dict(
+        value_GiBs=round(world * 3 * n * 4 * args.steps / leg['t'] / GIB, 2),
+        ms_per_step=round(1e3 * leg['t'] / args.steps, 4),
+        kernel_ms_avg_rank0=round(leg['k_avg'], 4),
+        note='every rank reduces its own 1 GiB operands, no collective (round-1 N>1 value)')
+    del leg
+    torch.cuda.empty_cache()
+
+    if dist.get_backend() == 'nccl':
+        cc = ccl.comm_create_ccl_from_process_group()
+    else:   # 1-GPU rehearsal: the same C++ schedules over gloo through pinned staging
+        from mpich_amd import coll
+        cc = coll.comm_for(None, True)
+    _CCL['comm'] = cc
+    total = (args.rsb_bytes // 4) // world * world
+    recvcount = total // world
+    # parity before timing: fp32 SUM at a reduced size, bit for bit against
+    # the schedule's association restated in numpy on every rank
+    rc_small = (1 << 16) + 3
+    sends = [rsb_inputs_host(r, world, rc_small) for r in range(world)]
+    ds = torch.from_numpy(sends[rank]).to(dev)
+    dr = torch.empty(rc_small, dtype=torch.float32, device=dev)
+    redop.check(ccl.reduce_scatter_block(ds, dr, rc_small, H.MPI_FLOAT, H.MPI_SUM, cc,
+                                         'recursive_halving'), 'MPIX_Reduce_scatter_block')
+    got = dr.cpu().numpy()
+    ok = got.tobytes() == rh_expected_block(sends, rank, rc_small).tobytes()
+    ok_all = allreduce_scalar(1.0 if ok else 0.0, dist.ReduceOp.MIN, dev) == 1.0
+    del ds, dr, sends
+    if not ok_all:
+        raise RuntimeError('recursive-halving RSB over RCCL differs from the reference association '
+                           '(fp32 SUM, recvcount %d) on some rank' % rc_small)
+
+    send = torch.empty(total, dtype=torch.float32, device=dev)
+    fill_uniform(send, 0x5EED0100 + rank)
+    recv = torch.empty(recvcount, dtype=torch.float32, device=dev)
+    ws = torch.empty(ccl.rsb_workspace_bytes(recvcount, H.MPI_FLOAT, cc, 'recursive_halving'),
+                     dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+
+    def step():
+        redop.check(ccl.reduce_scatter_block(send, recv, recvcount, H.MPI_FLOAT, H.MPI_SUM, cc,
+                                             'recursive_halving', workspace=ws),
+                    'MPIX_Reduce_scatter_block')
+
+    for _ in range(args.warmup):
+        step()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    t = allreduce_scalar(time.perf_counter() - t0, dist.ReduceOp.MAX, dev) / args.steps
+    busbytes = (world - 1) / world * total * 4
+    pof2 = 1
+    while pof2 * 2 <= world:
+        pof2 *= 2
+    link_bytes = (pof2 - 1) / pof2 * total * 4      # received over one link across the steps
+    # per-step breakdown on rank 0's stream (SURVEY.md §8(d) C4)
+    cc.set_step_timing(True)
+    step()
+    torch.cuda.synchronize()
+    cc.set_step_timing(False)
+    steps = cc.step_times()
+    comb_ms = sum(s['ms'] for s in steps if s['phase'] == 'combine')
+    exch_ms = sum(s['ms'] for s in steps if s['phase'] == 'exchange')
+    combined = (pof2 - 1) / pof2 * total            # elements this rank combined (pof2 ranks)
+    comb_gbs = 3 * combined * 4 / (comb_ms * 1e-3) / 1e9 if comb_ms > 0 else None
+    result.update(
+        value=round(busbytes / t / 1e9, 2),
+        ms_per_step=round(t * 1e3, 4),
+        config={'workload': 'MPI_Reduce_scatter_block(MPI_SUM, MPI_FLOAT), BASELINE configs[3]: '
+                            '4 GiB vector per rank, recursive halving, RCCL/xGMI chunk transport',
+                'vector_bytes_per_rank': total * 4, 'recvcount': recvcount,
+                'parallelism': 'rsb%d (one rank per GPU, libmpix_coll over RCCL)' % world},
+        parity=dict(checked=True, recvcount=rc_small, bit_exact_all_ranks=True,
+                    against='numpy restatement of the recursive-halving association'),
+        roofline={'bound': 'hbm', 'unit': 'GB/s',
+                  'achieved': round(comb_gbs, 1) if comb_gbs else None, 'peak': HBM_PEAK_GBS,
+                  'frac': round(comb_gbs / HBM_PEAK_GBS, 4) if comb_gbs else None,
+                  'traffic': None,
+                  'what': 'the HIP combine steps of rank 0 (3 x 4 B per combined element over '
+                          'their event-timed device time)',
+                  'link': {'bound': 'xgmi', 'achieved': round(link_bytes / t / 1e9, 2),
+                           'peak': XGMI_LINK_GBS,
+                           'frac': round(link_bytes / t / 1e9 / XGMI_LINK_GBS, 4),
+                           'note': 'bytes a rank receives over its one active link across the '
+                                   'log2(P) steps / step time'}},
+        steps_rank0=steps,
+        step_split_rank0=dict(exchange_ms=round(exch_ms, 3), combine_ms=round(comb_ms, 3)))
+    del send, recv, ws
+    torch.cuda.empty_cache()
+    return result
+
+
+def rsb_secondary(args, world, rank, dev, out):
+    """the other schedules on the same RCCL communicator: pairwise (all P-1
+    links in one group + one multi-input combine), pipelined pairwise, the
+    fused IPC pull; each parity-checked first (redscatblk3.c:43-56 closed
+    form on device, every rank)"""
+    from mpich_amd import ccl
+    cc = _CCL['comm']
+    total = (args.rsb_bytes // 4) // world * world
+    recvcount = total // world
+    send = torch.empty(total, dtype=torch.float32, device=dev)
+    fill_uniform(send, 0x5EED0100 + rank)
+    recv = torch.empty(recvcount, dtype=torch.float32, device=dev)
+    for algo in ('pairwise', 'pairwise_pipelined', 'pull'):
+        rc_small = 4096 + 3
+        blk = torch.cat([torch.full((rc_small,), rank + i, dtype=torch.int32, device=dev)
+                         for i in range(world)])
+        o = torch.empty(rc_small, dtype=torch.int32, device=dev)
+        redop.check(ccl.reduce_scatter_block(blk, o, rc_small, H.MPI_INT, H.MPI_SUM, cc, algo),
+                    'MPIX_Reduce_scatter_block')
+        ok = allreduce_scalar(1 if bool(torch.all(o == world * rank + world * (world - 1) // 2))
+                              else 0, dist.ReduceOp.MIN, dev)
+        if not ok:
+            raise RuntimeError('%s RSB fails the redscatblk3 closed form' % algo)
+
+        def once():
+            redop.check(ccl.reduce_scatter_block(send, recv, recvcount, H.MPI_FLOAT, H.MPI_SUM, cc,
+                                                 algo), 'MPIX_Reduce_scatter_block')
+        once()
+        reps = max(3, min(10, args.steps))
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            once()
+        torch.cuda.synchronize()
+        dist.barrier()
+        t = allreduce_scalar((time.perf_counter() - t0) / reps, dist.ReduceOp.MAX, dev)
+        link_bytes = total * 4 / world              # one block per peer link, all links at once
+        out[algo] = dict(parity_redscatblk3_all_ranks=True, ms=round(t * 1e3, 3),
+                         busbw_GBs=round((world - 1) / world * total * 4 / t / 1e9, 2),
+                         per_link_GBs=round(link_bytes / t / 1e9, 2), links_active=world - 1,
+                         frac_of_xgmi_link=round(link_bytes / t / 1e9 / XGMI_LINK_GBS, 4))
+    del send, recv
+    torch.cuda.empty_cache()
+
+
+def allreduce_secondary(args, world, rank, dev, res):
+    """MPI_Allreduce fp32 SUM, 1 GiB per rank: the reference's
+    reduce-scatter + allgather schedule (libmpix_coll over RCCL point-to-point
+    + the HIP combine, the reference association) next to RCCL's own
+    all_reduce (ncclAllReduce, the reference's MPIR_Allreduce_intra_ccl route,
+    rccl.c:223) as the comparator"""
+    from mpich_amd import ccl
+    cc = _CCL['comm']
+    m = 100003          # allred.c sum_test_1 closed form (in = i, sol = i*P), on device
+    x = torch.arange(m, dtype=torch.int32, device=dev)
+    y = torch.empty_like(x)
+    redop.check(ccl.allreduce(x, y, m, H.MPI_INT, H.MPI_SUM, cc, 'reduce_scatter_allgather'),
+                'MPIX_Allreduce')
+    if not allreduce_scalar(1 if bool(torch.all(y == x * world)) else 0, dist.ReduceOp.MIN, dev):
+        raise RuntimeError('allreduce fails the allred.c sum_test_1 closed form')
+    n = min(1 << 28, args.rsb_bytes // 4)          # 1 GiB per rank at the default size
+    send = torch.empty(n, dtype=torch.float32, device=dev)
+    fill_uniform(send, 0x5EED0200 + rank)
+    recv = torch.empty_like(send)
+    ws = torch.empty(n * 4, dtype=torch.uint8, device=dev)
+    res.update(parity_allred_sum_test_1_all_ranks=True, bytes_per_rank=n * 4, P=world)
+    for name, fn in (('c_reduce_scatter_allgather',
+                      lambda: redop.check(ccl.allreduce(send, recv, n, H.MPI_FLOAT, H.MPI_SUM, cc,
+                                                        'reduce_scatter_allgather', workspace=ws),
+                                          'MPIX_Allreduce')),
+                     ('rccl_all_reduce', lambda: (recv.copy_(send), dist.all_reduce(recv)))):
+        if name == 'rccl_all_reduce' and dist.get_backend() != 'nccl':
+            continue
+        fn()
+        reps = max(3, min(10, args.steps))
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        dist.barrier()
+        t = allreduce_scalar((time.perf_counter() - t0) / reps, dist.ReduceOp.MAX, dev)
+        res[name] = dict(ms=round(t * 1e3, 3),
+                         busbw_GBs=round(2 * (world - 1) / world * n * 4 / t / 1e9, 2))
+    del send, recv, ws
+    torch.cuda.empty_cache()
+
+
+_CCL = {}
 
 
 class _Emitter:
@@ -485,280 +722,88 @@ class _Emitter:
             r = dict(self.result)
             if note:
                 r['extras_watchdog'] = note
-                for k in ('reduce_scatter_block', 'allreduce'):
-                    part = dict(r.get(k) or {})
-                    part.setdefault('error', 'not finished: ' + note)
-                    r[k] = part
+                r.setdefault('error', 'secondary figures not finished: ' + note)
             print(json.dumps(r, default=str), flush=True)
 
 
 def _watchdog(seconds, emit):
+    """a hung secondary collective: rank 0 still prints the line (with the
+    headline), then every rank leaves with a NON-zero status so the hang
+    reads as a failure"""
     import threading
 
     def fire():
         emit.emit('secondary collectives exceeded %.0f s; headline kept, rank exits' % seconds)
         sys.stdout.flush()
         sys.stderr.flush()
-        os._exit(0)
+        os._exit(3)
     t = threading.Timer(seconds, fire)
     t.daemon = True
     t.start()
     return t
 
 
-def rsb_bench(args, world, rank, dev, out):
-    """BASELINE config 4: MPI_Reduce_scatter_block fp32 SUM, fixed vector per
-    rank (strong scaling): the reference's recursive-halving schedule and
-    the pairwise one over RCCL/xGMI (all links at once), and the fused
-    pull + combine kernel over hipIpc-mapped peer buffers."""
-    from mpich_amd import coll
-    if world == 1 or not dist.is_initialized():
-        out['note'] = 'P=1 is a local copy (coll_api.txt:402-411); see value for the combine'
-        return out
-    total = args.rsb_bytes // 4
-    recvcount = total // world
-    total = recvcount * world
-    send = torch.empty(total, dtype=torch.float32, device=dev)
-    fill_uniform(send, 0x5EED0100 + rank)
-    recv = torch.empty(recvcount, dtype=torch.float32, device=dev)
-    ws = (torch.empty(total * 4, dtype=torch.uint8, device=dev),
-          torch.empty(total * 4, dtype=torch.uint8, device=dev))
-    pof2 = 1
-    while pof2 * 2 <= world:
-        pof2 *= 2
-    p2p_ok = dist.get_backend() == 'nccl'     # the gloo rehearsal cannot move device tensors
-    for algo in ('recursive_halving', 'pairwise', 'pull'):
-        if algo != 'pull' and not p2p_ok:
-            out[algo] = dict(skipped='needs the nccl (RCCL) backend')
-            continue
-        try:
-            fn = coll.ALGORITHMS[algo]
-            kw = dict(extent=4)
-            if algo != 'pull':
-                kw['workspace'] = ws if algo == 'recursive_halving' else ws[0]
-            # parity first: redscatblk3.c:43-56 closed form (MPI_INT SUM), on device
-            rc_small = 4096 + 3
-            blk = torch.cat([torch.full((rc_small,), rank + i, dtype=torch.int32, device=dev)
-                             for i in range(world)])
-            o = torch.empty(rc_small, dtype=torch.int32, device=dev)
-            fn(blk, o, rc_small, H.MPI_INT, H.MPI_SUM, extent=4)
-            torch.cuda.synchronize()
-            ok = allreduce_scalar(1 if bool(torch.all(o == world * rank + world * (world - 1) // 2))
-                                  else 0, dist.ReduceOp.MIN, dev)
-
-            def once():
-                fn(send, recv, recvcount, H.MPI_FLOAT, H.MPI_SUM, **kw)
-            once()
-            reps = max(3, min(10, args.steps))
-            dist.barrier()
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for _ in range(reps):
-                once()
-            torch.cuda.synchronize()
-            dist.barrier()
-            t = (time.perf_counter() - t0) / reps
-            t = allreduce_scalar(t, dist.ReduceOp.MAX, dev)
-            busbytes = (world - 1) / world * total * 4
-            if algo == 'recursive_halving':
-                # bytes a rank receives over its one active link across the steps
-                link_bytes = (pof2 - 1) / pof2 * total * 4
-                links = 1
-            else:                                       # pairwise / pull: all links at once
-                link_bytes = total * 4 / world          # one block per peer link
-                links = world - 1
-            out[algo] = dict(parity_redscatblk3_all_ranks=bool(ok), ms=round(t * 1e3, 3),
-                             busbw_GBs=round(busbytes / t / 1e9, 2),
-                             per_link_GBs=round(link_bytes / t / 1e9, 2), links_active=links,
-                             frac_of_xgmi_link=round(link_bytes / t / 1e9 / 153.0, 4))
-            if algo == 'recursive_halving':
-                # per-step breakdown (SURVEY.md §8(d) C4), rank 0's stream
-                tl = []
-                dist.barrier()
-                fn(send, recv, recvcount, H.MPI_FLOAT, H.MPI_SUM, timer=tl, **kw)
-                torch.cuda.synchronize()
-                out[algo]['steps_rank0'] = tl[0].result()
-
-        except Exception as e:          # keep the other algorithms' figures
-            out[algo] = dict(error='%s: %s' % (type(e).__name__, e))
-    del ws
-    torch.cuda.empty_cache()
-    # the same schedules as C++ host code (libmpix_coll.so) on their own RCCL
-    # communicator: no Python between the steps
-    cc = ccl_comm() if p2p_ok else None
-    for algo in ('recursive_halving', 'pairwise', 'pairwise_pipelined'):
-        key = 'c_' + algo
-        if cc is None:
-            out[key] = dict(skipped='no RCCL communicator (%s)' % _CCL.get('error', 'gloo'))
-            continue
-        try:
-            from mpich_amd import ccl
-            rc_small = 4096 + 3
-            blk = torch.cat([torch.full((rc_small,), rank + i, dtype=torch.int32, device=dev)
-                             for i in range(world)])
-            o = torch.empty(rc_small, dtype=torch.int32, device=dev)
-            torch.cuda.synchronize()
-            redop.check(ccl.reduce_scatter_block(blk, o, rc_small, H.MPI_INT, H.MPI_SUM, cc, algo),
-                        'MPIX_Reduce_scatter_block')
-            ok = allreduce_scalar(1 if bool(torch.all(o == world * rank + world * (world - 1) // 2))
-                                  else 0, dist.ReduceOp.MIN, dev)
-
-            def once():
-                redop.check(ccl.reduce_scatter_block(send, recv, recvcount, H.MPI_FLOAT, H.MPI_SUM,
-                                                     cc, algo), 'MPIX_Reduce_scatter_block')
-            once()
-            reps = max(3, min(10, args.steps))
-            dist.barrier()
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for _ in range(reps):
-                once()
-            torch.cuda.synchronize()
-            dist.barrier()
-            t = (time.perf_counter() - t0) / reps
-            t = allreduce_scalar(t, dist.ReduceOp.MAX, dev)
-            busbytes = (world - 1) / world * total * 4
-            if algo == 'recursive_halving':
-                link_bytes, links = (pof2 - 1) / pof2 * total * 4, 1
-            else:
-                link_bytes, links = total * 4 / world, world - 1
-            out[key] = dict(parity_redscatblk3_all_ranks=bool(ok), ms=round(t * 1e3, 3),
-                            busbw_GBs=round(busbytes / t / 1e9, 2),
-                            per_link_GBs=round(link_bytes / t / 1e9, 2), links_active=links,
-                            frac_of_xgmi_link=round(link_bytes / t / 1e9 / 153.0, 4))
-        except Exception as e:
-            out[key] = dict(error='%s: %s' % (type(e).__name__, e))
-    del send, recv
-    torch.cuda.empty_cache()
-    out.update(P=world, bytes_per_rank=total * 4, recvcount=recvcount,
-               xgmi_link_GBs_assumed=153.0)
-    return out
-
-
-_CCL = {}
-
-
-def ccl_comm():
-    """one libmpix_coll RCCL communicator per process (MPIR_RCCLcomm_init,
-    rccl.c:21-52: rank 0's unique id broadcast over the process group).
-    Every rank always reaches the collective init, so a failure cannot leave
-    the others waiting in ncclCommInitRank."""
-    if 'comm' not in _CCL and 'error' not in _CCL:
-        try:
-            from mpich_amd import ccl
-            _CCL['comm'] = ccl.comm_create_ccl_from_process_group()
-        except Exception as e:
-            _CCL['error'] = '%s: %s' % (type(e).__name__, e)
-    return _CCL.get('comm')
-
-
-def allreduce_bench(args, world, rank, dev, res):
-    """MPI_Allreduce fp32 SUM, 1 GiB per rank: the reference's
-    reduce-scatter + allgather schedule on RCCL point-to-point + the HIP
-    combine (bit-identical to the reference association), next to RCCL's own
-    all_reduce (torch.distributed, ncclAllReduce -- the reference's
-    MPIR_Allreduce_intra_ccl route, rccl.c:223) as the comparator."""
-    from mpich_amd import coll
-    if world == 1 or not dist.is_initialized():
-        res['note'] = 'P=1 is a local copy'
-        return res
-    if dist.get_backend() != 'nccl':
-        res['skipped'] = 'needs the nccl (RCCL) backend'
-        return res
-    # parity: allred.c sum_test_1 closed form (in = i, sol = i*P), on device
-    m = 100003
-    x = torch.arange(m, dtype=torch.int32, device=dev)
-    y = torch.empty_like(x)
-    coll.allreduce(x, y, m, H.MPI_INT, H.MPI_SUM, extent=4)
-    torch.cuda.synchronize()
-    ok = allreduce_scalar(1 if bool(torch.all(y == x * world)) else 0, dist.ReduceOp.MIN, dev)
-    n = (1 << 30) // 4
-    send = torch.empty(n, dtype=torch.float32, device=dev)
-    fill_uniform(send, 0x5EED0200 + rank)
-    recv = torch.empty_like(send)
-    ws = torch.empty(n * 4, dtype=torch.uint8, device=dev)
-    res.update(parity_allred_sum_test_1_all_ranks=bool(ok), bytes_per_rank=n * 4, P=world)
-    for name, fn in (('mpich_schedule_hip_combine',
-                      lambda: coll.allreduce(send, recv, n, H.MPI_FLOAT, H.MPI_SUM, extent=4,
-                                             workspace=ws)),
-                     ('mpich_schedule_rd_allgather',
-                      lambda: coll.allreduce(send, recv, n, H.MPI_FLOAT, H.MPI_SUM, extent=4,
-                                             workspace=ws, allgather='recursive_doubling')),
-                     ('rccl_all_reduce', lambda: (recv.copy_(send), dist.all_reduce(recv)))):
-        fn()
-        reps = max(3, min(10, args.steps))
-        dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            fn()
-        torch.cuda.synchronize()
-        dist.barrier()
-        t = (time.perf_counter() - t0) / reps
-        t = allreduce_scalar(t, dist.ReduceOp.MAX, dev)
-        res[name] = dict(ms=round(t * 1e3, 3),
-                         busbw_GBs=round(2 * (world - 1) / world * n * 4 / t / 1e9, 2))
-    cc = ccl_comm()
-    if cc is None:
-        res['c_reduce_scatter_allgather'] = dict(skipped=_CCL.get('error', 'no communicator'))
+def main():
+    args = parse()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    # rehearsal knobs for a 1-GPU box (never set by the driver): every rank on
+    # device 0 and a gloo control plane + transport; RCCL refuses two ranks on
+    # one device (profiles/r01_rccl_probe.txt)
+    if os.environ.get('MPIX_BENCH_SAME_DEVICE') == '1':
+        local = 0
+    backend = os.environ.get('MPIX_BENCH_BACKEND', 'nccl')
+    if world > 1:
+        torch.cuda.set_device(local)
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        else:
+            dist.init_process_group(backend)
+    dev = torch.device('cuda', local)
+    torch.cuda.set_device(dev)
+    assert redop.lib().MPIX_Redop_init() == 0
+    if world == 1:
+        single_gpu(args, dev)
+        return 0
+    try:
+        result = multi_gpu(args, world, rank, dev)
+    except Exception as e:      # the value leg failed: say so at the top level, exit non-zero
+        if rank == 0:
+            print(json.dumps({'metric': METRIC_RSB, 'value': None, 'unit': 'GB/s', 'n_gpus': world,
+                              'error': '%s: %s' % (type(e).__name__, e)}), flush=True)
+        sys.stdout.flush()
+        os._exit(1)
+    emit = _Emitter(rank, result)
+    dog = _watchdog(args.extras_timeout, emit)
+    result['extras_timeout_s'] = args.extras_timeout
+    failed = None
+    if not args.no_extras:
+        for key, fn in (('reduce_scatter_block_other', rsb_secondary),
+                        ('allreduce', allreduce_secondary)):
+            part = result[key] = {}
+            try:
+                fn(args, world, rank, dev, part)
+            except Exception as e:
+                part['error'] = '%s: %s' % (type(e).__name__, e)
+                failed = '%s: %s' % (key, part['error'])
+                break       # the peers may be stuck in that leg: stop issuing collectives
+    if failed:
+        result['error'] = failed
+    emit.emit()
+    if failed:
+        sys.stdout.flush()
+        os._exit(1)
+    dist.barrier()
+    if dist.get_backend() == 'nccl':
+        _CCL.pop('comm').free()
     else:
-        from mpich_amd import ccl
-
-        def c_ar():
-            redop.check(ccl.allreduce(send, recv, n, H.MPI_FLOAT, H.MPI_SUM, cc,
-                                      'reduce_scatter_allgather', workspace=ws), 'MPIX_Allreduce')
-        try:
-            c_ar()
-            reps = max(3, min(10, args.steps))
-            dist.barrier()
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for _ in range(reps):
-                c_ar()
-            torch.cuda.synchronize()
-            dist.barrier()
-            t = (time.perf_counter() - t0) / reps
-            t = allreduce_scalar(t, dist.ReduceOp.MAX, dev)
-            res['c_reduce_scatter_allgather'] = dict(
-                ms=round(t * 1e3, 3), busbw_GBs=round(2 * (world - 1) / world * n * 4 / t / 1e9, 2))
-        except Exception as e:
-            res['c_reduce_scatter_allgather'] = dict(error='%s: %s' % (type(e).__name__, e))
-        # MPI_Reduce to rank 0 (reduce_scatter_gather, libmpix_coll over RCCL):
-        # reduce.c KAT first (in[i] = i on every rank, i*P at the root)
-        try:
-            m = 100003
-            x = torch.arange(m, dtype=torch.int32, device=dev)
-            y = torch.full_like(x, -1)
-            redop.check(ccl.reduce(x, y if rank == 0 else None, m, H.MPI_INT, H.MPI_SUM, 0, cc,
-                                   'reduce_scatter_gather'), 'MPIX_Reduce')
-            torch.cuda.synchronize()
-            ok = allreduce_scalar(1 if rank != 0 or bool(torch.all(y == x * world)) else 0,
-                                  dist.ReduceOp.MIN, dev)
-
-            def c_red():
-                redop.check(ccl.reduce(send, recv if rank == 0 else None, n, H.MPI_FLOAT,
-                                       H.MPI_SUM, 0, cc, 'reduce_scatter_gather'), 'MPIX_Reduce')
-            c_red()
-            reps = max(3, min(10, args.steps))
-            dist.barrier()
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for _ in range(reps):
-                c_red()
-            torch.cuda.synchronize()
-            dist.barrier()
-            t = (time.perf_counter() - t0) / reps
-            t = allreduce_scalar(t, dist.ReduceOp.MAX, dev)
-            res['c_reduce_to_root0'] = dict(
-                parity_reduce_c_all_ranks=bool(ok), ms=round(t * 1e3, 3),
-                busbw_GBs=round(n * 4 / t / 1e9, 2),   # nccl-tests: reduce busbw = algbw
-                algorithm='reduce_scatter_gather')
-        except Exception as e:
-            res['c_reduce_to_root0'] = dict(error='%s: %s' % (type(e).__name__, e))
-    del send, recv, ws
-    torch.cuda.empty_cache()
-    return res
+        from mpich_amd import coll
+        coll.free_comms()
+    dist.destroy_process_group()
+    dog.cancel()
+    return 0
 
 
 if __name__ == '__main__':
-    main()
+    sys.exit(main())

@@ -88,7 +88,17 @@ int MPIX_Comm_create_ccl(int rank, int size, const void *id, MPIX_Comm *comm);
  * NULL for the host-memory transport.  comms[r] is rank r's handle; each rank
  * must be driven by its own thread. */
 int MPIX_Comm_create_local(int size, const int *devices, MPIX_Comm *comms);
-int MPIX_Comm_create_custom(int rank, int size, MPIX_Exchange_fn fn, void *ctx, int host_memory,
+/* memory kinds of a custom communicator */
+#define MPIX_XPORT_DEVICE  0    /* device buffers; fn gets them as they are, stream-ordered */
+#define MPIX_XPORT_HOST    1    /* host buffers (schedule tests; needs MPIX_Comm_set_combine) */
+#define MPIX_XPORT_STAGED  2    /* device buffers, host transport: the library synchronises the
+                                   stream, copies the send data into pinned staging memory, calls
+                                   fn with HOST pointers (stream NULL) and copies what arrived
+                                   back to the device buffers on the stream -- the
+                                   MPIR_Coll_host_buffer_alloc / swap_back pattern
+                                   (coll_impl.c:305-381) for a transport that cannot touch GPU
+                                   memory (e.g. sockets, gloo) */
+int MPIX_Comm_create_custom(int rank, int size, MPIX_Exchange_fn fn, void *ctx, int memory_kind,
                             MPIX_Comm *comm);
 /* replace the combine (NULL restores MPIX_Reduce_local_async) */
 int MPIX_Comm_set_combine(MPIX_Comm comm, MPIX_Combine_fn fn);
@@ -112,6 +122,18 @@ int MPIX_Comm_free(MPIX_Comm comm);
                                            largest block each; below 8 MiB it is PAIRWISE):
                                            chunk k's combine, on a second stream, overlaps
                                            chunk k+1's group; same bits as PAIRWISE */
+#define MPIX_RSB_PULL               5   /* fused pull + combine: every rank maps
+                                           its peers' send buffers (hipIpc, as the reference's
+                                           GPU ipc path does, mpl_gpu_hip.c:174-204; ranks of a
+                                           local communicator share the address space) and ONE
+                                           multi-input kernel reads its block of all P-1 peers
+                                           over xGMI, folding them in the pairwise order: no
+                                           receive buffer, no copy, same bits as PAIRWISE.  A
+                                           barrier before (inputs complete) and after (peers done
+                                           reading).  Device buffers from hipMalloc; a host
+                                           communicator, or a buffer some rank cannot export,
+                                           runs PAIRWISE instead (same bits) */
+#define MPIX_RSB_LAST               MPIX_RSB_PULL
 size_t MPIX_Reduce_scatter_block_workspace(MPIX_Aint recvcount, MPIX_Datatype datatype,
                                            MPIX_Comm comm, int algorithm);
 int MPIX_Reduce_scatter_block(const void *sendbuf, void *recvbuf, MPIX_Aint recvcount,
@@ -191,6 +213,21 @@ int MPIX_Allreduce_async(const void *sendbuf, void *recvbuf, MPIX_Aint count,
 
 /* stream the blocking forms use: the communicator's own (NULL) by default */
 int MPIX_Comm_set_stream(MPIX_Comm comm, void *stream);
+
+/* Stream-ordered barrier: one 1-byte message to and from every peer on the
+ * transport (on RCCL the stream passes it only once every peer's stream has
+ * reached its own barrier). */
+int MPIX_Comm_barrier(MPIX_Comm comm);
+
+/* Per-step breakdown of the device schedules: with
+ * timing on, every exchange and combine step of the next collectives records
+ * a HIP event on the collective's stream; MPIX_Comm_step_times() (after the
+ * stream has completed) returns the device time between consecutive marks
+ * and the label of the step that ended at each (`labels` may be NULL; each
+ * label at most 32 bytes with its NUL) and clears the record.  Device
+ * communicators only. */
+int MPIX_Comm_set_step_timing(MPIX_Comm comm, int enable);
+int MPIX_Comm_step_times(MPIX_Comm comm, double *ms, char (*labels)[32], int max, int *n);
 
 #ifdef __cplusplus
 }

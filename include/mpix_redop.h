@@ -236,10 +236,33 @@ int MPIX_Ipc_export(const void *devptr, void *handle_out, MPIX_Aint *offset_out)
 int MPIX_Ipc_open(const void *handle, void **base_out);
 int MPIX_Ipc_close(void *base);
 
-/* 1 if (op, datatype) runs on the GPU path, else 0.  `count` is accepted
- * for signature parity and ignored (the reference passes 0 here too,
- * reduce_local.c:66-68).  When 0, a caller keeps its own CPU op table. */
+/* 1 if (op, datatype) goes to the GPU path, else 0 -- the contract of
+ * MPIR_Typerep_reduce_is_supported (typerep_yaksa_pack.c:227-271), which
+ * reduce_local.c:68 (count 0) and maint/gen_coll.py:546-547 (count of the
+ * collective) consult.  0 when the path is disabled (env MPIX_REDOP_ENABLE=0,
+ * as MPIR_CVAR_ENABLE_YAKSA_REDUCTION), when count > 0 and the packed size
+ * count * size exceeds the threshold (env MPIX_REDOP_THRESHOLD bytes, default
+ * -1 = no limit, as MPIR_CVAR_YAKSA_REDUCTION_THRESHOLD), or when no kernel
+ * covers the pair.  When 0, a caller keeps its own CPU op table. */
 int MPIX_Redop_is_supported(MPIX_Op op, MPIX_Aint count, MPIX_Datatype datatype);
+
+/* The same predicate with the operands in view, for reduce_local.c's branch:
+ * additionally 0 when BOTH buffers are host-resident and one operand holds
+ * fewer bytes than the host floor of its memory kind (pageable: env
+ * MPIX_REDOP_HOST_FLOOR, page-locked: MPIX_REDOP_PINNED_FLOOR), below which one
+ * core's op_fns.c loop beats the round trip over PCIe (crossover measured by
+ * bench.py, `host_crossover`).  A device-resident operand always answers as
+ * MPIX_Redop_is_supported does. */
+int MPIX_Redop_is_supported_buffers(MPIX_Op op, MPIX_Aint count, MPIX_Datatype datatype,
+                                    const void *inbuf, const void *inoutbuf);
+
+/* The predicate's knobs at run time (the env variables above set them at
+ * first use): enable 0/1, threshold (<= 0: none), the two host floors
+ * (<= 0: no floor). */
+int MPIX_Redop_set_support(int enable, MPIX_Aint threshold_bytes, MPIX_Aint host_floor_bytes,
+                           MPIX_Aint pinned_floor_bytes);
+int MPIX_Redop_get_support(int *enable, MPIX_Aint *threshold_bytes, MPIX_Aint *host_floor_bytes,
+                           MPIX_Aint *pinned_floor_bytes);
 
 /* Binding-level and internal legality of (op, datatype): 1 legal, 0 not. */
 int MPIX_Redop_op_dt_check(MPIX_Op op, MPIX_Datatype datatype);
@@ -260,9 +283,13 @@ MPIX_Aint MPIX_Datatype_size(MPIX_Datatype datatype);
 int MPIX_Redop_set_fortran_booleans(int true_value, int false_value);
 
 /* ---- per-op function table, MPIR_op_function signature (mpir_op.h:206) ----
- * Synchronous; same pointer rules as MPIX_Reduce_local.  The op functions
- * return void like the reference's; a failure is recorded and can be read
- * with MPIX_Redop_last_error() (the reference MPIR_Assert()s instead). */
+ * Synchronous; same pointer rules as MPIX_Reduce_local.  Only pairs that
+ * MPIX_Redop_is_supported() accepts may be passed: the op functions return
+ * void like the reference's, and a call that fails (a type no kernel covers,
+ * e.g. MPI_LONG_DOUBLE, or a HIP error) prints the reason and abort()s, as
+ * the reference's MPIR_Assert(0) does (op_fns.c:51-53).  With env
+ * MPIX_REDOP_OPFN_ABORT=0 the failure is only recorded and can be read with
+ * MPIX_Redop_last_error(). */
 typedef void MPIX_op_function(void *invec, void *inoutvec, MPIX_Aint *len,
                               MPIX_Datatype *type);
 extern MPIX_op_function *const MPIX_Op_table[16];

@@ -21,10 +21,11 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libmpix_col
 UNIQUE_ID_BYTES = 128
 
 RSB_AUTO, RSB_RECURSIVE_HALVING, RSB_PAIRWISE, RSB_PAIRWISE_SEQUENTIAL = 0, 1, 2, 3
-RSB_PAIRWISE_PIPELINED = 4
+RSB_PAIRWISE_PIPELINED, RSB_PULL = 4, 5
 RSB_ALGORITHMS = {'auto': RSB_AUTO, 'recursive_halving': RSB_RECURSIVE_HALVING,
                   'pairwise': RSB_PAIRWISE, 'pairwise_sequential': RSB_PAIRWISE_SEQUENTIAL,
-                  'pairwise_pipelined': RSB_PAIRWISE_PIPELINED}
+                  'pairwise_pipelined': RSB_PAIRWISE_PIPELINED, 'pull': RSB_PULL}
+XPORT_DEVICE, XPORT_HOST, XPORT_STAGED = 0, 1, 2
 AR_AUTO, AR_RECURSIVE_DOUBLING, AR_RSAG, AR_RSAG_RD, AR_RING = 0, 1, 2, 3, 4
 AR_ALGORITHMS = {'auto': AR_AUTO, 'recursive_doubling': AR_RECURSIVE_DOUBLING,
                  'reduce_scatter_allgather': AR_RSAG, 'rsag_rd_allgather': AR_RSAG_RD,
@@ -34,6 +35,16 @@ _lib = None
 
 COMBINE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ssize_t,
                               ctypes.c_int, ctypes.c_int, ctypes.c_void_p)
+
+
+class P2pOp(ctypes.Structure):
+    """MPIX_P2p_op"""
+    _fields_ = [('peer', ctypes.c_int), ('is_recv', ctypes.c_int), ('buf', ctypes.c_void_p),
+                ('bytes', ctypes.c_size_t)]
+
+
+EXCHANGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(P2pOp),
+                               ctypes.c_int, ctypes.c_void_p)
 
 
 def lib():
@@ -52,6 +63,10 @@ def lib():
             'MPIX_Comm_create_custom': ([i32, i32, vp, vp, i32, ctypes.POINTER(vp)], i32),
             'MPIX_Comm_set_combine': ([vp, vp], i32),
             'MPIX_Comm_set_stream': ([vp, vp], i32),
+            'MPIX_Comm_barrier': ([vp], i32),
+            'MPIX_Comm_set_step_timing': ([vp, i32], i32),
+            'MPIX_Comm_step_times': ([vp, ctypes.POINTER(ctypes.c_double), vp, i32,
+                                      ctypes.POINTER(i32)], i32),
             'MPIX_Comm_rank': ([vp, ctypes.POINTER(i32)], i32),
             'MPIX_Comm_size': ([vp, ctypes.POINTER(i32)], i32),
             'MPIX_Comm_free': ([vp], i32),
@@ -124,6 +139,25 @@ class Comm:
         redop.check(lib().MPIX_Comm_set_stream(self.h, None if stream is None else
                                                redop._stream_ptr(stream)), 'MPIX_Comm_set_stream')
 
+    def barrier(self):
+        redop.check(lib().MPIX_Comm_barrier(self.h), 'MPIX_Comm_barrier')
+
+    def set_step_timing(self, enable=True):
+        redop.check(lib().MPIX_Comm_set_step_timing(self.h, 1 if enable else 0),
+                    'MPIX_Comm_set_step_timing')
+
+    def step_times(self, max_steps=64):
+        """[{'phase': label, 'ms': t}] since timing was switched on (device
+        communicators; waits for the recorded events)"""
+        ms = (ctypes.c_double * max_steps)()
+        labels = ctypes.create_string_buffer(32 * max_steps)
+        n = ctypes.c_int()
+        redop.check(lib().MPIX_Comm_step_times(self.h, ms, labels, max_steps, ctypes.byref(n)),
+                    'MPIX_Comm_step_times')
+        raw = labels.raw
+        return [dict(phase=raw[32 * k:32 * (k + 1)].split(b'\0', 1)[0].decode(),
+                     ms=round(ms[k], 4)) for k in range(n.value)]
+
     def free(self):
         if self.h:
             rc = lib().MPIX_Comm_free(self.h)
@@ -156,6 +190,28 @@ def comm_create_ccl_from_process_group(group=None):
     dist.broadcast_object_list(obj, src=dist.get_global_rank(group, 0) if group else 0,
                                group=group)
     return comm_create_ccl(rank, size, obj[0])
+
+
+def comm_create_custom(rank, size, exchange, memory_kind=XPORT_DEVICE):
+    """communicator over a caller transport: `exchange(rank, ops)` gets a list
+    of (peer, is_recv, address, bytes) and moves them as one group (host
+    addresses for XPORT_HOST / XPORT_STAGED); it returns 0 on success"""
+    def tramp(ctx, r, ops, nops, stream):
+        try:
+            return int(exchange(r, [(ops[i].peer, ops[i].is_recv, ops[i].buf, ops[i].bytes)
+                                    for i in range(nops)]) or 0)
+        except Exception:           # never let an exception unwind through C
+            import traceback
+            traceback.print_exc()
+            return 1
+    cb = EXCHANGE_FN(tramp)
+    h = ctypes.c_void_p()
+    redop.check(lib().MPIX_Comm_create_custom(rank, size, ctypes.cast(cb, ctypes.c_void_p), None,
+                                               memory_kind, ctypes.byref(h)),
+                'MPIX_Comm_create_custom')
+    c = Comm(h.value)
+    c._keep.append(cb)
+    return c
 
 
 def comm_create_local(size, devices=None):

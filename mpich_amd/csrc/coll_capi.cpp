@@ -29,7 +29,9 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <string>
 #include <tuple>
+#include <utility>
 #include <vector>
 
 #include "mpix_coll.h"
@@ -87,6 +89,14 @@ struct MPIX_Comm_s {
     hipStream_t aux = nullptr;         // combine stream of the pipelined pairwise schedule
     std::vector<hipEvent_t> pipe_ev;   // its hand-off events (chunk k arrived, combines done)
     std::vector<uint64_t> send_seq, recv_seq;
+    int xkind = MPIX_XPORT_DEVICE;     // custom communicators: memory kind of the transport
+    char *stage = nullptr;             // MPIX_XPORT_STAGED: pinned staging of one exchange
+    size_t stage_bytes = 0;
+    hipEvent_t stage_ev = nullptr;     // recorded after the copies out of the staging memory
+    char *tok = nullptr;               // barrier tokens / published records, (1 + size) slots
+    std::map<std::string, void *> ipc_maps;    // peer allocations mapped by MPIX_RSB_PULL
+    bool timing = false;               // MPIX_Comm_set_step_timing
+    std::vector<std::pair<std::string, hipEvent_t>> marks;
     bool host() const { return kind == K_LOCAL_HOST || (kind == K_CUSTOM && device < 0); }
 };
 
@@ -234,6 +244,49 @@ int exchange_local(MPIX_Comm c, const MPIX_P2p_op *ops, int nops, hipStream_t s)
     return rc;
 }
 
+// MPIX_XPORT_STAGED: the transport only sees host memory, so the device
+// buffers are staged through one pinned area per exchange -- the pattern of
+// MPIR_Coll_host_buffer_alloc / swap_back (coll_impl.c:305-381).  The stream is
+// synchronised first (send data complete, and the previous exchange's copies
+// out of the staging area done), the transport runs on the host, and what
+// arrived goes back to the device buffers stream-ordered, ahead of the combine.
+int exchange_staged(MPIX_Comm c, const MPIX_P2p_op *ops, int nops, hipStream_t s)
+{
+    size_t total = 0;
+    for (int i = 0; i < nops; ++i)
+        total += round256(ops[i].bytes);
+    if (c->stage_ev)
+        HTRY(hipEventSynchronize(c->stage_ev));
+    else
+        HTRY(hipEventCreateWithFlags(&c->stage_ev, hipEventDisableTiming));
+    if (c->stage_bytes < total) {
+        if (c->stage)
+            HTRY(hipHostFree(c->stage));
+        c->stage = nullptr;
+        c->stage_bytes = 0;
+        void *h = nullptr;
+        HTRY(hipHostMalloc(&h, total, hipHostMallocDefault));
+        c->stage = static_cast<char *>(h);
+        c->stage_bytes = total;
+    }
+    std::vector<MPIX_P2p_op> h(ops, ops + nops);
+    size_t off = 0;
+    for (int i = 0; i < nops; ++i) {
+        h[i].buf = c->stage + off;
+        if (!ops[i].is_recv)
+            HTRY(hipMemcpyAsync(h[i].buf, ops[i].buf, ops[i].bytes, hipMemcpyDefault, s));
+        off += round256(ops[i].bytes);
+    }
+    HTRY(hipStreamSynchronize(s));
+    if (c->xfn(c->xctx, c->rank, h.data(), nops, nullptr))
+        return MPIX_REDOP_ERR_OTHER;
+    for (int i = 0; i < nops; ++i)
+        if (ops[i].is_recv)
+            HTRY(hipMemcpyAsync(ops[i].buf, h[i].buf, ops[i].bytes, hipMemcpyDefault, s));
+    HTRY(hipEventRecord(c->stage_ev, s));
+    return MPIX_REDOP_SUCCESS;
+}
+
 int exchange(MPIX_Comm c, const std::vector<MPIX_P2p_op> &ops, hipStream_t s)
 {
     // zero-length messages are not sent (both sides know the lengths, so
@@ -253,6 +306,8 @@ int exchange(MPIX_Comm c, const std::vector<MPIX_P2p_op> &ops, hipStream_t s)
         case K_LOCAL_HOST:
             return exchange_local(c, nz.data(), (int) nz.size(), s);
         default:
+            if (c->xkind == MPIX_XPORT_STAGED)
+                return exchange_staged(c, nz.data(), (int) nz.size(), s);
             return c->xfn(c->xctx, c->rank, nz.data(), (int) nz.size(), s) ? MPIX_REDOP_ERR_OTHER
                                                                            : MPIX_REDOP_SUCCESS;
     }
@@ -263,6 +318,83 @@ MPIX_P2p_op snd(int peer, const void *buf, size_t bytes)
     return MPIX_P2p_op{peer, 0, const_cast<void *>(buf), bytes};
 }
 MPIX_P2p_op rcv(int peer, void *buf, size_t bytes) { return MPIX_P2p_op{peer, 1, buf, bytes}; }
+
+// per-step breakdown (MPIX_Comm_set_step_timing): an event on the stream
+// after each phase of a schedule
+int mark(MPIX_Comm c, const char *label, hipStream_t s)
+{
+    if (!c->timing || c->host())
+        return MPIX_REDOP_SUCCESS;
+    hipEvent_t e;
+    HTRY(hipEventCreate(&e));
+    HTRY(hipEventRecord(e, s));
+    c->marks.emplace_back(label, e);
+    return MPIX_REDOP_SUCCESS;
+}
+
+// one published record per rank (barrier tokens are 1-byte records)
+constexpr size_t kRec = 128;
+
+int token_buffer(MPIX_Comm c)
+{
+    if (c->tok)
+        return MPIX_REDOP_SUCCESS;
+    const size_t bytes = kRec * (size_t) (c->size + 1);
+    if (c->host()) {
+        c->tok = static_cast<char *>(calloc(1, bytes));
+        return c->tok ? MPIX_REDOP_SUCCESS : MPIX_REDOP_ERR_OTHER;
+    }
+    void *p = nullptr;
+    HTRY(hipMalloc(&p, bytes));
+    HTRY(hipMemset(p, 0, bytes));
+    c->tok = static_cast<char *>(p);
+    return MPIX_REDOP_SUCCESS;
+}
+
+// every rank's `bytes` (<= kRec) of host data to every rank: one group of
+// P-1 sends and P-1 receives; out[q * kRec ...] holds rank q's (own included).
+// Synchronous: returns once the records are in host memory.
+int allgather_records(MPIX_Comm c, const void *mine, size_t bytes, std::vector<char> *out,
+                      hipStream_t s)
+{
+    TRY(token_buffer(c));
+    const int P = c->size;
+    out->assign(kRec * (size_t) P, 0);
+    std::vector<MPIX_P2p_op> ops;
+    for (int q = 0; q < P; ++q)
+        if (q != c->rank) {
+            ops.push_back(snd(q, c->tok, bytes));
+            ops.push_back(rcv(q, c->tok + kRec * (size_t) (1 + q), bytes));
+        }
+    if (c->host()) {
+        memcpy(c->tok, mine, bytes);
+        TRY(exchange(c, ops, s));
+        memcpy(out->data(), c->tok + kRec, kRec * (size_t) P);
+    } else {
+        HTRY(hipMemcpyAsync(c->tok, mine, bytes, hipMemcpyHostToDevice, s));
+        TRY(exchange(c, ops, s));
+        HTRY(hipMemcpyAsync(out->data(), c->tok + kRec, kRec * (size_t) P, hipMemcpyDeviceToHost,
+                            s));
+        HTRY(hipStreamSynchronize(s));
+    }
+    memcpy(out->data() + kRec * (size_t) c->rank, mine, bytes);
+    return MPIX_REDOP_SUCCESS;
+}
+
+// a 1-byte message to and from every peer, on the collective's stream
+int barrier(MPIX_Comm c, hipStream_t s)
+{
+    if (c->size == 1)
+        return MPIX_REDOP_SUCCESS;
+    TRY(token_buffer(c));
+    std::vector<MPIX_P2p_op> ops;
+    for (int q = 0; q < c->size; ++q)
+        if (q != c->rank) {
+            ops.push_back(snd(q, c->tok, 1));
+            ops.push_back(rcv(q, c->tok + kRec * (size_t) (1 + q), 1));
+        }
+    return exchange(c, ops, s);
+}
 
 // ------------------------------------------------------------ data movement
 int copy(MPIX_Comm c, void *dst, const void *src, size_t bytes, hipStream_t s)
@@ -373,6 +505,13 @@ int finish(MPIX_Comm c, int rc, hipStream_t s, bool blocking)
     return rc;
 }
 
+// MPIX_EQUAL compares whole packed buffers behind one 8-byte header
+// (opequal.c:20-35); MPIR_Reduce_equal / MPIR_Allreduce_equal run it only
+// through schedules that never split the message (binomial reduce, recursive
+// doubling allreduce), so the block-splitting schedules refuse it
+bool splits_message_forbidden(MPIX_Op op) { return ((uint32_t) op & 0xffu) == 0x0fu &&
+                                                   ((uint32_t) op >> 24) == 0x58u; }
+
 int check_args(MPIX_Comm c, const void *recvbuf, MPIX_Aint count, MPIX_Datatype dt, MPIX_Op op,
                size_t *ext)
 {
@@ -384,6 +523,13 @@ int check_args(MPIX_Comm c, const void *recvbuf, MPIX_Aint count, MPIX_Datatype 
         return MPIX_REDOP_ERR_OP;
     *ext = (size_t) MPIX_Datatype_extent(dt);
     if (!*ext)
+        return MPIX_REDOP_ERR_TYPE;
+    // a pair no kernel covers (MPI_LONG_DOUBLE, REAL16, ...) would only fail
+    // at its first combine, mid-schedule, with peers still posted to this
+    // rank: decline it here, before any exchange, so every rank returns the
+    // same error (the reference computes these on the CPU, which the caller
+    // keeps for them).  A custom combine takes whatever it is given.
+    if (!c->combine && !MPIX_Redop_is_supported(op, 0, dt))
         return MPIX_REDOP_ERR_TYPE;
     if (!recvbuf && count)
         return MPIX_REDOP_ERR_BUFFER;
@@ -408,7 +554,9 @@ int rs_recursive_halving(const char *sb, char *rb, const std::vector<size_t> &cn
         return MPIX_REDOP_SUCCESS;
     char *tmp_results = ws;
     char *tmp_recvbuf = ws + round256(total * ext);
+    TRY(mark(c, "start", s));
     TRY(copy(c, tmp_results, sb, total * ext, s));                         // :91-96
+    TRY(mark(c, "local copy", s));
     const int pof2 = pof2_of(size), rem = size - pof2;
     int newrank;
     if (rank < 2 * rem) {                                                   // :110-137
@@ -420,6 +568,7 @@ int rs_recursive_halving(const char *sb, char *rb, const std::vector<size_t> &cn
             TRY(combine(c, tmp_recvbuf, tmp_results, (MPIX_Aint) total, dt, op, s));
             newrank = rank / 2;
         }
+        TRY(mark(c, "prologue", s));
     } else {
         newrank = rank - rem;
     }
@@ -454,8 +603,10 @@ int rs_recursive_halving(const char *sb, char *rb, const std::vector<size_t> &cn
             // zero-length legs are skipped on both sides (:188-208)
             TRY(exchange(c, {snd(dst, tmp_results + newdisps[send_idx] * ext, send_cnt * ext),
                              rcv(dst, tmp_recvbuf + newdisps[recv_idx] * ext, recv_cnt * ext)}, s));
+            TRY(mark(c, "exchange", s));
             TRY(combine(c, tmp_recvbuf + newdisps[recv_idx] * ext,
                         tmp_results + newdisps[recv_idx] * ext, (MPIX_Aint) recv_cnt, dt, op, s));
+            TRY(mark(c, "combine", s));
             send_idx = recv_idx;
             last_idx = recv_idx + mask;
             mask >>= 1;
@@ -469,6 +620,7 @@ int rs_recursive_halving(const char *sb, char *rb, const std::vector<size_t> &cn
         else
             TRY(exchange(c, {rcv(rank + 1, rb, cnts[rank] * ext)}, s));
     }
+    TRY(mark(c, "epilogue", s));
     return MPIX_REDOP_SUCCESS;
 }
 
@@ -589,6 +741,135 @@ int rs_pairwise_pipelined(const char *sb, char *rb, const std::vector<size_t> &c
         if (disps[rank] * ext < blk) {
             TRY(copy(c, ws, acc, blk, s));
             TRY(copy(c, rb, ws, blk, s));
+        } else {
+            TRY(copy(c, rb, acc, blk, s));
+        }
+    }
+    return MPIX_REDOP_SUCCESS;
+}
+
+size_t rs_workspace(size_t total, size_t mine, size_t ext, int size, int algo);
+
+// What a rank publishes for MPIX_RSB_PULL: the buffer its peers read, as an
+// IPC handle + offset into its allocation (another process) or as the raw
+// address (a local communicator: the ranks share the address space).
+struct PullRec {
+    int32_t valid;
+    int32_t pad;
+    uint64_t raw;
+    int64_t offset;
+    char handle[sizeof(hipIpcMemHandle_t)];
+};
+static_assert(sizeof(PullRec) <= kRec, "pull record size");
+
+// the peer allocation behind `r`, mapped once and cached by handle (a
+// communicator holds at most kMaxMaps mappings; past that the cache is
+// dropped after the stream has drained the kernels that used them)
+int peer_base(MPIX_Comm c, const PullRec &r, hipStream_t s, const char **out)
+{
+    if (c->kind == K_LOCAL_DEV) {
+        *out = reinterpret_cast<const char *>(r.raw);
+        return MPIX_REDOP_SUCCESS;
+    }
+    constexpr size_t kMaxMaps = 64;
+    std::string key(r.handle, sizeof r.handle);
+    auto it = c->ipc_maps.find(key);
+    if (it == c->ipc_maps.end()) {
+        if (c->ipc_maps.size() >= kMaxMaps) {
+            HTRY(hipStreamSynchronize(s));
+            for (auto &m : c->ipc_maps)
+                (void) hipIpcCloseMemHandle(m.second);
+            c->ipc_maps.clear();
+        }
+        hipIpcMemHandle_t h;
+        memcpy(&h, r.handle, sizeof h);
+        void *base = nullptr;
+        HTRY(hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess));
+        it = c->ipc_maps.emplace(key, base).first;
+    }
+    *out = static_cast<const char *>(it->second) + r.offset;
+    return MPIX_REDOP_SUCCESS;
+}
+
+// MPIX_RSB_PULL: the pairwise schedule with the transport and the receive
+// buffers folded into the combine.  Every rank publishes the buffer holding
+// its inputs; after the stream has finished writing it (hipStreamSynchronize:
+// complete and visible to other devices) the records are all-gathered, which
+// is also the "inputs ready" barrier; ONE multi-input kernel then reads block
+// `rank` of every peer through the mappings in the order of
+// …_intra_pairwise.c:86-100 (i = 1..P-1, source rank - i), i.e. the bits of
+// PAIRWISE; a closing barrier on the stream keeps every rank from reusing its
+// buffer before all peers have pulled from it.
+int rs_pull(const char *sb, char *rb, const std::vector<size_t> &cnts, MPIX_Datatype dt, MPIX_Op op,
+            MPIX_Comm c, hipStream_t s, size_t ext)
+{
+    const int rank = c->rank, size = c->size;
+    std::vector<size_t> disps(size, 0);
+    for (int i = 1; i < size; ++i)
+        disps[i] = disps[i - 1] + cnts[i - 1];
+    size_t total = 0;
+    for (size_t n : cnts)
+        total += n;
+    auto fallback = [&]() -> int {     // same bits: the one-group pairwise schedule
+        char *w;
+        TRY(workspace(c, nullptr, 0, rs_workspace(total, cnts[rank], ext, size, MPIX_RSB_PAIRWISE),
+                      s, &w));
+        return release_scratch(c, w, rs_pairwise(sb, rb, cnts, dt, op, c, w, s, ext, true), s);
+    };
+    if (c->host() || c->combine)
+        return fallback();
+    const size_t blk = cnts[rank] * ext;
+    const bool in_place = sb == rb;
+    char *acc = in_place ? rb + disps[rank] * ext : rb;
+    if (!in_place)
+        TRY(copy(c, rb, sb + disps[rank] * ext, blk, s));                   // :58-64
+    PullRec me;
+    memset(&me, 0, sizeof me);
+    me.raw = reinterpret_cast<uint64_t>(sb);
+    me.valid = 1;
+    if (c->kind != K_LOCAL_DEV) {
+        hipDeviceptr_t base = nullptr;
+        size_t bytes = 0;
+        hipIpcMemHandle_t h;
+        if (hipMemGetAddressRange(&base, &bytes, (hipDeviceptr_t) sb) != hipSuccess ||
+            hipIpcGetMemHandle(&h, (void *) base) != hipSuccess) {
+            (void) hipGetLastError();
+            me.valid = 0;       // every rank sees it and takes the fallback
+        } else {
+            memcpy(me.handle, &h, sizeof h);
+            me.offset = (int64_t) (sb - static_cast<const char *>((void *) base));
+        }
+    }
+    HTRY(hipStreamSynchronize(s));      // this rank's inputs complete before anyone reads them
+    std::vector<char> all;
+    TRY(allgather_records(c, &me, sizeof me, &all, s));
+    std::vector<PullRec> recs(size);
+    bool ok = true;
+    for (int q = 0; q < size; ++q) {
+        memcpy(&recs[q], all.data() + kRec * (size_t) q, sizeof(PullRec));
+        ok &= recs[q].valid == 1;
+    }
+    if (!ok)
+        return fallback();
+    std::vector<const void *> ins;
+    for (int i = 1; i < size; ++i) {
+        const int src = (rank - i + size) % size;
+        const char *base;
+        TRY(peer_base(c, recs[src], s, &base));
+        ins.push_back(base + disps[rank] * ext);
+    }
+    TRY(mark(c, "publish", s));
+    if (cnts[rank])
+        TRY(combine_multi(c, ins, acc, (MPIX_Aint) cnts[rank], dt, op, s));
+    TRY(mark(c, "pull+combine", s));
+    TRY(barrier(c, s));                 // peers done reading this rank's buffer
+    if (in_place && rank != 0) {
+        if (disps[rank] * ext < blk) {
+            char *w;
+            TRY(scratch(c, round256(blk), s, &w));
+            TRY(copy(c, w, acc, blk, s));
+            TRY(copy(c, rb, w, blk, s));
+            TRY(release_scratch(c, w, MPIX_REDOP_SUCCESS, s));
         } else {
             TRY(copy(c, rb, acc, blk, s));
         }
@@ -1018,9 +1299,13 @@ int reduce_entry(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Datat
         return MPIX_REDOP_ERR_BUFFER;
     const int pof2 = pof2_of(c->size);
     const size_t nb = (size_t) count * ext;
+    if (algorithm == MPIX_REDUCE_AUTO && splits_message_forbidden(op))
+        algorithm = MPIX_REDUCE_BINOMIAL;       // MPIR_Reduce_equal: binomial only
     if (algorithm == MPIX_REDUCE_AUTO)  // generic.json:206-250 (intra, builtin op)
         algorithm = (nb <= 2048 || (size_t) count < (size_t) pof2) ? MPIX_REDUCE_BINOMIAL
                                                                    : MPIX_REDUCE_SCATTER_GATHER;
+    if (algorithm == MPIX_REDUCE_SCATTER_GATHER && splits_message_forbidden(op))
+        return MPIX_REDOP_ERR_OP;
     if (algorithm == MPIX_REDUCE_SCATTER_GATHER && (size_t) count < (size_t) pof2)
         return MPIX_REDOP_ERR_COUNT;    // the reference asserts count >= pof2 (:86)
     TRY(set_device(c));
@@ -1093,8 +1378,10 @@ int rs_entry(const void *sendbuf, void *recvbuf, const std::vector<size_t> &cnts
     for (size_t n : cnts)
         total += n;
     TRY(check_args(c, recvbuf, (MPIX_Aint) cnts[c->rank], dt, op, &ext));
-    if (algorithm < MPIX_RSB_AUTO || algorithm > MPIX_RSB_PAIRWISE_PIPELINED)
+    if (algorithm < MPIX_RSB_AUTO || algorithm > MPIX_RSB_LAST)
         return MPIX_REDOP_ERR_ARG;
+    if (splits_message_forbidden(op))
+        return MPIX_REDOP_ERR_OP;
     if (!total)
         return MPIX_REDOP_SUCCESS;
     if (!recvbuf && !sendbuf)
@@ -1109,6 +1396,8 @@ int rs_entry(const void *sendbuf, void *recvbuf, const std::vector<size_t> &cnts
                       blocking);
     char *w;
     TRY(workspace(c, ws, ws_bytes, rs_workspace(total, cnts[c->rank], ext, c->size, algo), s, &w));
+    if (algo == MPIX_RSB_PULL)
+        return finish(c, rs_pull(sb, rb, cnts, dt, op, c, s, ext), s, blocking);
     int rc = algo == MPIX_RSB_RECURSIVE_HALVING
                  ? rs_recursive_halving(sb, rb, cnts, dt, op, c, w, s, ext)
                  : algo == MPIX_RSB_PAIRWISE_PIPELINED
@@ -1159,12 +1448,14 @@ int allreduce_entry(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Da
     const size_t nb = (size_t) count * ext;
     const int pof2 = pof2_of(c->size);
     if (algorithm == MPIX_ALLREDUCE_AUTO)       // generic.json:99-135 (builtin ops)
-        algorithm = (nb > 8 && (size_t) count >= (size_t) pof2)
+        algorithm = (nb > 8 && (size_t) count >= (size_t) pof2 && !splits_message_forbidden(op))
                         ? MPIX_ALLREDUCE_REDUCE_SCATTER_ALLGATHER
                         : MPIX_ALLREDUCE_RECURSIVE_DOUBLING;
     if ((algorithm == MPIX_ALLREDUCE_REDUCE_SCATTER_ALLGATHER ||
          algorithm == MPIX_ALLREDUCE_RSAG_RD_ALLGATHER) && (size_t) count < (size_t) pof2)
         return MPIX_REDOP_ERR_COUNT;    // :127
+    if (algorithm != MPIX_ALLREDUCE_RECURSIVE_DOUBLING && splits_message_forbidden(op))
+        return MPIX_REDOP_ERR_OP;       // MPIR_Allreduce_equal uses recursive doubling only
     if (sendbuf)
         TRY(copy(c, rb, sendbuf, nb, s));
     if (c->size == 1)
@@ -1267,15 +1558,17 @@ int MPIX_Comm_create_local(int size, const int *devices, MPIX_Comm *comms)
     return MPIX_REDOP_SUCCESS;
 }
 
-int MPIX_Comm_create_custom(int rank, int size, MPIX_Exchange_fn fn, void *ctx, int host_memory,
+int MPIX_Comm_create_custom(int rank, int size, MPIX_Exchange_fn fn, void *ctx, int memory_kind,
                             MPIX_Comm *comm)
 {
-    if (!comm || !fn || size < 1 || rank < 0 || rank >= size)
+    if (!comm || !fn || size < 1 || rank < 0 || rank >= size || memory_kind < MPIX_XPORT_DEVICE ||
+        memory_kind > MPIX_XPORT_STAGED)
         return MPIX_REDOP_ERR_ARG;
     MPIX_Comm c = new_comm(rank, size, K_CUSTOM);
     c->xfn = fn;
     c->xctx = ctx;
-    if (!host_memory) {
+    c->xkind = memory_kind;
+    if (memory_kind != MPIX_XPORT_HOST) {
         int dev;
         if (hipGetDevice(&dev) != hipSuccess) {
             delete c;
@@ -1306,6 +1599,50 @@ int MPIX_Comm_set_stream(MPIX_Comm comm, void *stream)
         return MPIX_REDOP_ERR_ARG;
     comm->stream = stream;
     return MPIX_REDOP_SUCCESS;
+}
+
+int MPIX_Comm_barrier(MPIX_Comm comm)
+{
+    if (!comm)
+        return MPIX_REDOP_ERR_ARG;
+    TRY(set_device(comm));
+    hipStream_t s = stream_of(comm->stream ? comm->stream : comm->own_stream);
+    return finish(comm, barrier(comm, s), s, true);
+}
+
+int MPIX_Comm_set_step_timing(MPIX_Comm comm, int enable)
+{
+    if (!comm)
+        return MPIX_REDOP_ERR_ARG;
+    comm->timing = enable != 0;
+    return MPIX_REDOP_SUCCESS;
+}
+
+int MPIX_Comm_step_times(MPIX_Comm comm, double *ms, char (*labels)[32], int max, int *n)
+{
+    if (!comm || !n || max < 0 || (max && !ms))
+        return MPIX_REDOP_ERR_ARG;
+    *n = 0;
+    int rc = MPIX_REDOP_SUCCESS;
+    if (!comm->marks.empty() && hipEventSynchronize(comm->marks.back().second) != hipSuccess)
+        rc = MPIX_REDOP_ERR_OTHER;
+    for (size_t k = 1; k < comm->marks.size() && rc == MPIX_REDOP_SUCCESS && *n < max; ++k) {
+        float t = 0.f;
+        if (hipEventElapsedTime(&t, comm->marks[k - 1].second, comm->marks[k].second) != hipSuccess) {
+            rc = MPIX_REDOP_ERR_OTHER;
+            break;
+        }
+        ms[*n] = t;
+        if (labels) {
+            strncpy(labels[*n], comm->marks[k].first.c_str(), 31);
+            labels[*n][31] = 0;
+        }
+        ++*n;
+    }
+    for (auto &m : comm->marks)
+        (void) hipEventDestroy(m.second);
+    comm->marks.clear();
+    return rc;
 }
 
 int MPIX_Comm_rank(MPIX_Comm comm, int *rank)
@@ -1349,8 +1686,21 @@ int MPIX_Comm_free(MPIX_Comm comm)
         }
         for (hipEvent_t e : comm->pipe_ev)
             (void) hipEventDestroy(e);
+        if (comm->stage_ev) {
+            (void) hipEventSynchronize(comm->stage_ev);
+            (void) hipEventDestroy(comm->stage_ev);
+        }
+        if (comm->stage)
+            (void) hipHostFree(comm->stage);
+        if (comm->tok)
+            (void) hipFree(comm->tok);
+        for (auto &m : comm->ipc_maps)
+            (void) hipIpcCloseMemHandle(m.second);
+        for (auto &m : comm->marks)
+            (void) hipEventDestroy(m.second);
     } else {
         free(comm->scratch);
+        free(comm->tok);
     }
     if (comm->nccl && ncclCommDestroy(comm->nccl) != ncclSuccess)         // rccl.c:237-250
         rc = MPIX_REDOP_ERR_OTHER;

@@ -259,6 +259,24 @@ size_t g_bounce_bytes = (size_t) 1 << 20;
 // and staging is faster (profiles/r01_pageable_sweep.txt)
 std::atomic<int> g_pipe_threads{8};
 std::atomic<size_t> g_pipe_chunk{(size_t) 16 << 20};
+// Support-predicate knobs, the pattern of MPIR_CVAR_ENABLE_YAKSA_REDUCTION and
+// MPIR_CVAR_YAKSA_REDUCTION_THRESHOLD (typerep_yaksa_pack.c:44-64,229-240):
+// MPIX_REDOP_ENABLE=0 makes every predicate answer 0 (the caller keeps its CPU
+// op table); MPIX_REDOP_THRESHOLD > 0 declines calls whose packed size
+// (count * type size) exceeds it (default -1, no limit).  The pointer-aware
+// predicate also declines operands that are BOTH host-resident below a floor
+// (MPIX_REDOP_HOST_FLOOR for pageable memory, MPIX_REDOP_PINNED_FLOOR for
+// page-locked memory, bytes per operand): there one core's op_fns.c loop beats
+// the PCIe round trip (crossover measured by bench.py's host_crossover leg).
+std::atomic<bool> g_enable{true};
+std::atomic<long long> g_threshold{-1};
+std::atomic<long long> g_host_floor{(long long) 1 << 30};
+std::atomic<long long> g_pinned_floor{(long long) 64 << 20};
+// MPIX_Op_table entries return void, like MPIR_op_function: a call the GPU
+// path declines aborts by default, as op_fns.c's MPIR_Assert(0) does
+// (op_fns.c:51-53); MPIX_REDOP_OPFN_ABORT=0 only records the error
+// (MPIX_Redop_last_error)
+std::atomic<bool> g_opfn_abort{true};
 
 void read_env()
 {
@@ -291,6 +309,16 @@ void read_env()
         if (c >= 65536 && c <= (256ll << 20))
             g_pipe_chunk = (size_t) c;
     }
+    if (const char *s = getenv("MPIX_REDOP_ENABLE"))
+        g_enable = atoi(s) != 0;
+    if (const char *s = getenv("MPIX_REDOP_THRESHOLD"))
+        g_threshold = atoll(s);
+    if (const char *s = getenv("MPIX_REDOP_HOST_FLOOR"))
+        g_host_floor = atoll(s);
+    if (const char *s = getenv("MPIX_REDOP_PINNED_FLOOR"))
+        g_pinned_floor = atoll(s);
+    if (const char *s = getenv("MPIX_REDOP_OPFN_ABORT"))
+        g_opfn_abort = atoi(s) != 0;
     if (const char *s = getenv("MPIX_REDOP_BOUNCE_BYTES")) {
         long long c = atoll(s);
         if (c >= 0 && c <= (64ll << 20))
@@ -411,6 +439,28 @@ LaunchCfg launch_cfg()
 
 Params params() { return Params{g_ftrue.load(), g_ffalse.load()}; }
 
+// Spin until the pinned completion word holds `seq`.  The stream is queried
+// every 4096 spins once 20 ms have passed (a query inside a short spin costs
+// latency): an idle stream means the work and the word's store are done; a
+// stream in an error state (a faulted kernel) ends the wait with that error
+// instead of spinning forever.
+int spin_on_flag(DevState *d, hipStream_t s, uint32_t seq)
+{
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spins = 1; __atomic_load_n(d->flag, __ATOMIC_ACQUIRE) != seq; ++spins) {
+        if ((spins & 0xfff) != 0 ||
+            std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(20))
+            continue;
+        hipError_t q = hipStreamQuery(s);
+        if (q == hipErrorNotReady)
+            continue;
+        if (q == hipSuccess)
+            return MPIX_REDOP_SUCCESS;
+        return hip_err(q);
+    }
+    return MPIX_REDOP_SUCCESS;
+}
+
 // Completion wait of the synchronous entry points.  MPI progress engines
 // poll; a blocking hipStreamSynchronize costs wake-up latency per call, and an
 // event query goes through the runtime's signal path, so by default the
@@ -427,9 +477,7 @@ int wait_stream(DevState *d, hipStream_t s)
         e = hipStreamWriteValue32(s, (void *) d->flag, seq, 0);
         if (e != hipSuccess)
             return hip_err(e);
-        while (__atomic_load_n(d->flag, __ATOMIC_ACQUIRE) != seq) {
-        }
-        return MPIX_REDOP_SUCCESS;
+        return spin_on_flag(d, s, seq);
     }
     e = hipEventRecord(d->done, s);
     if (e != hipSuccess)
@@ -559,18 +607,8 @@ int run_sync(DevState *d, const void *in, void *io, uint64_t count, uint32_t it,
         bool signalled = false;
         int rc = enqueue(in, io, count, it, ext, op, d->s[0], (uint32_t *) d->flag, d->flag_ctr,
                          seq, &signalled);
-        if (signalled) {
-            // an idle stream also means done, so the wait cannot outlive the
-            // kernel even if the word were never stored; the stream is only
-            // queried after 20 ms (a query inside the spin costs latency)
-            const auto t0 = std::chrono::steady_clock::now();
-            for (uint32_t spins = 1; __atomic_load_n(d->flag, __ATOMIC_ACQUIRE) != seq; ++spins)
-                if ((spins & 0xfff) == 0 &&
-                    std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20) &&
-                    hipStreamQuery(d->s[0]) == hipSuccess)
-                    break;
-            return MPIX_REDOP_SUCCESS;
-        }
+        if (signalled)      // the kernel stores the word itself
+            return spin_on_flag(d, d->s[0], seq);
         int rc2 = wait_stream(d, d->s[0]);
         return rc ? rc : rc2;
     }
@@ -630,6 +668,51 @@ int staged(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext, 
     int rc2 = wait_stream(d, d->s[0]);
     int rc3 = wait_stream(d, d->s[1]);
     return rc ? rc : (rc2 ? rc2 : rc3);
+}
+
+// MPIX_EQUAL with host-resident operand(s) too large for the bounce buffer:
+// whole-buffer copies into device scratch, ONE k_equal launch, and the 8-byte
+// is_equal header back (k_equal writes nothing else).  When the scratch
+// cannot be had nothing has been touched and MPI_ERR_TYPE sends the caller to
+// its own op table.
+int equal_whole(const void *in, void *io, uint64_t n, bool in_host, bool io_host, int dev)
+{
+    DevState *d = dev_state(dev);
+    if (!d)
+        return MPIX_REDOP_ERR_OTHER;
+    const size_t half = ((size_t) n + 255) & ~(size_t) 255;
+    if (d->scratch_bytes < 2 * half) {
+        if (d->scratch) {
+            (void) hipStreamSynchronize(d->s[0]);
+            (void) hipStreamSynchronize(d->s[1]);
+            (void) hipFree(d->scratch);
+        }
+        d->scratch = nullptr;
+        d->scratch_bytes = 0;
+        if (hipMalloc(&d->scratch, 2 * half) != hipSuccess) {
+            (void) hipGetLastError();
+            return MPIX_REDOP_ERR_TYPE;
+        }
+        d->scratch_bytes = 2 * half;
+    }
+    hipStream_t s = d->s[0];
+    const void *kin = in;
+    void *kio = io;
+    int rc = MPIX_REDOP_SUCCESS;
+    if (in_host) {
+        rc = hip_err(hipMemcpyAsync(d->scratch, in, n, hipMemcpyHostToDevice, s));
+        kin = d->scratch;
+    }
+    if (rc == MPIX_REDOP_SUCCESS && io_host) {
+        kio = (char *) d->scratch + half;
+        rc = hip_err(hipMemcpyAsync(kio, io, n, hipMemcpyHostToDevice, s));
+    }
+    if (rc == MPIX_REDOP_SUCCESS)
+        rc = hip_err(mpix::launch_equal(kin, kio, n, s));
+    if (rc == MPIX_REDOP_SUCCESS && io_host)
+        rc = hip_err(hipMemcpyAsync(io, kio, 8, hipMemcpyDeviceToHost, s));
+    int rc2 = wait_stream(d, s);
+    return rc ? rc : rc2;
 }
 
 // Small pageable operand(s): memcpy into the pinned bounce buffer, one
@@ -1041,6 +1124,12 @@ int MPIX_Reduce_local(const void *inbuf, void *inoutbuf, MPIX_Aint count, MPIX_D
         if (rc >= 0)
             return set_err(rc);
     }
+    if (opi == 15 && (in_stage || io_stage))
+        // MPIX_EQUAL is one comparison over the whole buffer behind one
+        // 8-byte header (opequal.c:20-35; MPIR_Reduce_equal: "we can't split
+        // the message"), so it is never chunked
+        return set_err(equal_whole(in_stage ? inbuf : pin, io_stage ? inoutbuf : (void *) pio,
+                                   (uint64_t) count, in_stage, io_stage, dev));
     const int pipe_threads = g_pipe_threads.load();
     if (pageable && zc && pipe_threads > 0 &&
         (uint64_t) count * ext >= 2 * (uint64_t) pipe_threads * g_pipe_chunk.load()) {
@@ -1277,18 +1366,83 @@ int MPIX_Ipc_close(void *base)
     return set_err(hip_err(hipIpcCloseMemHandle(base)));
 }
 
-int MPIX_Redop_is_supported(MPIX_Op op, MPIX_Aint count, MPIX_Datatype datatype)
+// the (op, type) half of the predicate: a kernel exists (knob-independent)
+static int has_gpu_path(uint32_t op, uint32_t it)
 {
-    (void) count;
-    uint32_t it = to_internal((uint32_t) datatype);
-    if (it == kNull || extent_of(it) == 0 || !internal_ok((uint32_t) op, it))
+    if (it == kNull || extent_of(it) == 0 || !internal_ok(op, it))
         return 0;
-    uint32_t opi = (uint32_t) op & 0xf;
+    uint32_t opi = op & 0xf;
     if (opi == 13 || opi == 14)
         return 1;
     if (opi == 15)
         return (it & 0xffffff00u) == U8;
     return gpu_entry(opi, it) ? 1 : 0;
+}
+
+// MPIR_Typerep_reduce_is_supported (typerep_yaksa_pack.c:227-271): the enable
+// knob, the size threshold on the packed size for count > 0 (count 0, as
+// reduce_local.c:68 passes it, only asks about the pair), then the pair
+int MPIX_Redop_is_supported(MPIX_Op op, MPIX_Aint count, MPIX_Datatype datatype)
+{
+    launch_cfg();
+    if (!g_enable.load())
+        return 0;
+    uint32_t it = to_internal((uint32_t) datatype);
+    if (count > 0) {
+        const long long thr = g_threshold.load();
+        const uint64_t sz = size_of(it);
+        if (thr > 0 && sz && (uint64_t) count > (uint64_t) thr / sz)
+            return 0;
+    }
+    return has_gpu_path((uint32_t) op, it);
+}
+
+// The same with the operands in view: both host-resident below the floor of
+// their memory kind -> 0, MPICH keeps its op_fns.c loop for the chunk.  A
+// device operand always goes to the GPU (the CPU could only reach it through
+// two PCIe copies).
+int MPIX_Redop_is_supported_buffers(MPIX_Op op, MPIX_Aint count, MPIX_Datatype datatype,
+                                    const void *inbuf, const void *inoutbuf)
+{
+    if (!MPIX_Redop_is_supported(op, count, datatype))
+        return 0;
+    if (count <= 0 || !inbuf || !inoutbuf)
+        return 1;
+    int d0 = 0, d1 = 0;
+    const void *p0, *p1;
+    const Where w0 = classify(inbuf, &d0, &p0), w1 = classify(inoutbuf, &d1, &p1);
+    if (w0 == Where::Device || w1 == Where::Device)
+        return 1;
+    const long long floor_bytes = (w0 == Where::Pageable || w1 == Where::Pageable)
+                                      ? g_host_floor.load() : g_pinned_floor.load();
+    const uint64_t bytes = (uint64_t) count * extent_of(to_internal((uint32_t) datatype));
+    return (floor_bytes > 0 && bytes < (uint64_t) floor_bytes) ? 0 : 1;
+}
+
+int MPIX_Redop_set_support(int enable, MPIX_Aint threshold_bytes, MPIX_Aint host_floor_bytes,
+                           MPIX_Aint pinned_floor_bytes)
+{
+    launch_cfg();
+    g_enable = enable != 0;
+    g_threshold = (long long) threshold_bytes;
+    g_host_floor = (long long) host_floor_bytes;
+    g_pinned_floor = (long long) pinned_floor_bytes;
+    return MPIX_REDOP_SUCCESS;
+}
+
+int MPIX_Redop_get_support(int *enable, MPIX_Aint *threshold_bytes, MPIX_Aint *host_floor_bytes,
+                           MPIX_Aint *pinned_floor_bytes)
+{
+    launch_cfg();
+    if (enable)
+        *enable = g_enable.load() ? 1 : 0;
+    if (threshold_bytes)
+        *threshold_bytes = (MPIX_Aint) g_threshold.load();
+    if (host_floor_bytes)
+        *host_floor_bytes = (MPIX_Aint) g_host_floor.load();
+    if (pinned_floor_bytes)
+        *pinned_floor_bytes = (MPIX_Aint) g_pinned_floor.load();
+    return MPIX_REDOP_SUCCESS;
 }
 
 int MPIX_Redop_op_dt_check(MPIX_Op op, MPIX_Datatype datatype)
@@ -1389,10 +1543,26 @@ const char *MPIX_Redop_build_info(void)
 }
 
 // ------------------------------------------------ MPIR_op_function table
+// A failed call is fatal, like the reference's MPIR_Assert(0) on a type its
+// op function does not cover (op_fns.c:51-53), unless MPIX_REDOP_OPFN_ABORT=0:
+// then the error class is only recorded for MPIX_Redop_last_error().
+static void opfn_failed(const char *name, int rc, MPIX_Datatype type)
+{
+    if (!g_opfn_abort.load())
+        return;
+    fprintf(stderr, "MPIX_Op_table: %s on datatype 0x%08x failed: %s (MPI error class %d); "
+                    "only pairs MPIX_Redop_is_supported() accepts may use the table\n",
+            name, (unsigned) type, MPIX_Redop_error_string(rc), rc);
+    fflush(stderr);
+    abort();
+}
 #define MPIX_OPFN(name, handle)                                                           \
     void name(void *invec, void *inoutvec, MPIX_Aint *len, MPIX_Datatype *type)           \
     {                                                                                     \
-        (void) MPIX_Reduce_local(invec, inoutvec, *len, *type, handle);                  \
+        launch_cfg();                                                                     \
+        int rc_ = MPIX_Reduce_local(invec, inoutvec, *len, *type, handle);               \
+        if (rc_ != MPIX_REDOP_SUCCESS)                                                    \
+            opfn_failed(#name, rc_, *type);                                               \
     }
 MPIX_OPFN(MPIX_MAXF, MPIX_MAX)
 MPIX_OPFN(MPIX_MINF, MPIX_MIN)

@@ -53,6 +53,9 @@ def lib():
             'MPIX_Reduce_local_iovec_async': ([vp, vp, aint, ctypes.POINTER(aint),
                                                ctypes.POINTER(aint), i32, i32, vp], i32),
             'MPIX_Redop_is_supported': ([i32, aint, i32], i32),
+            'MPIX_Redop_is_supported_buffers': ([i32, aint, i32, vp, vp], i32),
+            'MPIX_Redop_set_support': ([i32, aint, aint, aint], i32),
+            'MPIX_Redop_get_support': ([ctypes.POINTER(i32)] + [ctypes.POINTER(aint)] * 3, i32),
             'MPIX_Ipc_export': ([vp, vp, ctypes.POINTER(aint)], i32),
             'MPIX_Ipc_open': ([vp, ctypes.POINTER(vp)], i32),
             'MPIX_Ipc_close': ([vp], i32),
@@ -117,7 +120,9 @@ def _checked_extent(op, datatype):
     if ext is None:
         cop, cdt = H.as_c_int(op), H.as_c_int(datatype)
         ext = 0
-        if lib().MPIX_Redop_is_supported(cop, 1, cdt):
+        # the pair itself, whatever the enable / threshold knobs say: the
+        # span check guards every call the kernels would run
+        if lib().MPIX_Redop_op_dt_check(cop, cdt) or lib().MPIX_Redop_internal_op_dt_check(cop, cdt):
             ext = max(0, lib().MPIX_Datatype_extent(cdt))
         _extent_cache[key] = ext
     return ext
@@ -138,6 +143,33 @@ def _span_check(count, datatype, op, *bufs):
         if nb is not None and nb < count * ext:
             raise ValueError('buffer of %d bytes is too small for %d elements of extent %d'
                              % (nb, count, ext))
+
+
+def _bounds(buf):
+    """[lo, hi) addresses a tensor / array may touch: its whole storage (a
+    derived target may reach before the view's start, lb < 0); None for a
+    raw pointer (the caller vouches for the span)"""
+    if isinstance(buf, torch.Tensor):
+        st = buf.untyped_storage()
+        return st.data_ptr(), st.data_ptr() + st.nbytes()
+    if hasattr(buf, 'ctypes'):
+        root = buf
+        while getattr(root, 'base', None) is not None and hasattr(root.base, 'ctypes'):
+            root = root.base
+        import numpy as np
+        return np.byte_bounds(root)
+    return None
+
+
+def _range_check(buf, lo_off, hi_off, what):
+    """bytes [addr+lo_off, addr+hi_off) of `buf` must lie inside its storage"""
+    b = _bounds(buf)
+    if b is None or hi_off <= lo_off:
+        return
+    a = _addr(buf)
+    if a + lo_off < b[0] or a + hi_off > b[1]:
+        raise ValueError('%s: bytes [%d, %d) of the buffer fall outside its storage (%d bytes)'
+                         % (what, lo_off, hi_off, b[1] - b[0]))
 
 
 def _stream_ptr(stream):
@@ -169,6 +201,11 @@ def reduce_local_async(inbuf, inoutbuf, count, datatype, op, stream=None):
 def reduce_local_vector(inbuf, inoutbuf, count, blocklen, stride, basic_type, op, stream=None,
                         sync=False):
     """Vector target / packed source (typerep_op.c:115-150)."""
+    ext = _checked_extent(op, basic_type)
+    if ext > 0 and isinstance(count, int) and isinstance(blocklen, int) and count > 0 \
+            and blocklen > 0 and isinstance(stride, int) and stride >= blocklen:
+        _range_check(inoutbuf, 0, ((count - 1) * stride + blocklen) * ext, 'vector target')
+        _range_check(inbuf, 0, count * blocklen * ext, 'packed source')
     if sync:
         return lib().MPIX_Reduce_local_vector(_addr(inbuf), _addr(inoutbuf), count, blocklen,
                                               stride, H.as_c_int(basic_type), H.as_c_int(op))
@@ -181,6 +218,13 @@ def reduce_local_iov_async(inbuf, inoutbuf, seg_offsets, seg_counts, basic_type,
                            stream=None):
     """derived target given as its flattened iov (byte offsets, element counts)"""
     n = len(seg_offsets)
+    ext = _checked_extent(op, basic_type)
+    if ext > 0 and n and all(c >= 0 for c in seg_counts):
+        live = [(o, c) for o, c in zip(seg_offsets, seg_counts) if c > 0]
+        if live:
+            _range_check(inoutbuf, min(o for o, _ in live), max(o + c * ext for o, c in live),
+                         'iov target')
+            _range_check(inbuf, 0, sum(c for _, c in live) * ext, 'packed source')
     offs = (ctypes.c_ssize_t * n)(*seg_offsets)
     cnts = (ctypes.c_ssize_t * n)(*seg_counts)
     return lib().MPIX_Reduce_local_iov_async(_addr(inbuf), _addr(inoutbuf), n, offs, cnts,
@@ -193,6 +237,14 @@ def reduce_local_iovec_async(inbuf, inoutbuf, iov_offsets, iov_lens, basic_type,
     """derived target given as its raw iov (byte offsets, byte lengths):
     typerep_op_fallback incl. the pairtype gather (typerep_op.c:100-150)"""
     n = len(iov_offsets)
+    ext = _checked_extent(op, basic_type)
+    size = datatype_size(basic_type) if ext > 0 else 0
+    if ext > 0 and size > 0 and n and all(x >= 0 for x in iov_lens):
+        live = [(o, ln) for o, ln in zip(iov_offsets, iov_lens) if ln > 0]
+        if live:
+            _range_check(inoutbuf, min(o for o, _ in live), max(o + ln for o, ln in live),
+                         'iov target')
+            _range_check(inbuf, 0, (sum(ln for _, ln in live) // size) * ext, 'packed source')
     offs = (ctypes.c_ssize_t * n)(*iov_offsets)
     lens = (ctypes.c_ssize_t * n)(*iov_lens)
     return lib().MPIX_Reduce_local_iovec_async(_addr(inbuf), _addr(inoutbuf), n, offs, lens,
@@ -239,6 +291,31 @@ def check(rc, what='MPI_Reduce_local'):
 
 def is_supported(op, datatype, count=0):
     return bool(lib().MPIX_Redop_is_supported(H.as_c_int(op), count, H.as_c_int(datatype)))
+
+
+def is_supported_buffers(op, datatype, count, inbuf, inoutbuf):
+    """the pointer-aware predicate (host-resident operands below the floor of
+    their memory kind stay with the caller's CPU loop)"""
+    return bool(lib().MPIX_Redop_is_supported_buffers(H.as_c_int(op), count, H.as_c_int(datatype),
+                                                      _addr(inbuf), _addr(inoutbuf)))
+
+
+def set_support(enable=True, threshold_bytes=-1, host_floor_bytes=None, pinned_floor_bytes=None):
+    """the predicate's knobs (None keeps the current floor); returns an MPI error class"""
+    cur = get_support()
+    return lib().MPIX_Redop_set_support(
+        1 if enable else 0, threshold_bytes,
+        cur['host_floor_bytes'] if host_floor_bytes is None else host_floor_bytes,
+        cur['pinned_floor_bytes'] if pinned_floor_bytes is None else pinned_floor_bytes)
+
+
+def get_support():
+    e = ctypes.c_int()
+    t, h, p = ctypes.c_ssize_t(), ctypes.c_ssize_t(), ctypes.c_ssize_t()
+    check(lib().MPIX_Redop_get_support(ctypes.byref(e), ctypes.byref(t), ctypes.byref(h),
+                                       ctypes.byref(p)))
+    return dict(enable=bool(e.value), threshold_bytes=t.value, host_floor_bytes=h.value,
+                pinned_floor_bytes=p.value)
 
 
 def op_dt_check(op, datatype):

@@ -1,0 +1,150 @@
+"""The C++ schedules of libmpix_coll.so with the HIP combine, one PROCESS per
+rank -- the way MPICH runs every collective test (test/mpi/coll/testlist.in,
+`mpiexec -n N`; redscatblk3.c:48-78):
+
+  * test_staged_*: any number of ranks on the test box's one GPU, over a
+    custom communicator whose transport is gloo on host memory
+    (MPIX_XPORT_STAGED: the library stages the device buffers through pinned
+    memory around each exchange step, the MPIR_Coll_host_buffer_alloc pattern);
+  * test_rccl_*: one rank per GPU over RCCL (MPIX_Comm_create_ccl, the
+    transport of the 8-GPU bench), skipped below 2 devices.
+
+Every rank's block is compared bit for bit with the oracle's single-process
+simulation of the reference schedule (recursive halving:
+reduce_scatter_block_intra_recursive_halving.c:38-260; pairwise, pipelined
+pairwise and the fused pull: …_intra_pairwise.c:42-104; allreduce:
+allreduce_intra_reduce_scatter_allgather.c:41-277)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+MPI_FLOAT, MPI_2INT = 0x4c00040a, 0x4c000816
+MPI_SUM, MPI_MAXLOC = 0x58000003, 0x5800000c
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _inputs(rank, world, recvcount, kind):
+    rng = np.random.default_rng(0x5EED0400 + rank)
+    if kind == 'float':
+        return rng.uniform(-1, 1, world * recvcount).astype(np.float32), MPI_FLOAT, MPI_SUM
+    # MPI_2INT {value, loc}: values from 0..3 force ties (loc = min wins, opmaxloc.c)
+    v = rng.integers(0, 4, world * recvcount).astype(np.int32)
+    loc = rng.integers(0, 1 << 20, world * recvcount).astype(np.int32)
+    return np.stack([v, loc], 1).reshape(-1), MPI_2INT, MPI_MAXLOC
+
+
+def _worker(rank, world, port, outdir, backend, cases):
+    import torch.distributed as dist
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dev = rank if backend == 'nccl' else 0
+    torch.cuda.set_device(dev)
+    if backend == 'nccl':
+        dist.init_process_group('nccl', rank=rank, world_size=world,
+                                device_id=torch.device('cuda', dev))
+    else:
+        dist.init_process_group('gloo', rank=rank, world_size=world)
+    from mpich_amd import coll
+    for name, algo, kind, recvcount in cases:
+        send, dt, op = _inputs(rank, world, recvcount, kind)
+        ext = 8 if kind == 'pair' else 4
+        ds = torch.from_numpy(send.view(np.uint8).copy()).cuda()
+        if algo.startswith('allreduce'):
+            dr = torch.empty_like(ds)
+            coll.allreduce(ds, dr, world * recvcount, dt, op,
+                           allgather='recursive_doubling' if algo.endswith('_rd') else 'direct')
+        else:
+            dr = torch.empty(recvcount * ext, dtype=torch.uint8, device='cuda')
+            timer = [] if algo == 'recursive_halving' else None
+            for _ in range(2):      # the second call reuses scratch, mappings, staging
+                coll.reduce_scatter_block(ds, dr, recvcount, dt, op, algorithm=algo, timer=timer)
+            if timer is not None:           # per-step breakdown of both calls
+                phases = [t['phase'] for t in timer]
+                assert phases and phases[-1] == 'epilogue', phases
+                if world & (world - 1) == 0:
+                    assert phases.count('combine') == 2 * (world.bit_length() - 1), phases
+        torch.cuda.synchronize()
+        np.save(os.path.join(outdir, '%s_send%d.npy' % (name, rank)), send)
+        np.save(os.path.join(outdir, '%s_recv%d.npy' % (name, rank)), dr.cpu().numpy())
+    dist.barrier()
+    coll.free_comms()
+    dist.destroy_process_group()
+
+
+def _check(oracle, tmp_path, world, cases):
+    for name, algo, kind, recvcount in cases:
+        sends = [np.load(tmp_path / ('%s_send%d.npy' % (name, r))) for r in range(world)]
+        dt, op = (MPI_FLOAT, MPI_SUM) if kind == 'float' else (MPI_2INT, MPI_MAXLOC)
+        raw = [s.view(np.uint8) for s in sends]
+        if algo == 'recursive_halving':
+            exp = oracle.rsb_recursive_halving(raw, recvcount, dt, op)
+        elif algo.startswith('allreduce'):
+            exp = oracle.allreduce_rabenseifner(raw, world * recvcount, dt, op)
+        else:
+            exp = oracle.rsb_pairwise(raw, recvcount, dt, op)
+        for r in range(world):
+            got = np.load(tmp_path / ('%s_recv%d.npy' % (name, r)))
+            assert got.tobytes() == exp[r].tobytes(), (name, r)
+
+
+def _run(oracle, tmp_path, world, backend, cases):
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), backend, cases), nprocs=world,
+             join=True)
+    _check(oracle, tmp_path, world, cases)
+
+
+ALGOS = ('recursive_halving', 'pairwise', 'pairwise_pipelined', 'pull')
+
+
+@pytest.mark.parametrize('world', [2, 3, 4, 8])
+def test_staged_rsb_matches_oracle(oracle, tmp_path, world):
+    """every reduce-scatter schedule, fp32 SUM and MPI_2INT MAXLOC, ranks as
+    processes sharing the GPU, gloo transport through pinned staging"""
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    cases = [('%s_%s' % (a, k), a, k, 40009 if k == 'float' else 20011)
+             for a in ALGOS for k in ('float', 'pair')]
+    _run(oracle, tmp_path, world, 'gloo', cases)
+
+
+def test_staged_pipelined_large_blocks(oracle, tmp_path):
+    """blocks above 8 MiB: the pipelined pairwise schedule really cuts them
+    into chunks (combine of chunk k on the second stream), same bits"""
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    cases = [('pipe', 'pairwise_pipelined', 'float', (10 << 20) // 4 + 3)]
+    _run(oracle, tmp_path, 2, 'gloo', cases)
+
+
+@pytest.mark.parametrize('world', [3, 4])
+def test_staged_allreduce_matches_oracle(oracle, tmp_path, world):
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    cases = [('ar', 'allreduce', 'float', 25013), ('ar_rd', 'allreduce_rd', 'float', 25013)]
+    _run(oracle, tmp_path, world, 'gloo', cases)
+
+
+def test_rccl_rsb_matches_oracle(oracle, tmp_path):
+    """one process per GPU over RCCL (the bench's transport at N > 1)"""
+    ndev = torch.cuda.device_count() if torch.cuda.is_available() else 0
+    if ndev < 2:
+        pytest.skip('RCCL across processes needs >= 2 GPUs (this box has %d); RCCL refuses two '
+                    'ranks on one device (profiles/r01_rccl_probe.txt)' % ndev)
+    world = min(ndev, 8)
+    cases = [('%s_%s' % (a, k), a, k, 100003 if k == 'float' else 50021)
+             for a in ALGOS for k in ('float', 'pair')]
+    cases.append(('ar', 'allreduce', 'float', 25013))
+    _run(oracle, tmp_path, world, 'nccl', cases)

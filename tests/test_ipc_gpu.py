@@ -1,8 +1,10 @@
-"""Fused pull + combine reduce-scatter over hipIpc-mapped peer buffers,
-rehearsed with several processes sharing the one GPU of the test box
-(gloo carries the handles and barriers; the kernel reads the peers' device
-memory directly).  Result must equal the reference pairwise schedule
-(oracle simulation) bit for bit."""
+"""Fused pull + combine reduce-scatter over hipIpc-mapped peer buffers
+(MPIX_RSB_PULL of libmpix_coll, the C entry point), rehearsed with several
+processes sharing the one GPU of the test box: the library publishes IPC
+handles and runs its barriers over the communicator's transport (gloo through
+pinned staging here); the kernel reads the peers' device memory directly.
+Result must equal the reference pairwise schedule (oracle simulation) bit for
+bit."""
 import os
 import socket
 
@@ -41,16 +43,16 @@ def _worker(rank, world, port, outdir, recvcount, dtype_name):
     ds = torch.from_numpy(send).cuda()
     if in_place:                # MPI_IN_PLACE: peers pull from recvbuf itself
         dr = ds.clone()
-        coll.reduce_scatter_block_pull(None, dr, recvcount, dt, op, extent=4)
+        coll.reduce_scatter_block_pull(None, dr, recvcount, dt, op)
     else:
         dr = torch.empty(recvcount, dtype=ds.dtype, device='cuda')
         for _ in range(2):      # second call reuses the cached peer mappings
-            coll.reduce_scatter_block_pull(ds, dr, recvcount, dt, op, extent=4)
+            coll.reduce_scatter_block_pull(ds, dr, recvcount, dt, op)
     torch.cuda.synchronize()
     np.save(os.path.join(outdir, 'send%d.npy' % rank), send)
     np.save(os.path.join(outdir, 'recv%d.npy' % rank), dr[:recvcount].cpu().numpy())
     dist.barrier()
-    coll.ipc_cache_clear()
+    coll.free_comms()           # closes the cached peer mappings
     dist.barrier()
     dist.destroy_process_group()
 

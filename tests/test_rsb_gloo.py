@@ -1,10 +1,12 @@
-"""Multi-process CPU coverage of the N>1 path: the recursive-halving
-MPI_Reduce_scatter_block schedule of mpich_amd/coll.py run over the gloo
-backend with world sizes 2..8 (power-of-two and not), the oracle injected
-as the combine.  Checks (a) bit-identity with the oracle's single-process
-simulation of the reference schedule
-(reduce_scatter_block_intra_recursive_halving.c:38-260) and (b) the
-reference's own closed form (test/mpi/coll/redscatblk3.c:48-78)."""
+"""Multi-process CPU coverage of the N>1 path: the C++ schedules of
+libmpix_coll.so (the library MPICH would link, include/mpix_coll.h) run as
+one process per rank, over a custom host-memory communicator whose exchange
+steps are gloo batch_isend_irecv groups (mpich_amd/coll.py), the oracle
+installed as the combine (a C function: the product has no CPU compute path).
+World sizes 2..8, power-of-two and not.  Checks (a) bit-identity with the
+oracle's single-process simulation of the reference schedule
+(reduce_scatter_block_intra_recursive_halving.c:38-260, …_pairwise.c:42-104)
+and (b) the reference's own closed form (test/mpi/coll/redscatblk3.c:48-78)."""
 import os
 import socket
 
@@ -48,22 +50,20 @@ def _worker(rank, world, port, outdir, recvcount, mode, algo='recursive_halving'
     if in_place:
         recv, sendt = sendt, None
 
-    def combine(inb, inoutb, count):
-        a = inoutb.numpy()
-        b = inb.numpy()
-        assert orc.reduce_local(b, a, count, dt, MPI_SUM) == 0
-
+    combine = orc.combine_fn_address()
     if algo == 'recursive_halving':
-        tl = []     # the per-step timer is inert on host tensors
-        coll.reduce_scatter_block(sendt, recv, recvcount, dt, MPI_SUM, combine=combine, extent=4,
-                                  timer=tl)
-        assert len(tl) == 1 and tl[0].result() == []
+        tl = []     # the per-step timer is inert on host buffers
+        coll.reduce_scatter_block(sendt, recv, recvcount, dt, MPI_SUM, combine=combine, timer=tl)
+        assert tl == []
+    elif algo == 'pull':        # host communicator: the pairwise schedule, same bits
+        coll.reduce_scatter_block_pull(sendt, recv, recvcount, dt, MPI_SUM, combine=combine)
     else:
         coll.reduce_scatter_block_pairwise(sendt, recv, recvcount, dt, MPI_SUM, combine=combine,
-                                           extent=4, concurrent=(algo == 'pairwise'))
+                                           concurrent=(algo == 'pairwise'))
     np.save(os.path.join(outdir, 'send%d.npy' % rank), send)
     np.save(os.path.join(outdir, 'recv%d.npy' % rank), recv.numpy()[:recvcount])
     dist.barrier()
+    coll.free_comms()
     dist.destroy_process_group()
 
 
@@ -120,7 +120,7 @@ def test_rsb_gloo_redscatblk3(tmp_path, world):
         assert np.all(recvs[r] == world * r + world * (world - 1) // 2)
 
 
-@pytest.mark.parametrize('algo', ['pairwise', 'pairwise_sequential'])
+@pytest.mark.parametrize('algo', ['pairwise', 'pairwise_sequential', 'pull'])
 @pytest.mark.parametrize('world', [2, 3, 4, 7])
 def test_pairwise_gloo_matches_oracle(oracle, tmp_path, world, algo):
     """concurrent (one group, all links) and the reference's sequential
@@ -134,19 +134,6 @@ def test_pairwise_gloo_matches_oracle(oracle, tmp_path, world, algo):
     sends, recvs = _run(world, 1000, 'int', tmp_path, algo)
     for r in range(world):
         assert np.all(recvs[r] == world * r + world * (world - 1) // 2)
-
-
-def test_plan_matches_reference_counts():
-    """step table of the schedule for P=8: halves 4,2,1 blocks."""
-    from mpich_amd import coll
-    rc = 10
-    for r in range(8):
-        p = coll.plan(r, 8, rc)
-        assert [s[2] for s in p['steps']] == [40, 20, 10]
-        assert [s[4] for s in p['steps']] == [40, 20, 10]
-        assert [s[0] for s in p['steps']] == [r ^ 4, r ^ 2, r ^ 1]
-    p = coll.plan(0, 6, rc)          # non-pof2: even rank < 2*rem sits out
-    assert p['newrank'] == -1 and p['steps'] == []
 
 
 def _ar_worker(rank, world, port, outdir, count, algo='reduce_scatter_allgather'):
@@ -163,10 +150,7 @@ def _ar_worker(rank, world, port, outdir, count, algo='reduce_scatter_allgather'
     send = rng.uniform(-1, 1, count).astype(np.float32)
     recv = torch.zeros(count, dtype=torch.float32)
 
-    def mk_combine(dt, op):
-        def combine(inb, inoutb, n):
-            assert orc.reduce_local(inb.numpy(), inoutb.numpy(), n, dt, op) == 0
-        return combine
+    combine = orc.combine_fn_address()
     if algo == 'recursive_doubling':
         fn = coll.allreduce_recursive_doubling
     else:   # second phase: one group of direct sends, or the reference's exchanges
@@ -174,8 +158,7 @@ def _ar_worker(rank, world, port, outdir, count, algo='reduce_scatter_allgather'
 
         def fn(*a, **k):
             return coll.allreduce(*a, allgather=ag, **k)
-    fn(torch.from_numpy(send.copy()), recv, count, MPI_FLOAT, MPI_SUM,
-       combine=mk_combine(MPI_FLOAT, MPI_SUM), extent=4)
+    fn(torch.from_numpy(send.copy()), recv, count, MPI_FLOAT, MPI_SUM, combine=combine)
     np.save(os.path.join(outdir, 'send%d.npy' % rank), send)
     np.save(os.path.join(outdir, 'recv%d.npy' % rank), recv.numpy())
     # the allred.c KATs that were generated for this world size, end to end
@@ -188,12 +171,13 @@ def _ar_worker(rank, world, port, outdir, count, algo='reduce_scatter_allgather'
         ext = len(c['expected']) // c['count']
         out = torch.zeros(c['count'] * ext, dtype=torch.uint8)
         fn(torch.from_numpy(c['inputs'][rank].copy()), out, c['count'], c['datatype'], c['op'],
-           combine=mk_combine(c['datatype'], c['op']), extent=ext)
+           combine=combine)
         if gu.mismatches(c, out.numpy()):
             bad.append(c['id'])
     with open(os.path.join(outdir, 'bad%d.txt' % rank), 'w') as f:
         f.write(' '.join(bad))
     dist.barrier()
+    coll.free_comms()
     dist.destroy_process_group()
 
 
