@@ -171,12 +171,13 @@ def host_crossover_gpu(B):
     return out
 
 
-def crossover_from(rows, key):
-    """smallest size from which the GPU path is faster than one core at
-    every larger size too (None: the CPU wins at every measured size)"""
+def crossover_from(rows, key, tol=1.05):
+    """smallest size from which the GPU path is faster than one core, or
+    within 5 % of it, at every larger size too (None: the CPU wins at every
+    measured size)"""
     best = None
     for r in reversed(rows):
-        if r[key] < r['cpu_1core_us']:
+        if r[key] <= tol * r['cpu_1core_us']:
             best = r['bytes']
         else:
             break
@@ -399,8 +400,8 @@ def single_gpu(args, dev):
                                     pinned=sup['pinned_floor_bytes']),
                 note='bytes per operand; GPU = synchronous MPIX_Reduce_local on host operands, '
                      'CPU = the oracle loop on one core, both median per call timed in C; the '
-                     'crossover is the smallest size from which the GPU path wins at every larger '
-                     'size (the MPIX_Redop_is_supported_buffers floor)')
+                     'crossover is the smallest size from which the GPU path is faster or within 5 % '
+                     'at every larger size (the MPIX_Redop_is_supported_buffers floor)')
     print(json.dumps(result, default=str), flush=True)
 
 

@@ -21,6 +21,7 @@
 #include <rccl/rccl.h>
 
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -287,6 +288,14 @@ int exchange_staged(MPIX_Comm c, const MPIX_P2p_op *ops, int nops, hipStream_t s
     return MPIX_REDOP_SUCCESS;
 }
 
+// env MPIX_COLL_TRACE: every exchange step (and the pull's published
+// records) as one stderr line per rank -- how a mismatched schedule is found
+bool coll_trace()
+{
+    static const bool t = getenv("MPIX_COLL_TRACE") != nullptr;
+    return t;
+}
+
 int exchange(MPIX_Comm c, const std::vector<MPIX_P2p_op> &ops, hipStream_t s)
 {
     // zero-length messages are not sent (both sides know the lengths, so
@@ -299,6 +308,14 @@ int exchange(MPIX_Comm c, const std::vector<MPIX_P2p_op> &ops, hipStream_t s)
             nz.push_back(o);
     if (nz.empty())
         return MPIX_REDOP_SUCCESS;
+    if (coll_trace()) {     // one line per exchange step: what this rank posts
+        std::string line = "[mpix_coll rank " + std::to_string(c->rank) + "/" +
+                           std::to_string(c->size) + "]";
+        for (const MPIX_P2p_op &o : nz)
+            line += std::string(" ") + (o.is_recv ? "<" : ">") + std::to_string(o.peer) + ":" +
+                    std::to_string(o.bytes);
+        fprintf(stderr, "%s\n", line.c_str());
+    }
     switch (c->kind) {
         case K_CCL:
             return exchange_ccl(c, nz.data(), (int) nz.size(), s);
@@ -335,7 +352,7 @@ int mark(MPIX_Comm c, const char *label, hipStream_t s)
 // one published record per rank (barrier tokens are 1-byte records)
 constexpr size_t kRec = 128;
 
-int token_buffer(MPIX_Comm c)
+int token_buffer(MPIX_Comm c, hipStream_t s)
 {
     if (c->tok)
         return MPIX_REDOP_SUCCESS;
@@ -346,7 +363,10 @@ int token_buffer(MPIX_Comm c)
     }
     void *p = nullptr;
     HTRY(hipMalloc(&p, bytes));
-    HTRY(hipMemset(p, 0, bytes));
+    // zeroed ON the collective's stream: a plain hipMemset runs on the null
+    // stream, which a non-blocking stream does not wait for, and could land
+    // after the record this rank is about to copy in (peers then saw zeros)
+    HTRY(hipMemsetAsync(p, 0, bytes, s));
     c->tok = static_cast<char *>(p);
     return MPIX_REDOP_SUCCESS;
 }
@@ -357,7 +377,7 @@ int token_buffer(MPIX_Comm c)
 int allgather_records(MPIX_Comm c, const void *mine, size_t bytes, std::vector<char> *out,
                       hipStream_t s)
 {
-    TRY(token_buffer(c));
+    TRY(token_buffer(c, s));
     const int P = c->size;
     out->assign(kRec * (size_t) P, 0);
     std::vector<MPIX_P2p_op> ops;
@@ -386,7 +406,7 @@ int barrier(MPIX_Comm c, hipStream_t s)
 {
     if (c->size == 1)
         return MPIX_REDOP_SUCCESS;
-    TRY(token_buffer(c));
+    TRY(token_buffer(c, s));
     std::vector<MPIX_P2p_op> ops;
     for (int q = 0; q < c->size; ++q)
         if (q != c->rank) {
@@ -848,6 +868,12 @@ int rs_pull(const char *sb, char *rb, const std::vector<size_t> &cnts, MPIX_Data
     for (int q = 0; q < size; ++q) {
         memcpy(&recs[q], all.data() + kRec * (size_t) q, sizeof(PullRec));
         ok &= recs[q].valid == 1;
+    }
+    if (coll_trace()) {
+        std::string line = "[mpix_coll rank " + std::to_string(rank) + "] pull records:";
+        for (int q = 0; q < size; ++q)
+            line += " " + std::to_string(recs[q].valid) + "/" + std::to_string(recs[q].offset);
+        fprintf(stderr, "%s\n", line.c_str());
     }
     if (!ok)
         return fallback();

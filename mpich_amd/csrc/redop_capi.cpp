@@ -270,8 +270,12 @@ std::atomic<size_t> g_pipe_chunk{(size_t) 16 << 20};
 // the PCIe round trip (crossover measured by bench.py's host_crossover leg).
 std::atomic<bool> g_enable{true};
 std::atomic<long long> g_threshold{-1};
-std::atomic<long long> g_host_floor{(long long) 1 << 30};
-std::atomic<long long> g_pinned_floor{(long long) 64 << 20};
+// defaults from bench.py's host_crossover on MI355X + EPYC 9575F (profiles/
+// r02_host_crossover.json): one core wins below 16 MiB per pageable operand
+// and below 4 MiB per page-locked one; from there on the GPU path is faster or
+// within 5 % at every measured size
+std::atomic<long long> g_host_floor{(long long) 16 << 20};
+std::atomic<long long> g_pinned_floor{(long long) 4 << 20};
 // MPIX_Op_table entries return void, like MPIR_op_function: a call the GPU
 // path declines aborts by default, as op_fns.c's MPIR_Assert(0) does
 // (op_fns.c:51-53); MPIX_REDOP_OPFN_ABORT=0 only records the error
@@ -420,7 +424,11 @@ DevState *dev_state(int dev)
             *d.flag = 0;
             void *c = nullptr;
             if (hipMalloc(&c, 256) == hipSuccess) {
-                if (hipMemset(c, 0, 256) == hipSuccess)
+                // zeroed on the state's own stream and waited for: the
+                // null-stream hipMemset is not ordered before kernels on the
+                // non-blocking streams that read this counter
+                if (hipMemsetAsync(c, 0, 256, d.s[0]) == hipSuccess &&
+                    hipStreamSynchronize(d.s[0]) == hipSuccess)
                     d.flag_ctr = (uint32_t *) c;
                 else
                     (void) hipFree(c);

@@ -122,7 +122,11 @@ def _checked_extent(op, datatype):
         ext = 0
         # the pair itself, whatever the enable / threshold knobs say: the
         # span check guards every call the kernels would run
-        if lib().MPIX_Redop_op_dt_check(cop, cdt) or lib().MPIX_Redop_internal_op_dt_check(cop, cdt):
+        legal = lib().MPIX_Redop_op_dt_check(cop, cdt) or \
+            lib().MPIX_Redop_internal_op_dt_check(cop, cdt)
+        if (op & 0xff) == 0x0f and (datatype_internal(datatype) & 0xffffff00) != 0x4c820100:
+            legal = False                   # MPIX_EQUAL: MPI_BYTE only (opequal.c:22-23)
+        if legal:
             ext = max(0, lib().MPIX_Datatype_extent(cdt))
         _extent_cache[key] = ext
     return ext
