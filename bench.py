@@ -79,6 +79,9 @@ def bench_lib():
                                           ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                           ctypes.POINTER(ctypes.c_double),
                                           ctypes.POINTER(ctypes.c_double)]
+    L.mpix_bench_call_loop.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       ctypes.POINTER(ctypes.c_double)]
     L.mpix_bench_chunked_async.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                            ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
                                            ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
@@ -304,17 +307,26 @@ def reduce_local_leg(args, world, rank, dev):
     fill_uniform(inb, 0x5EED0002 + 2 * rank)
     torch.cuda.synchronize()
 
-    def step():
-        redop.check(redop.MPI_Reduce_local(inb, inout, n, H.MPI_FLOAT, H.MPI_SUM))
+    # one step = one synchronous MPIX_Reduce_local, called back to back from C
+    # (libmpix_bench's loop: the C-ABI as MPICH calls it, no Python between
+    # the calls); the first call goes through the Python mirror, which checks
+    # the buffer spans and the MPI error class
+    B = bench_lib()
+    fn = ctypes.cast(redop.lib().MPIX_Reduce_local, ctypes.c_void_p).value
+    redop.check(redop.MPI_Reduce_local(inb, inout, n, H.MPI_FLOAT, H.MPI_SUM))
 
-    for _ in range(args.warmup):
-        step()
+    def steps(k):
+        tl = ctypes.c_double()
+        redop.check(B.mpix_bench_call_loop(fn, inb.data_ptr(), inout.data_ptr(), n,
+                                           H.as_c_int(H.MPI_FLOAT), H.as_c_int(H.MPI_SUM), k,
+                                           ctypes.byref(tl)), 'MPIX_Reduce_local')
+
+    steps(args.warmup)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    steps(args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -328,7 +328,10 @@ int MPIX_Redop_get_launch(int *block_threads, int *unroll, int *max_grid);
  * them with threads = 0, are staged through device scratch with
  * hipMemcpyAsync.  Same bits either way.  Defaults 8 workers x 16 MiB (env
  * MPIX_REDOP_PAGEABLE_THREADS / MPIX_REDOP_PAGEABLE_CHUNK at first use);
- * threads 0..16, chunk 64 KiB..256 MiB. */
+ * threads 0..16, chunk 64 KiB..256 MiB.  The slots are one set per device
+ * for the whole process (threads x 2 x chunk of page-locked memory, 256 MiB
+ * at the defaults, freed by MPIX_Redop_finalize); a call that finds the set
+ * in use by another thread stages its operands instead. */
 int MPIX_Redop_set_pageable(int threads, MPIX_Aint chunk_bytes);
 int MPIX_Redop_get_pageable(int *threads, MPIX_Aint *chunk_bytes);
 

@@ -75,6 +75,27 @@ extern "C" int mpix_bench_call_latency(void *fn, const void *in, void *io, int64
     return 0;
 }
 
+// `reps` back-to-back calls of a synchronous reduce entry point (the headline
+// loop of bench.py: one MPIX_Reduce_local per step, issued from C as MPICH
+// issues it, so no binding overhead sits between the calls); *total_s is the
+// wall time of the whole loop.
+extern "C" int mpix_bench_call_loop(void *fn, const void *in, void *io, int64_t count, int dt,
+                                    int op, int reps, double *total_s)
+{
+    if (!fn || reps < 0 || !total_s)
+        return 12;
+    sync_reduce_fn f = (sync_reduce_fn) fn;
+    auto a = std::chrono::steady_clock::now();
+    for (int i = 0; i < reps; ++i) {
+        int rc = f(in, io, count, dt, op);
+        if (rc)
+            return rc;
+    }
+    auto b = std::chrono::steady_clock::now();
+    *total_s = std::chrono::duration<double>(b - a).count();
+    return 0;
+}
+
 // The chunked regime of a pipelined collective (one combine per arriving
 // chunk), issued from C: `count` elements of `elem_size` bytes cut into
 // chunks of `chunk` elements, each enqueued through the stream-ordered entry

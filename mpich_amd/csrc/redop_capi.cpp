@@ -354,14 +354,24 @@ struct DevState {
     char *bounce = nullptr;     // pinned host: in half + inout half, bounce_half bytes each
     char *bounce_dev = nullptr; // its device mapping
     size_t bounce_half = 0;
-    // large pageable operands: one stream + pinned slot pair per host worker
-    struct PipeSlot {
-        hipStream_t s = nullptr;
-        char *host = nullptr;   // in half + inout half, pipe_half bytes each
-        char *dev = nullptr;    // its device mapping
-    } pipe[16];
-    size_t pipe_half = 0;       // slot half size; slots [0, threads) hold host != nullptr
 };
+
+// Large pageable operands: one stream + pinned slot pair per host worker, ONE
+// set per device for the whole process (not per calling thread), so the
+// pinned footprint is workers x 2 x chunk (256 MiB at the defaults) per device
+// however many MPI_THREAD_MULTIPLE threads call in.  A call that finds the set
+// busy stages its operands instead (same kernel, same bits).
+struct PipeSlot {
+    hipStream_t s = nullptr;
+    char *host = nullptr;   // in half + inout half, half bytes each
+    char *dev = nullptr;    // its device mapping
+};
+struct PipeSet {
+    std::mutex mu;
+    PipeSlot slot[16];
+    size_t half = 0;        // slot half size; slots [0, threads) hold host != nullptr
+};
+PipeSet *g_pipes = new PipeSet[64];     // per device; never destroyed (finalize frees the memory)
 // Per-thread device state (streams, flag word, scratch).  A thread that exits
 // hands its array to a process-wide pool and the next new thread takes it over
 // instead of creating streams of its own, so MPI_THREAD_MULTIPLE codes that
@@ -776,25 +786,28 @@ int bounced(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext,
 int pipelined(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext, uint32_t op,
               bool in_pg, bool io_pg, int dev, int nthreads)
 {
-    DevState *d = dev_state(dev);
-    if (!d)
-        return MPIX_REDOP_ERR_OTHER;
+    if (dev < 0 || dev >= kMaxDev)
+        return -1;
+    PipeSet &P = g_pipes[dev];
+    std::unique_lock<std::mutex> busy(P.mu, std::try_to_lock);
+    if (!busy.owns_lock())
+        return -1;      // another thread is using the set: stage instead
     const size_t half = (g_pipe_chunk.load() + 255) & ~(size_t) 255;
-    bool ready = d->pipe_half >= half;
+    bool ready = P.half >= half;
     for (int w = 0; ready && w < nthreads; ++w)
-        ready = d->pipe[w].host != nullptr;
+        ready = P.slot[w].host != nullptr;
     if (!ready) {
         // (re)allocate every worker's slot at the current chunk size
-        for (DevState::PipeSlot &sl : d->pipe) {
+        for (PipeSlot &sl : P.slot) {
             if (sl.s)
                 (void) hipStreamSynchronize(sl.s);
             if (sl.host)
                 (void) hipHostFree(sl.host);
             sl.host = sl.dev = nullptr;
         }
-        d->pipe_half = 0;
+        P.half = 0;
         for (int w = 0; w < nthreads; ++w) {
-            DevState::PipeSlot &sl = d->pipe[w];
+            PipeSlot &sl = P.slot[w];
             if (!sl.s && hipStreamCreateWithFlags(&sl.s, hipStreamNonBlocking) != hipSuccess)
                 return -1;
             void *h = nullptr, *hd = nullptr;
@@ -807,7 +820,7 @@ int pipelined(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ex
             sl.host = (char *) h;
             sl.dev = (char *) hd;
         }
-        d->pipe_half = half;
+        P.half = half;
     }
     uint64_t chunk = half / ext;
     if (chunk == 0)
@@ -816,7 +829,7 @@ int pipelined(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ex
     const int W = (int) std::min<uint64_t>((uint64_t) nthreads, nchunks);
     std::atomic<int> err{MPIX_REDOP_SUCCESS};
     auto work = [&](int w) {
-        DevState::PipeSlot &sl = d->pipe[w];
+        PipeSlot &sl = P.slot[w];
         if (hipSetDevice(dev) != hipSuccess) {
             int z = MPIX_REDOP_SUCCESS;
             err.compare_exchange_strong(z, MPIX_REDOP_ERR_OTHER);
@@ -1059,12 +1072,6 @@ static void free_states(DevState *arr)
         }
         if (d.bounce)
             (void) hipHostFree(d.bounce);
-        for (DevState::PipeSlot &sl : d.pipe) {
-            if (sl.s)
-                (void) hipStreamDestroy(sl.s);
-            if (sl.host)
-                (void) hipHostFree(sl.host);
-        }
         d = DevState();
     }
     delete[] arr;
@@ -1082,6 +1089,23 @@ int MPIX_Redop_finalize(void)
     t_dev.arr = nullptr;
     for (DevState *arr : pooled)
         free_states(arr);
+    for (int i = 0; i < kMaxDev; ++i) {     // the process-wide pageable worker slots
+        PipeSet &P = g_pipes[i];
+        std::lock_guard<std::mutex> l(P.mu);
+        if (!P.slot[0].s && !P.slot[0].host)
+            continue;
+        DeviceGuard g(i);
+        for (PipeSlot &sl : P.slot) {
+            if (sl.s) {
+                (void) hipStreamSynchronize(sl.s);
+                (void) hipStreamDestroy(sl.s);
+            }
+            if (sl.host)
+                (void) hipHostFree(sl.host);
+            sl = PipeSlot();
+        }
+        P.half = 0;
+    }
     return MPIX_REDOP_SUCCESS;
 }
 

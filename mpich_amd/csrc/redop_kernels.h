@@ -264,6 +264,30 @@ template <> struct RawOf<8> { typedef unsigned int type __attribute__((ext_vecto
 template <> struct RawOf<16> { typedef unsigned int type __attribute__((ext_vector_type(4))); };
 template <> struct RawOf<32> { typedef unsigned int type __attribute__((ext_vector_type(8))); };
 
+// Payload store of the stride-2 vector target, write-through (global_store
+// sc0 sc1: the half-written line leaves L2 at once instead of waiting dirty
+// for eviction) for 1..8-byte units: +1.9 % at the 2.5 GiB traffic floor of
+// config 5, same FETCH/WRITE bytes (profiles/r02_tune_vector2.txt,
+// tools/tune_vector2.hip S1 vs S0).  A relaxed system-scope atomic store is
+// only the cache policy here: no ordering is asked of it.
+template <typename T>
+__device__ __forceinline__ void st_payload_wt(T *p, const T &v)
+{
+    if constexpr (sizeof(T) == 8) {
+        unsigned long long u;
+        __builtin_memcpy(&u, &v, 8);
+        __hip_atomic_store(reinterpret_cast<unsigned long long *>(p), u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    } else if constexpr (sizeof(T) == 4) {
+        unsigned int u;
+        __builtin_memcpy(&u, &v, 4);
+        __hip_atomic_store(reinterpret_cast<unsigned int *>(p), u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    } else {
+        *p = v;
+    }
+}
+
 template <class C>
 __global__ void __launch_bounds__(256)
 k_vector_s2(const typename C::unit *__restrict__ in, typename C::unit *__restrict__ io, uint64_t n,
@@ -280,7 +304,7 @@ k_vector_s2(const typename C::unit *__restrict__ in, typename C::unit *__restric
         } else {    // the last pair would reach one element past the type's span
             t = io[2 * j];
         }
-        io[2 * j] = C::apply(t, in[j], prm);
+        st_payload_wt(io + 2 * j, C::apply(t, in[j], prm));
     }
 }
 
