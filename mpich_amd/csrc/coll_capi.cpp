@@ -68,8 +68,15 @@ struct Local {
 };
 
 // a peer that never reaches the matching step is an application bug; fail the
-// call instead of hanging the process
+// call instead of hanging the process.  The deadline is on the system clock:
+// libstdc++ waits on it with pthread_cond_timedwait, which ThreadSanitizer
+// intercepts (a steady-clock wait_for goes through pthread_cond_clockwait,
+// which GCC 11's TSan does not, and reads as a double lock)
 const auto kPeerTimeout = std::chrono::seconds(300);
+std::chrono::system_clock::time_point peer_deadline()
+{
+    return std::chrono::system_clock::now() + kPeerTimeout;
+}
 
 }  // namespace
 
@@ -187,7 +194,7 @@ int exchange_local(MPIX_Comm c, const MPIX_P2p_op *ops, int nops, hipStream_t s)
         Slot sl;
         {
             std::unique_lock<std::mutex> g(L.m);
-            if (!L.cv.wait_for(g, kPeerTimeout, [&] { return L.slots.count(k) != 0; })) {
+            if (!L.cv.wait_until(g, peer_deadline(), [&] { return L.slots.count(k) != 0; })) {
                 rc = MPIX_REDOP_ERR_OTHER;
                 break;
             }
@@ -227,7 +234,7 @@ int exchange_local(MPIX_Comm c, const MPIX_P2p_op *ops, int nops, hipStream_t s)
         std::shared_ptr<DoneEv> d;
         {
             std::unique_lock<std::mutex> g(L.m);
-            if (!L.cv.wait_for(g, kPeerTimeout, [&] { return L.slots[k].consumed; })) {
+            if (!L.cv.wait_until(g, peer_deadline(), [&] { return L.slots[k].consumed; })) {
                 rc = MPIX_REDOP_ERR_OTHER;
                 continue;
             }
