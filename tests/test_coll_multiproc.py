@@ -137,6 +137,61 @@ def test_staged_allreduce_matches_oracle(oracle, tmp_path, world):
     _run(oracle, tmp_path, world, 'gloo', cases)
 
 
+def _config4_worker(rank, world, port, outdir, total_bytes):
+    """BASELINE config 4's vector size on the staged transport: 2 ranks, a
+    4 GiB fp32 vector each, recursive halving + HIP combine; each rank checks
+    its 2 GiB block on the device, bit for bit, against the schedule's one
+    IEEE add per element (P = 2: inout = own + partner's) computed by torch
+    from the partner's regenerated input, and an MPI_INT run against the
+    redscatblk3.c closed form at the same size"""
+    import torch.distributed as dist
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from mpich_amd import coll
+    n = total_bytes // 4
+    rc = n // world
+
+    def vec(r):
+        g = torch.Generator(device='cuda')
+        g.manual_seed(0x5EED0C40 + r)
+        return torch.empty(n, dtype=torch.float32, device='cuda').uniform_(-1, 1, generator=g)
+    x = vec(rank)
+    out = torch.empty(rc, dtype=torch.float32, device='cuda')
+    coll.reduce_scatter_block(x, out, rc, MPI_FLOAT, MPI_SUM, algorithm='recursive_halving')
+    del x
+    torch.cuda.empty_cache()
+    mine = vec(rank)[rank * rc:(rank + 1) * rc].clone()
+    other = vec(1 - rank)[rank * rc:(rank + 1) * rc].clone()
+    torch.cuda.empty_cache()
+    ok_f = bool(torch.equal((mine + other).view(torch.int32), out.view(torch.int32)))
+    del mine, other, out
+    torch.cuda.empty_cache()
+    xi = torch.cat([torch.full((rc,), rank + b, dtype=torch.int32, device='cuda')
+                    for b in range(world)])
+    oi = torch.empty(rc, dtype=torch.int32, device='cuda')
+    coll.reduce_scatter_block(xi, oi, rc, 0x4c000405, MPI_SUM, algorithm='recursive_halving')
+    ok_i = bool(torch.all(oi == world * rank + world * (world - 1) // 2))
+    with open(os.path.join(outdir, 'ok%d.txt' % rank), 'w') as f:
+        f.write('%d %d' % (ok_f, ok_i))
+    del xi, oi
+    dist.barrier()
+    coll.free_comms()
+    dist.destroy_process_group()
+
+
+def test_staged_rsb_config4_full_size(tmp_path):
+    """recursive halving at the 4 GiB-per-rank vector of BASELINE configs[3]
+    (two ranks on the test GPU), fp32 bit-exact and MPI_INT closed form"""
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    mp.spawn(_config4_worker, args=(2, _free_port(), str(tmp_path), 4 << 30), nprocs=2,
+             join=True)
+    for r in range(2):
+        assert open(tmp_path / ('ok%d.txt' % r)).read() == '1 1', r
+
+
 def test_rccl_rsb_matches_oracle(oracle, tmp_path):
     """one process per GPU over RCCL (the bench's transport at N > 1)"""
     ndev = torch.cuda.device_count() if torch.cuda.is_available() else 0
