@@ -635,11 +635,13 @@ def rsb_secondary(args, world, rank, dev, out):
     send = torch.empty(total, dtype=torch.float32, device=dev)
     fill_uniform(send, 0x5EED0100 + rank)
     recv = torch.empty(recvcount, dtype=torch.float32, device=dev)
+    torch.cuda.synchronize()
     for algo in ('pairwise', 'pairwise_pipelined', 'pull'):
         rc_small = 4096 + 3
         blk = torch.cat([torch.full((rc_small,), rank + i, dtype=torch.int32, device=dev)
                          for i in range(world)])
         o = torch.empty(rc_small, dtype=torch.int32, device=dev)
+        torch.cuda.synchronize()        # inputs ready before the communicator's stream reads them
         redop.check(ccl.reduce_scatter_block(blk, o, rc_small, H.MPI_INT, H.MPI_SUM, cc, algo),
                     'MPIX_Reduce_scatter_block')
         ok = allreduce_scalar(1 if bool(torch.all(o == world * rank + world * (world - 1) // 2))
@@ -680,6 +682,7 @@ def allreduce_secondary(args, world, rank, dev, res):
     m = 100003          # allred.c sum_test_1 closed form (in = i, sol = i*P), on device
     x = torch.arange(m, dtype=torch.int32, device=dev)
     y = torch.empty_like(x)
+    torch.cuda.synchronize()
     redop.check(ccl.allreduce(x, y, m, H.MPI_INT, H.MPI_SUM, cc, 'reduce_scatter_allgather'),
                 'MPIX_Allreduce')
     if not allreduce_scalar(1 if bool(torch.all(y == x * world)) else 0, dist.ReduceOp.MIN, dev):
@@ -689,6 +692,7 @@ def allreduce_secondary(args, world, rank, dev, res):
     fill_uniform(send, 0x5EED0200 + rank)
     recv = torch.empty_like(send)
     ws = torch.empty(n * 4, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
     res.update(parity_allred_sum_test_1_all_ranks=True, bytes_per_rank=n * 4, P=world)
     for name, fn in (('c_reduce_scatter_allgather',
                       lambda: redop.check(ccl.allreduce(send, recv, n, H.MPI_FLOAT, H.MPI_SUM, cc,

@@ -91,6 +91,23 @@ def _is_device(*bufs):
     return True
 
 
+def _order_after_torch(comm, dev):
+    """order the blocking collective after the torch work that produced its
+    inputs (torch semantics; an MPI caller synchronises its own streams
+    first).  A side stream of torch's is handed to the communicator; torch's
+    default stream is the legacy NULL stream, which the communicator's own
+    non-blocking stream does not wait for (and a NULL handle means "own
+    stream" to MPIX_Comm_set_stream), so that one is synchronised instead."""
+    if not dev:
+        return
+    cs = torch.cuda.current_stream()
+    if cs.cuda_stream:
+        comm.set_stream(cs)
+    else:
+        cs.synchronize()
+        comm.set_stream(None)
+
+
 def reduce_scatter_block(sendbuf, recvbuf, recvcount, datatype, op, group=None,
                          algorithm='recursive_halving', combine=None, workspace=None, timer=None):
     """MPI_Reduce_scatter_block(sendbuf, recvbuf, recvcount, datatype, op, comm).
@@ -108,6 +125,7 @@ def reduce_scatter_block(sendbuf, recvbuf, recvcount, datatype, op, group=None,
                          'kernel (device buffers)')
     c = comm_for(group, dev)
     c.set_combine(combine)
+    _order_after_torch(c, dev)
     if timer is not None:
         c.set_step_timing(True)
     try:
@@ -168,6 +186,7 @@ def allreduce(sendbuf, recvbuf, count, datatype, op, group=None, combine=None, w
         raise ValueError('host buffers need a combine function')
     c = comm_for(group, dev)
     c.set_combine(combine)
+    _order_after_torch(c, dev)
     redop.check(ccl.allreduce(sendbuf, recvbuf, count, datatype, op, c, algorithm,
                               workspace=workspace), 'MPIX_Allreduce')
     return recvbuf

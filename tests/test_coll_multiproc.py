@@ -172,9 +172,16 @@ def _config4_worker(rank, world, port, outdir, total_bytes):
                     for b in range(world)])
     oi = torch.empty(rc, dtype=torch.int32, device='cuda')
     coll.reduce_scatter_block(xi, oi, rc, 0x4c000405, MPI_SUM, algorithm='recursive_halving')
-    ok_i = bool(torch.all(oi == world * rank + world * (world - 1) // 2))
+    want = world * rank + world * (world - 1) // 2
+    bad = (oi != want).nonzero()
+    ok_i = bad.numel() == 0
     with open(os.path.join(outdir, 'ok%d.txt' % rank), 'w') as f:
         f.write('%d %d' % (ok_f, ok_i))
+    if not ok_i:
+        with open(os.path.join(outdir, 'bad%d.txt' % rank), 'w') as f:
+            f.write('%d bad of %d, first %s, last %s, values %s' % (
+                bad.numel(), rc, bad[:3].flatten().tolist(), bad[-3:].flatten().tolist(),
+                torch.unique(oi[bad.flatten()[:1000000]]).tolist()[:10]))
     del xi, oi
     dist.barrier()
     coll.free_comms()
@@ -189,7 +196,9 @@ def test_staged_rsb_config4_full_size(tmp_path):
     mp.spawn(_config4_worker, args=(2, _free_port(), str(tmp_path), 4 << 30), nprocs=2,
              join=True)
     for r in range(2):
-        assert open(tmp_path / ('ok%d.txt' % r)).read() == '1 1', r
+        got = open(tmp_path / ('ok%d.txt' % r)).read()
+        detail = open(tmp_path / ('bad%d.txt' % r)).read() if got != '1 1' else ''
+        assert got == '1 1', (r, detail)
 
 
 def test_rccl_rsb_matches_oracle(oracle, tmp_path):

@@ -7,4 +7,10 @@ timeout -k 10 600 python3 -u -m pytest -x -v --durations=5 --timeout 400 --timeo
     tests/test_coll_multiproc.py > $O/mp.log 2>&1
 rc=$?
 tail -15 $O/mp.log
-exit $rc
+
+MPIX_BENCH_SAME_DEVICE=1 MPIX_BENCH_BACKEND=gloo timeout -k 10 400 python3 -m torch.distributed.run \
+    --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 \
+    --steps 3 --warmup 1 --rsb-bytes 268435456 > $O/bench_n2_rehearsal.json 2> $O/bench_n2.err
+rc2=$?
+tail -c 1500 $O/bench_n2_rehearsal.json
+exit $((rc + rc2))
