@@ -63,7 +63,7 @@ def _gloo_exchange(group):
 def comm_for(group=None, device=True):
     """the libmpix_coll communicator of `group` for device (True) or host
     (False) buffers, created once per (group, kind)"""
-    key = (id(group), bool(device))
+    key = (group, bool(device))         # the group object itself: an id() could be reused
     c = _comms.get(key)
     if c is None:
         rank, size = dist.get_rank(group), dist.get_world_size(group)
@@ -136,6 +136,21 @@ def reduce_scatter_block(sendbuf, recvbuf, recvcount, datatype, op, group=None,
         if timer is not None:
             c.set_step_timing(False)
             timer.extend(c.step_times() if dev else [])
+    return recvbuf
+
+
+def reduce_scatter(sendbuf, recvbuf, recvcounts, datatype, op, group=None, algorithm='auto',
+                   combine=None, workspace=None):
+    """MPI_Reduce_scatter with per-rank recvcounts (zeros allowed); sendbuf
+    None is MPI_IN_PLACE.  Same schedules and rules as reduce_scatter_block."""
+    dev = _is_device(recvbuf, sendbuf)
+    if not dev and combine is None:
+        raise ValueError('host buffers need a combine function')
+    c = comm_for(group, dev)
+    c.set_combine(combine)
+    _order_after_torch(c, dev)
+    redop.check(ccl.reduce_scatter(sendbuf, recvbuf, list(recvcounts), datatype, op, c, algorithm,
+                                   workspace=workspace), 'MPIX_Reduce_scatter')
     return recvbuf
 
 

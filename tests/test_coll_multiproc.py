@@ -137,6 +137,54 @@ def test_staged_allreduce_matches_oracle(oracle, tmp_path, world):
     _run(oracle, tmp_path, world, 'gloo', cases)
 
 
+def _ragged_worker(rank, world, port, outdir):
+    """MPI_Reduce_scatter with ragged / empty per-rank counts and MPI_IN_PLACE
+    (reduce_scatter_intra_recursive_halving.c:38-262 / _pairwise.c:42-115)
+    over the staged transport, every algorithm"""
+    import torch.distributed as dist
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from mpich_amd import coll
+    counts = [0 if q == 1 else (q * 37 + 11) % 5 * 1000 + q for q in range(world)]
+    total = sum(counts)
+    send = np.random.default_rng(0x5EED0D00 + rank).uniform(-1, 1, total).astype(np.float32)
+    np.save(os.path.join(outdir, 'rg_send%d.npy' % rank), send)
+    for algo in ('recursive_halving', 'pairwise', 'pairwise_pipelined', 'pull'):
+        for in_place in (False, True):
+            ds = torch.from_numpy(send.copy()).cuda()
+            if in_place:
+                coll.reduce_scatter(None, ds, counts, MPI_FLOAT, MPI_SUM, algorithm=algo)
+                out = ds[:counts[rank]]
+            else:
+                out = torch.empty(max(counts[rank], 1), dtype=torch.float32, device='cuda')
+                coll.reduce_scatter(ds, out, counts, MPI_FLOAT, MPI_SUM, algorithm=algo)
+                out = out[:counts[rank]]
+            np.save(os.path.join(outdir, 'rg_%s_%d_%d.npy' % (algo, in_place, rank)),
+                    out.cpu().numpy())
+    dist.barrier()
+    coll.free_comms()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world', [3, 5])
+def test_staged_reduce_scatter_ragged_in_place(oracle, tmp_path, world):
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    mp.spawn(_ragged_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    counts = [0 if q == 1 else (q * 37 + 11) % 5 * 1000 + q for q in range(world)]
+    raw = [np.load(tmp_path / ('rg_send%d.npy' % r)).view(np.uint8) for r in range(world)]
+    exp_rh = oracle.rs_schedule(raw, counts, MPI_FLOAT, MPI_SUM, 'recursive_halving')
+    exp_pw = oracle.rs_schedule(raw, counts, MPI_FLOAT, MPI_SUM, 'pairwise')
+    for algo in ('recursive_halving', 'pairwise', 'pairwise_pipelined', 'pull'):
+        exp = exp_rh if algo == 'recursive_halving' else exp_pw
+        for in_place in (0, 1):
+            for r in range(world):
+                got = np.load(tmp_path / ('rg_%s_%d_%d.npy' % (algo, in_place, r)))
+                assert got.tobytes() == exp[r].tobytes(), (algo, in_place, r)
+
+
 def _config4_worker(rank, world, port, outdir, total_bytes):
     """BASELINE config 4's vector size on the staged transport: 2 ranks, a
     4 GiB fp32 vector each, recursive halving + HIP combine; each rank checks
