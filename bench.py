@@ -396,6 +396,7 @@ def single_gpu(args, dev):
             else (64 << 10, 1 << 20, 16 << 20))
         end_to_end(result, n)
         crossover = host_crossover_gpu(B)
+        result['configs_3_and_5'] = other_configs(inb, inout, n, stream)
     if args.sweep:
         result['sweep'] = size_sweep(inb, inout, n, stream, nbytes_alg)
     del inout, inb
@@ -415,6 +416,57 @@ def single_gpu(args, dev):
                      'crossover is the smallest size from which the GPU path is faster or within 5 % '
                      'at every larger size (the MPIX_Redop_is_supported_buffers floor)')
     print(json.dumps(result, default=str), flush=True)
+
+
+def other_configs(inb, inout, n, stream):
+    """BASELINE configs 3 and 5 on the same buffers (kernel-only, HIP events):
+    every supported (op, type) pair at 1 GiB per operand (past the 256 MB
+    MALL; min / median / max over the pairs, and the slowest three), and
+    vector(2^26, 1, 2, MPI_DOUBLE) SUM on a 1 GiB target span (algorithmic
+    bytes 3 x 512 MiB; physical floor 2.5 GiB)"""
+    nbytes = 4 * n
+    a8 = inout.view(torch.uint8)
+    b8 = inb.view(torch.uint8)
+    a8.view(torch.int8).random_(0, 3)      # small values: no NaN/Inf, no data-dependent paths
+    b8.view(torch.int8).random_(0, 3)
+    torch.cuda.synchronize()
+    rows = []
+    for tn in ('MPI_INT8_T', 'MPI_INT16_T', 'MPI_INT32_T', 'MPI_INT64_T', 'MPI_INTEGER16',
+               'MPIX_C_FLOAT16', 'MPIX_BFLOAT16', 'MPI_FLOAT', 'MPI_DOUBLE', 'MPI_COMPLEX4',
+               'MPI_C_FLOAT_COMPLEX', 'MPI_C_DOUBLE_COMPLEX', 'MPI_C_BOOL', 'MPI_LOGICAL', 'MPI_BYTE',
+               'MPI_2INT', 'MPI_FLOAT_INT', 'MPI_DOUBLE_INT', 'MPI_SHORT_INT'):
+        dt = getattr(H, tn)
+        ext = redop.datatype_extent(dt)
+        m = nbytes // ext
+        for on, op in H.OPS.items():
+            if op in (H.MPI_REPLACE, H.MPI_NO_OP) or not redop.is_supported(op, dt):
+                continue
+            redop.check(redop.reduce_local_async(b8, a8, m, dt, op, stream))
+            avg, _, _ = event_time_per_launch(
+                lambda: redop.check(redop.reduce_local_async(b8, a8, m, dt, op, stream)), 5, stream,
+                rounds=2)
+            rows.append((round(3 * m * ext / (avg * 1e-3) / 1e9, 1), tn, on))
+    rows.sort()
+    gbs = [r[0] for r in rows]
+    cnt = 1 << 26
+    src = inb.view(torch.float64)[:cnt]
+    dst = inout.view(torch.float64)[:2 * cnt]
+    src.zero_()
+    dst.zero_()
+    torch.cuda.synchronize()
+    redop.check(redop.reduce_local_vector(src, dst, cnt, 1, 2, H.MPI_DOUBLE, H.MPI_SUM, stream))
+    vavg, _, _ = event_time_per_launch(
+        lambda: redop.check(redop.reduce_local_vector(src, dst, cnt, 1, 2, H.MPI_DOUBLE, H.MPI_SUM,
+                                                      stream)), 10, stream)
+    return dict(
+        config3_per_pair_1GiB=dict(pairs=len(rows), min_GBs=gbs[0], median_GBs=gbs[len(gbs) // 2],
+                                   max_GBs=gbs[-1], min_frac=round(gbs[0] / HBM_PEAK_GBS, 4),
+                                   slowest=[dict(GBs=g, type=t, op=o) for g, t, o in rows[:3]]),
+        config5_vector=dict(kernel_ms=round(vavg, 4),
+                            GBs_algorithmic=round(3 * cnt * 8 / (vavg * 1e-3) / 1e9, 1),
+                            GBs_physical=round(2.5 * GIB / (vavg * 1e-3) / 1e9, 1),
+                            frac_algorithmic=round(3 * cnt * 8 / (vavg * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                                   4)))
 
 
 def end_to_end(result, n):
