@@ -288,6 +288,28 @@ __device__ __forceinline__ void st_payload_wt(T *p, const T &v)
     }
 }
 
+// Packed-source load of the stride-2 vector target, non-temporal for 4- and
+// 8-byte units (read once, never revisited): with the write-through payload
+// store +3.9 % over the default-policy source load at the same traffic
+// (profiles/r02_tune_vector2b.txt, tools/tune_vector2.hip S6 vs S1).
+template <typename T>
+__device__ __forceinline__ T ld_source_nt(const T *p)
+{
+    if constexpr (sizeof(T) == 8) {
+        unsigned long long u = __builtin_nontemporal_load(reinterpret_cast<const unsigned long long *>(p));
+        T v;
+        __builtin_memcpy(&v, &u, 8);
+        return v;
+    } else if constexpr (sizeof(T) == 4) {
+        unsigned int u = __builtin_nontemporal_load(reinterpret_cast<const unsigned int *>(p));
+        T v;
+        __builtin_memcpy(&v, &u, 4);
+        return v;
+    } else {
+        return *p;
+    }
+}
+
 template <class C>
 __global__ void __launch_bounds__(256)
 k_vector_s2(const typename C::unit *__restrict__ in, typename C::unit *__restrict__ io, uint64_t n,
@@ -304,7 +326,7 @@ k_vector_s2(const typename C::unit *__restrict__ in, typename C::unit *__restric
         } else {    // the last pair would reach one element past the type's span
             t = io[2 * j];
         }
-        st_payload_wt(io + 2 * j, C::apply(t, in[j], prm));
+        st_payload_wt(io + 2 * j, C::apply(t, ld_source_nt(in + j), prm));
     }
 }
 

@@ -93,6 +93,36 @@ __global__ void __launch_bounds__(256) k_s4(const double *__restrict__ in, doubl
     }
 }
 
+// S5 = S1's write-through store + S3's shape (2 pairs per lane at block stride, nt source)
+__global__ void __launch_bounds__(256) k_s5(const double *__restrict__ in, double *__restrict__ io,
+                                            uint64_t n)
+{
+    const uint64_t k0 = (uint64_t) blockIdx.x * 512 + threadIdx.x, k1 = k0 + 256;
+    d2 t0 = {0, 0}, t1 = {0, 0};
+    if (k0 < n)
+        t0 = reinterpret_cast<const d2 *>(io)[k0];
+    if (k1 < n)
+        t1 = reinterpret_cast<const d2 *>(io)[k1];
+    if (k0 < n)
+        __hip_atomic_store(io + 2 * k0, t0.x + __builtin_nontemporal_load(in + k0),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (k1 < n)
+        __hip_atomic_store(io + 2 * k1, t1.x + __builtin_nontemporal_load(in + k1),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// S6 = S1 with the source read non-temporally
+__global__ void __launch_bounds__(256) k_s6(const double *__restrict__ in, double *__restrict__ io,
+                                            uint64_t n)
+{
+    uint64_t k = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n)
+        return;
+    d2 t = reinterpret_cast<const d2 *>(io)[k];
+    __hip_atomic_store(io + 2 * k, t.x + __builtin_nontemporal_load(in + k), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 struct Var {
     std::string name;
     void (*launch)(const double *, double *, uint64_t, hipStream_t);
@@ -120,6 +150,15 @@ void s4(const double *in, double *io, uint64_t n, hipStream_t s)
     hipLaunchKernelGGL(k_s4, dim3((unsigned) ((n + 1023) / 1024)), dim3(256), 0, s, in, io, n);
 }
 
+void s5(const double *in, double *io, uint64_t n, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_s5, dim3((unsigned) ((n + 511) / 512)), dim3(256), 0, s, in, io, n);
+}
+void s6(const double *in, double *io, uint64_t n, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_s6, dim3((unsigned) ((n + 255) / 256)), dim3(256), 0, s, in, io, n);
+}
+
 int main()
 {
     const uint64_t n = 67108864;
@@ -130,7 +169,9 @@ int main()
     std::vector<Var> v = {{"S0 shipped k_vector_s2", s0, {}}, {"S1 write-through store", s1, {}},
                           {"S2 persistent grid 2048", s2, {}},
                           {"S3 2 pairs/lane, nt source", s3, {}},
-                          {"S4 LDS-staged 16 KiB tile", s4, {}}};
+                          {"S4 LDS-staged 16 KiB tile", s4, {}},
+                          {"S5 write-through + 2 pairs/lane + nt source", s5, {}},
+                          {"S6 write-through + nt source", s6, {}}};
     hipStream_t s;
     CK(hipStreamCreate(&s));
     // correctness first: every variant from the same start equals S0
