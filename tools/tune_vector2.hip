@@ -123,6 +123,43 @@ __global__ void __launch_bounds__(256) k_s6(const double *__restrict__ in, doubl
                        __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// S7 = S6 with the target pair loaded non-temporally too
+__global__ void __launch_bounds__(256) k_s7(const double *__restrict__ in, double *__restrict__ io,
+                                            uint64_t n)
+{
+    uint64_t k = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n)
+        return;
+    d2 t = __builtin_nontemporal_load(reinterpret_cast<const d2 *>(io) + k);
+    __hip_atomic_store(io + 2 * k, t.x + __builtin_nontemporal_load(in + k), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// S8 = S6 with 512-thread blocks; S9 = S6 with 1024-thread blocks (same kernel body)
+template <int B>
+__global__ void __launch_bounds__(1024) k_s8(const double *__restrict__ in, double *__restrict__ io,
+                                             uint64_t n)
+{
+    uint64_t k = (uint64_t) blockIdx.x * B + threadIdx.x;
+    if (k >= n)
+        return;
+    d2 t = reinterpret_cast<const d2 *>(io)[k];
+    __hip_atomic_store(io + 2 * k, t.x + __builtin_nontemporal_load(in + k), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// S10 = S6 with the target loaded as relaxed system-scope atomics (sc0 sc1 loads)
+__global__ void __launch_bounds__(256) k_s10(const double *__restrict__ in, double *__restrict__ io,
+                                             uint64_t n)
+{
+    uint64_t k = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n)
+        return;
+    double t = __hip_atomic_load(io + 2 * k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(io + 2 * k, t + __builtin_nontemporal_load(in + k), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 struct Var {
     std::string name;
     void (*launch)(const double *, double *, uint64_t, hipStream_t);
@@ -159,6 +196,20 @@ void s6(const double *in, double *io, uint64_t n, hipStream_t s)
     hipLaunchKernelGGL(k_s6, dim3((unsigned) ((n + 255) / 256)), dim3(256), 0, s, in, io, n);
 }
 
+void s7(const double *in, double *io, uint64_t n, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_s7, dim3((unsigned) ((n + 255) / 256)), dim3(256), 0, s, in, io, n);
+}
+template <int B>
+void s8(const double *in, double *io, uint64_t n, hipStream_t s)
+{
+    hipLaunchKernelGGL((k_s8<B>), dim3((unsigned) ((n + B - 1) / B)), dim3(B), 0, s, in, io, n);
+}
+void s10(const double *in, double *io, uint64_t n, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_s10, dim3((unsigned) ((n + 255) / 256)), dim3(256), 0, s, in, io, n);
+}
+
 int main()
 {
     const uint64_t n = 67108864;
@@ -171,7 +222,11 @@ int main()
                           {"S3 2 pairs/lane, nt source", s3, {}},
                           {"S4 LDS-staged 16 KiB tile", s4, {}},
                           {"S5 write-through + 2 pairs/lane + nt source", s5, {}},
-                          {"S6 write-through + nt source", s6, {}}};
+                          {"S6 write-through + nt source", s6, {}},
+                          {"S7 S6 + nt target load", s7, {}},
+                          {"S8 S6 with 512-thread blocks", s8<512>, {}},
+                          {"S9 S6 with 1024-thread blocks", s8<1024>, {}},
+                          {"S10 S6 with sc0 sc1 payload-only target load", s10, {}}};
     hipStream_t s;
     CK(hipStreamCreate(&s));
     // correctness first: every variant from the same start equals S0
