@@ -347,6 +347,39 @@ def test_custom_transport_and_symbols(oracle):
     assert c.free() == 0
 
 
+@pytest.mark.parametrize('P', [1, 2, 5])
+def test_barrier_and_custom_memory_kinds(oracle, P):
+    """MPIX_Comm_barrier: every rank leaves only after every rank entered (host
+    transport); MPIX_Comm_create_custom rejects an unknown memory kind; the
+    step timer is inert on host communicators"""
+    from mpich_amd import ccl
+    import time
+    comms = host_comms(P, oracle)
+    entered = [None] * P
+
+    def body(r, c):
+        time.sleep(0.05 * r)            # arrive in turn
+        entered[r] = time.monotonic()
+        c.barrier()
+        left = time.monotonic()
+        c.set_step_timing(True)
+        assert ccl.reduce_scatter_block(np.zeros(P, np.float32), np.zeros(1, np.float32), 1,
+                                        MPI_FLOAT, MPI_SUM, c, 'recursive_halving') == 0
+        c.set_step_timing(False)
+        return left, c.step_times()
+    out = run_ranks(comms, body)
+    assert all(left >= max(entered) for left, _ in out)
+    assert all(st == [] for _, st in out)
+    free_all(comms)
+    L = ccl.lib()
+    h = ctypes.c_void_p()
+    XFN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                           ctypes.c_int, ctypes.c_void_p)
+    fn = XFN(lambda *a: 0)
+    assert L.MPIX_Comm_create_custom(0, 1, ctypes.cast(fn, ctypes.c_void_p), None, 3,
+                                     ctypes.byref(h)) == 12     # MPI_ERR_ARG
+
+
 # ------------------------------------------------------------------ GPU
 def _dev_comms(P):
     from mpich_amd import ccl
