@@ -688,7 +688,7 @@ def rsb_secondary(args, world, rank, dev, out):
     fill_uniform(send, 0x5EED0100 + rank)
     recv = torch.empty(recvcount, dtype=torch.float32, device=dev)
     torch.cuda.synchronize()
-    for algo in ('pairwise', 'pairwise_pipelined', 'pull'):
+    for algo in ('recursive_halving_multipath', 'pairwise', 'pairwise_pipelined', 'pull'):
         rc_small = 4096 + 3
         blk = torch.cat([torch.full((rc_small,), rank + i, dtype=torch.int32, device=dev)
                          for i in range(world)])
@@ -714,10 +714,20 @@ def rsb_secondary(args, world, rank, dev, out):
         torch.cuda.synchronize()
         dist.barrier()
         t = allreduce_scalar((time.perf_counter() - t0) / reps, dist.ReduceOp.MAX, dev)
-        link_bytes = total * 4 / world              # one block per peer link, all links at once
+        if algo == 'recursive_halving_multipath':
+            # every directed link of a rank carries 1/(P/2) of each step's half
+            pof2 = 1
+            while pof2 * 2 <= world:
+                pof2 *= 2
+            mp = pof2 >= 4 and pof2 == world
+            link_bytes = (pof2 - 1) / pof2 * total * 4 / (world // 2 if mp else 1)
+            links = world - 1 if mp else 1
+        else:
+            link_bytes = total * 4 / world          # one block per peer link, all links at once
+            links = world - 1
         out[algo] = dict(parity_redscatblk3_all_ranks=True, ms=round(t * 1e3, 3),
                          busbw_GBs=round((world - 1) / world * total * 4 / t / 1e9, 2),
-                         per_link_GBs=round(link_bytes / t / 1e9, 2), links_active=world - 1,
+                         per_link_GBs=round(link_bytes / t / 1e9, 2), links_active=links,
                          frac_of_xgmi_link=round(link_bytes / t / 1e9 / XGMI_LINK_GBS, 4))
     del send, recv
     torch.cuda.empty_cache()

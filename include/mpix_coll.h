@@ -133,7 +133,17 @@ int MPIX_Comm_free(MPIX_Comm comm);
                                            reading).  Device buffers from hipMalloc; a host
                                            communicator, or a buffer some rank cannot export,
                                            runs PAIRWISE instead (same bits) */
-#define MPIX_RSB_LAST               MPIX_RSB_PULL
+#define MPIX_RSB_RECURSIVE_HALVING_MULTIPATH 6  /* RECURSIVE_HALVING's schedule and association
+                                           (same bits), each step's exchange routed over all
+                                           xGMI links: with P a power of two >= 4 and equal
+                                           blocks, a step's half is cut into P/2 parts, one sent
+                                           to the partner directly and each other relayed
+                                           through a distinct third rank (first hop on link
+                                           r^a, second on link r^(a^m)), the relay hops
+                                           pipelined in chunks; every directed link of every
+                                           rank carries 1/(P/2) of the half.  Other shapes run
+                                           RECURSIVE_HALVING */
+#define MPIX_RSB_LAST               MPIX_RSB_RECURSIVE_HALVING_MULTIPATH
 size_t MPIX_Reduce_scatter_block_workspace(MPIX_Aint recvcount, MPIX_Datatype datatype,
                                            MPIX_Comm comm, int algorithm);
 int MPIX_Reduce_scatter_block(const void *sendbuf, void *recvbuf, MPIX_Aint recvcount,

@@ -21,10 +21,11 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libmpix_col
 UNIQUE_ID_BYTES = 128
 
 RSB_AUTO, RSB_RECURSIVE_HALVING, RSB_PAIRWISE, RSB_PAIRWISE_SEQUENTIAL = 0, 1, 2, 3
-RSB_PAIRWISE_PIPELINED, RSB_PULL = 4, 5
+RSB_PAIRWISE_PIPELINED, RSB_PULL, RSB_RECURSIVE_HALVING_MULTIPATH = 4, 5, 6
 RSB_ALGORITHMS = {'auto': RSB_AUTO, 'recursive_halving': RSB_RECURSIVE_HALVING,
                   'pairwise': RSB_PAIRWISE, 'pairwise_sequential': RSB_PAIRWISE_SEQUENTIAL,
-                  'pairwise_pipelined': RSB_PAIRWISE_PIPELINED, 'pull': RSB_PULL}
+                  'pairwise_pipelined': RSB_PAIRWISE_PIPELINED, 'pull': RSB_PULL,
+                  'recursive_halving_multipath': RSB_RECURSIVE_HALVING_MULTIPATH}
 XPORT_DEVICE, XPORT_HOST, XPORT_STAGED = 0, 1, 2
 AR_AUTO, AR_RECURSIVE_DOUBLING, AR_RSAG, AR_RSAG_RD, AR_RING = 0, 1, 2, 3, 4
 AR_ALGORITHMS = {'auto': AR_AUTO, 'recursive_doubling': AR_RECURSIVE_DOUBLING,

@@ -651,6 +651,126 @@ int rs_recursive_halving(const char *sb, char *rb, const std::vector<size_t> &cn
     return MPIX_REDOP_SUCCESS;
 }
 
+// True when the multipath recursive halving applies: P a power of two >= 4
+// and equal blocks (every rank's half has the same size at every step, so a
+// relay knows what it forwards without a size exchange).
+bool multipath_shape(const std::vector<size_t> &cnts, int size)
+{
+    if (size < 4 || (size & (size - 1)))
+        return false;
+    for (size_t n : cnts)
+        if (n != cnts[0])
+            return false;
+    return true;
+}
+
+// relay masks of a step with mask m: one of every pair {a, a ^ m}, a != m
+// (the smaller), so first hops (r ^ a) and second hops (r ^ a ^ m) together
+// use each of the other P - 2 links once
+std::vector<int> relay_masks(int m, int size)
+{
+    std::vector<int> A;
+    for (int a = 1; a < size; ++a)
+        if (a != m && a < (a ^ m))
+            A.push_back(a);
+    return A;
+}
+
+size_t multipath_relay_bytes(size_t recvcount, size_t ext, int size)
+{
+    return (size_t) (size / 2 - 1) * round256(recvcount * ext);
+}
+
+// MPIX_RSB_RECURSIVE_HALVING_MULTIPATH: rs_recursive_halving's schedule with
+// each exchange step spread over every link.  Step with mask m: rank r's
+// half (D elements, D = m * recvcount) is cut into n = P/2 parts; part 0 goes
+// to the partner r ^ m directly, part j to the relay r ^ a_j, which forwards
+// it to its own r ^ a_j ^ m = the partner.  Every rank is at once source,
+// relay for the ranks r ^ a_j and destination of its partner's relayed
+// parts, so all P - 1 directed links of every rank carry D / n.  The relay
+// hops are pipelined in C chunks per part: group g moves direct and first-hop
+// chunk g and forwards chunk g - 1.  The partner's half lands in tmp_recvbuf
+// exactly where rs_recursive_halving receives it, and one combine per step
+// folds it in: same operands, same order, same bits.
+int rs_recursive_halving_multipath(const char *sb, char *rb, const std::vector<size_t> &cnts,
+                                   MPIX_Datatype dt, MPIX_Op op, MPIX_Comm c, char *ws,
+                                   hipStream_t s, size_t ext)
+{
+    const int rank = c->rank, size = c->size;
+    const size_t rc = cnts[0], total = rc * size;
+    char *tmp_results = ws;
+    char *tmp_recvbuf = ws + round256(total * ext);
+    char *relay = tmp_recvbuf + round256(total * ext);     // (P/2 - 1) part slots
+    const size_t slot = round256(rc * ext);
+    TRY(mark(c, "start", s));
+    TRY(copy(c, tmp_results, sb, total * ext, s));                         // :91-96
+    TRY(mark(c, "local copy", s));
+    int mask = size >> 1, send_idx = 0, recv_idx = 0, last_idx = size;
+    while (mask > 0) {
+        const int dst = rank ^ mask;
+        if (rank < dst) {
+            send_idx = recv_idx + mask;
+        } else {
+            recv_idx = send_idx + mask;
+        }
+        const size_t D = (size_t) mask * rc;             // both halves, every rank
+        const std::vector<int> A = relay_masks(mask, size);
+        const size_t n = A.size() + 1;
+        auto lo = [&](size_t j) { return D * j / n; };   // part j: [lo(j), lo(j+1))
+        const char *sbase = tmp_results + (size_t) send_idx * rc * ext;
+        char *rbase = tmp_recvbuf + (size_t) recv_idx * rc * ext;
+        // chunks per part: >= 4 MiB each, at most 8 (one group when small)
+        const size_t part_bytes = (lo(1) - lo(0)) * ext;
+        size_t C = part_bytes >> 22;
+        C = C < 1 ? 1 : (C > 8 ? 8 : C);
+        for (size_t g = 0; g <= C; ++g) {
+            std::vector<MPIX_P2p_op> ops;
+            auto piece = [&](size_t j, size_t k, size_t *off, size_t *len) {
+                const size_t pl = lo(j + 1) - lo(j);
+                const size_t a = pl * k / C, b = pl * (k + 1) / C;
+                *off = lo(j) + a;
+                *len = b - a;
+            };
+            if (g < C) {
+                size_t off, len;
+                piece(0, g, &off, &len);
+                ops.push_back(snd(dst, sbase + off * ext, len * ext));
+                ops.push_back(rcv(dst, rbase + off * ext, len * ext));
+                for (size_t j = 1; j < n; ++j) {
+                    const int a = A[j - 1];
+                    piece(j, g, &off, &len);
+                    const size_t roff = off - lo(j);          // within the relay slot
+                    ops.push_back(snd(rank ^ a, sbase + off * ext, len * ext));
+                    ops.push_back(rcv(rank ^ a, relay + (j - 1) * slot + roff * ext, len * ext));
+                }
+            }
+            if (g > 0) {
+                for (size_t j = 1; j < n; ++j) {
+                    const int a = A[j - 1];
+                    size_t off, len;
+                    piece(j, g - 1, &off, &len);
+                    const size_t roff = off - lo(j);
+                    ops.push_back(snd(rank ^ a ^ mask, relay + (j - 1) * slot + roff * ext,
+                                      len * ext));
+                    ops.push_back(rcv(rank ^ a ^ mask, rbase + off * ext, len * ext));
+                }
+            }
+            TRY(exchange(c, ops, s));
+        }
+        TRY(mark(c, "exchange", s));
+        TRY(combine(c, rbase, tmp_results + (size_t) recv_idx * rc * ext, (MPIX_Aint) D, dt, op,
+                    s));
+        TRY(mark(c, "combine", s));
+        send_idx = recv_idx;
+        last_idx = recv_idx + mask;
+        mask >>= 1;
+    }
+    (void) last_idx;
+    TRY(copy(c, rb, tmp_results + (size_t) rank * rc * ext, rc * ext, s));   // :232-240
+    TRY(mark(c, "epilogue", s));
+    return MPIX_REDOP_SUCCESS;
+}
+
 // MPIR_Reduce_scatter_intra_pairwise (reduce_scatter_intra_pairwise.c:42-115;
 // the _block variant …_block_intra_pairwise.c:42-104 with equal counts):
 // step i = 1..P-1 sends block (rank+i) to rank+i and folds the block
@@ -933,6 +1053,9 @@ size_t rs_workspace(size_t total, size_t mine, size_t ext, int size, int algo)
     switch (algo) {
         case MPIX_RSB_RECURSIVE_HALVING:
             return 2 * round256(total * ext);
+        case MPIX_RSB_RECURSIVE_HALVING_MULTIPATH:   // + the relay slots (total = size * mine)
+            return 2 * round256(total * ext) +
+                   (total == mine * (size_t) size ? multipath_relay_bytes(mine, ext, size) : 0);
         case MPIX_RSB_PAIRWISE:
         case MPIX_RSB_PAIRWISE_PIPELINED:
             return (size - 1) * round256(mine * ext);
@@ -1424,6 +1547,8 @@ int rs_entry(const void *sendbuf, void *recvbuf, const std::vector<size_t> &cnts
     char *rb = static_cast<char *>(recvbuf);
     const char *sb = sendbuf ? static_cast<const char *>(sendbuf) : rb;
     int algo = rs_choose(algorithm, total * ext);
+    if (algo == MPIX_RSB_RECURSIVE_HALVING_MULTIPATH && !multipath_shape(cnts, c->size))
+        algo = MPIX_RSB_RECURSIVE_HALVING;
     if (c->size == 1)
         return finish(c, sendbuf ? copy(c, rb, sb, cnts[0] * ext, s) : MPIX_REDOP_SUCCESS, s,
                       blocking);
@@ -1433,6 +1558,8 @@ int rs_entry(const void *sendbuf, void *recvbuf, const std::vector<size_t> &cnts
         return finish(c, rs_pull(sb, rb, cnts, dt, op, c, s, ext), s, blocking);
     int rc = algo == MPIX_RSB_RECURSIVE_HALVING
                  ? rs_recursive_halving(sb, rb, cnts, dt, op, c, w, s, ext)
+             : algo == MPIX_RSB_RECURSIVE_HALVING_MULTIPATH
+                 ? rs_recursive_halving_multipath(sb, rb, cnts, dt, op, c, w, s, ext)
                  : algo == MPIX_RSB_PAIRWISE_PIPELINED
                        ? rs_pairwise_pipelined(sb, rb, cnts, dt, op, c, w, s, ext)
                        : rs_pairwise(sb, rb, cnts, dt, op, c, w, s, ext, algo == MPIX_RSB_PAIRWISE);

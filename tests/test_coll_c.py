@@ -87,7 +87,32 @@ def test_rsb_host_matches_oracle_schedule(oracle, P, algo):
         assert recvs[r].tobytes() == exp[r].tobytes(), r
 
 
-@pytest.mark.parametrize('algo', ['recursive_halving', 'pairwise', 'auto'])
+@pytest.mark.parametrize('recvcount', [1, 7, 1001, (1 << 24) // 4 + 5])
+@pytest.mark.parametrize('P', [2, 3, 4, 8, 16])
+def test_rsb_multipath_host_matches_recursive_halving(oracle, P, recvcount):
+    """MPIX_RSB_RECURSIVE_HALVING_MULTIPATH: the recursive-halving schedule
+    with every step's half spread over all links through relays (P a power of
+    two >= 4; other P fall back to plain recursive halving) -- bit-identical
+    to the oracle's recursive-halving simulation, also with blocks large
+    enough for the relay hops to be pipelined in several chunks"""
+    from mpich_amd import ccl
+    if recvcount > 100000 and P > 8:
+        pytest.skip('large blocks at P = 2..8 only (memory)')
+    sends = float_sends(P, P * recvcount, seed=0x5EED0E00)
+    recvs = [np.zeros(recvcount, np.float32) for _ in range(P)]
+    comms = host_comms(P, oracle)
+    rcs = run_ranks(comms, lambda r, c: ccl.reduce_scatter_block(
+        sends[r], recvs[r], recvcount, MPI_FLOAT, MPI_SUM, c, 'recursive_halving_multipath'))
+    free_all(comms)
+    assert rcs == [0] * P
+    exp = oracle.rsb_recursive_halving([s.view(np.uint8) for s in sends], recvcount, MPI_FLOAT,
+                                       MPI_SUM)
+    for r in range(P):
+        assert recvs[r].tobytes() == exp[r].tobytes(), r
+
+
+@pytest.mark.parametrize('algo', ['recursive_halving', 'pairwise', 'auto',
+                                  'recursive_halving_multipath'])
 @pytest.mark.parametrize('P', [2, 3, 4, 6, 8])
 def test_rsb_host_redscatblk3(oracle, P, algo):
     """redscatblk3.c:43-56: block i of rank r holds r + i; the result on rank
@@ -387,7 +412,8 @@ def _dev_comms(P):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('algo', ['recursive_halving', 'pairwise', 'pairwise_sequential'])
+@pytest.mark.parametrize('algo', ['recursive_halving', 'pairwise', 'pairwise_sequential',
+                                  'recursive_halving_multipath'])
 @pytest.mark.parametrize('P', [2, 3, 4, 8])
 def test_rsb_device_local_matches_oracle(oracle, P, algo):
     import torch

@@ -89,7 +89,7 @@ def _check(oracle, tmp_path, world, cases):
         sends = [np.load(tmp_path / ('%s_send%d.npy' % (name, r))) for r in range(world)]
         dt, op = (MPI_FLOAT, MPI_SUM) if kind == 'float' else (MPI_2INT, MPI_MAXLOC)
         raw = [s.view(np.uint8) for s in sends]
-        if algo == 'recursive_halving':
+        if algo.startswith('recursive_halving'):
             exp = oracle.rsb_recursive_halving(raw, recvcount, dt, op)
         elif algo.startswith('allreduce'):
             exp = oracle.allreduce_rabenseifner(raw, world * recvcount, dt, op)
@@ -106,7 +106,7 @@ def _run(oracle, tmp_path, world, backend, cases):
     _check(oracle, tmp_path, world, cases)
 
 
-ALGOS = ('recursive_halving', 'pairwise', 'pairwise_pipelined', 'pull')
+ALGOS = ('recursive_halving', 'pairwise', 'pairwise_pipelined', 'pull', 'recursive_halving_multipath')
 
 
 @pytest.mark.parametrize('world', [2, 3, 4, 8])
