@@ -760,10 +760,22 @@ def allreduce_secondary(args, world, rank, dev, res):
                       lambda: redop.check(ccl.allreduce(send, recv, n, H.MPI_FLOAT, H.MPI_SUM, cc,
                                                         'reduce_scatter_allgather', workspace=ws),
                                           'MPIX_Allreduce')),
+                     ('c_rsag_multipath',
+                      lambda: redop.check(ccl.allreduce(send, recv, n, H.MPI_FLOAT, H.MPI_SUM, cc,
+                                                        'rsag_multipath', workspace=ws),
+                                          'MPIX_Allreduce')),
                      ('rccl_all_reduce', lambda: (recv.copy_(send), dist.all_reduce(recv)))):
         if name == 'rccl_all_reduce' and dist.get_backend() != 'nccl':
             continue
         fn()
+        if name == 'c_reduce_scatter_allgather':
+            ref = recv.clone()
+        elif name == 'c_rsag_multipath':    # same association, so the same bits
+            same = bool(torch.equal(recv.view(torch.int32), ref.view(torch.int32)))
+            if not allreduce_scalar(1 if same else 0, dist.ReduceOp.MIN, dev):
+                raise RuntimeError('rsag_multipath allreduce differs from reduce_scatter_allgather')
+            res['rsag_multipath_bit_identical_all_ranks'] = True
+            del ref
         reps = max(3, min(10, args.steps))
         dist.barrier()
         torch.cuda.synchronize()

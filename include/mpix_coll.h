@@ -213,6 +213,11 @@ int MPIX_Exscan_async(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_
 #define MPIX_ALLREDUCE_RSAG_RD_ALLGATHER    3   /* the reference's log2(P) allgather steps */
 #define MPIX_ALLREDUCE_RING                 4   /* allreduce_intra_ring.c: ring reduce-scatter
                                                    (P-1 steps) + allgather of the blocks */
+#define MPIX_ALLREDUCE_RSAG_MULTIPATH       5   /* REDUCE_SCATTER_ALLGATHER with every
+                                                   reduce-scatter step spread over all links
+                                                   through relays (P a power of two >= 4,
+                                                   count a multiple of P; else plain steps);
+                                                   same bits */
 size_t MPIX_Allreduce_workspace(MPIX_Aint count, MPIX_Datatype datatype, MPIX_Comm comm);
 int MPIX_Allreduce(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Datatype datatype,
                    MPIX_Op op, MPIX_Comm comm, int algorithm, void *workspace,

@@ -27,10 +27,10 @@ RSB_ALGORITHMS = {'auto': RSB_AUTO, 'recursive_halving': RSB_RECURSIVE_HALVING,
                   'pairwise_pipelined': RSB_PAIRWISE_PIPELINED, 'pull': RSB_PULL,
                   'recursive_halving_multipath': RSB_RECURSIVE_HALVING_MULTIPATH}
 XPORT_DEVICE, XPORT_HOST, XPORT_STAGED = 0, 1, 2
-AR_AUTO, AR_RECURSIVE_DOUBLING, AR_RSAG, AR_RSAG_RD, AR_RING = 0, 1, 2, 3, 4
+AR_AUTO, AR_RECURSIVE_DOUBLING, AR_RSAG, AR_RSAG_RD, AR_RING, AR_RSAG_MULTIPATH = 0, 1, 2, 3, 4, 5
 AR_ALGORITHMS = {'auto': AR_AUTO, 'recursive_doubling': AR_RECURSIVE_DOUBLING,
                  'reduce_scatter_allgather': AR_RSAG, 'rsag_rd_allgather': AR_RSAG_RD,
-                 'ring': AR_RING}
+                 'ring': AR_RING, 'rsag_multipath': AR_RSAG_MULTIPATH}
 
 _lib = None
 

@@ -191,7 +191,8 @@ def allreduce(sendbuf, recvbuf, count, datatype, op, group=None, combine=None, w
     allgather 'direct' = one group of P-1 direct exchanges, 'recursive_doubling'
     = the reference's log2(P) steps (:191-226); same bits either way.
     algorithm overrides: auto | recursive_doubling | reduce_scatter_allgather |
-    rsag_rd_allgather | ring.  sendbuf None = MPI_IN_PLACE."""
+    rsag_rd_allgather | ring | rsag_multipath (each reduce-scatter step over
+    every link through relays; same bits).  sendbuf None = MPI_IN_PLACE."""
     if algorithm is None:
         if allgather not in ('direct', 'recursive_doubling'):
             raise ValueError('allgather must be direct or recursive_doubling')

@@ -681,17 +681,63 @@ size_t multipath_relay_bytes(size_t recvcount, size_t ext, int size)
     return (size_t) (size / 2 - 1) * round256(recvcount * ext);
 }
 
+// One exchange step of a recursive-halving schedule routed over every link
+// (P a power of two >= 4, the same D elements moving each way between every
+// rank r and its partner r ^ mask).  Rank r's D elements at sbase are cut into
+// n = P/2 parts: part 0 goes to the partner directly, part j to the relay
+// r ^ a_j, which forwards it to its own r ^ a_j ^ mask = the partner.  Every
+// rank is at once source, relay for the ranks r ^ a_j and destination of its
+// partner's relayed parts, so all P - 1 directed links of every rank carry
+// D / n.  The relay hops are pipelined in C chunks per part: group g moves
+// direct and first-hop chunk g and forwards chunk g - 1.  The partner's D
+// elements land at rbase exactly as one direct receive would leave them.
+// relay: (P/2 - 1) slots of `slot` bytes (>= one part).
+int multipath_exchange(MPIX_Comm c, const char *sbase, char *rbase, size_t D, int mask, char *relay,
+                       size_t slot, hipStream_t s, size_t ext)
+{
+    const int rank = c->rank;
+    const std::vector<int> A = relay_masks(mask, c->size);
+    const size_t n = A.size() + 1;
+    auto lo = [&](size_t j) { return D * j / n; };   // part j: [lo(j), lo(j+1))
+    // chunks per part: >= 4 MiB each, at most 8 (one group when small)
+    size_t C = ((lo(1) - lo(0)) * ext) >> 22;
+    C = C < 1 ? 1 : (C > 8 ? 8 : C);
+    auto piece = [&](size_t j, size_t k, size_t *off, size_t *len) {
+        const size_t pl = lo(j + 1) - lo(j);
+        const size_t a = pl * k / C, b = pl * (k + 1) / C;
+        *off = lo(j) + a;
+        *len = b - a;
+    };
+    for (size_t g = 0; g <= C; ++g) {
+        std::vector<MPIX_P2p_op> ops;
+        size_t off, len;
+        if (g < C) {
+            piece(0, g, &off, &len);
+            ops.push_back(snd(rank ^ mask, sbase + off * ext, len * ext));
+            ops.push_back(rcv(rank ^ mask, rbase + off * ext, len * ext));
+            for (size_t j = 1; j < n; ++j) {
+                piece(j, g, &off, &len);
+                ops.push_back(snd(rank ^ A[j - 1], sbase + off * ext, len * ext));
+                ops.push_back(rcv(rank ^ A[j - 1], relay + (j - 1) * slot + (off - lo(j)) * ext,
+                                  len * ext));
+            }
+        }
+        if (g > 0) {
+            for (size_t j = 1; j < n; ++j) {
+                piece(j, g - 1, &off, &len);
+                ops.push_back(snd(rank ^ A[j - 1] ^ mask,
+                                  relay + (j - 1) * slot + (off - lo(j)) * ext, len * ext));
+                ops.push_back(rcv(rank ^ A[j - 1] ^ mask, rbase + off * ext, len * ext));
+            }
+        }
+        TRY(exchange(c, ops, s));
+    }
+    return MPIX_REDOP_SUCCESS;
+}
+
 // MPIX_RSB_RECURSIVE_HALVING_MULTIPATH: rs_recursive_halving's schedule with
-// each exchange step spread over every link.  Step with mask m: rank r's
-// half (D elements, D = m * recvcount) is cut into n = P/2 parts; part 0 goes
-// to the partner r ^ m directly, part j to the relay r ^ a_j, which forwards
-// it to its own r ^ a_j ^ m = the partner.  Every rank is at once source,
-// relay for the ranks r ^ a_j and destination of its partner's relayed
-// parts, so all P - 1 directed links of every rank carry D / n.  The relay
-// hops are pipelined in C chunks per part: group g moves direct and first-hop
-// chunk g and forwards chunk g - 1.  The partner's half lands in tmp_recvbuf
-// exactly where rs_recursive_halving receives it, and one combine per step
-// folds it in: same operands, same order, same bits.
+// every exchange step spread over all links (multipath_exchange), then one
+// combine per step into tmp_results: same operands, same order, same bits.
 int rs_recursive_halving_multipath(const char *sb, char *rb, const std::vector<size_t> &cnts,
                                    MPIX_Datatype dt, MPIX_Op op, MPIX_Comm c, char *ws,
                                    hipStream_t s, size_t ext)
@@ -701,71 +747,27 @@ int rs_recursive_halving_multipath(const char *sb, char *rb, const std::vector<s
     char *tmp_results = ws;
     char *tmp_recvbuf = ws + round256(total * ext);
     char *relay = tmp_recvbuf + round256(total * ext);     // (P/2 - 1) part slots
-    const size_t slot = round256(rc * ext);
+    const size_t slot = round256(rc * ext);                 // a part is at most one block
     TRY(mark(c, "start", s));
     TRY(copy(c, tmp_results, sb, total * ext, s));                         // :91-96
     TRY(mark(c, "local copy", s));
-    int mask = size >> 1, send_idx = 0, recv_idx = 0, last_idx = size;
+    int mask = size >> 1, send_idx = 0, recv_idx = 0;
     while (mask > 0) {
-        const int dst = rank ^ mask;
-        if (rank < dst) {
+        if (rank < (rank ^ mask))
             send_idx = recv_idx + mask;
-        } else {
+        else
             recv_idx = send_idx + mask;
-        }
         const size_t D = (size_t) mask * rc;             // both halves, every rank
-        const std::vector<int> A = relay_masks(mask, size);
-        const size_t n = A.size() + 1;
-        auto lo = [&](size_t j) { return D * j / n; };   // part j: [lo(j), lo(j+1))
-        const char *sbase = tmp_results + (size_t) send_idx * rc * ext;
         char *rbase = tmp_recvbuf + (size_t) recv_idx * rc * ext;
-        // chunks per part: >= 4 MiB each, at most 8 (one group when small)
-        const size_t part_bytes = (lo(1) - lo(0)) * ext;
-        size_t C = part_bytes >> 22;
-        C = C < 1 ? 1 : (C > 8 ? 8 : C);
-        for (size_t g = 0; g <= C; ++g) {
-            std::vector<MPIX_P2p_op> ops;
-            auto piece = [&](size_t j, size_t k, size_t *off, size_t *len) {
-                const size_t pl = lo(j + 1) - lo(j);
-                const size_t a = pl * k / C, b = pl * (k + 1) / C;
-                *off = lo(j) + a;
-                *len = b - a;
-            };
-            if (g < C) {
-                size_t off, len;
-                piece(0, g, &off, &len);
-                ops.push_back(snd(dst, sbase + off * ext, len * ext));
-                ops.push_back(rcv(dst, rbase + off * ext, len * ext));
-                for (size_t j = 1; j < n; ++j) {
-                    const int a = A[j - 1];
-                    piece(j, g, &off, &len);
-                    const size_t roff = off - lo(j);          // within the relay slot
-                    ops.push_back(snd(rank ^ a, sbase + off * ext, len * ext));
-                    ops.push_back(rcv(rank ^ a, relay + (j - 1) * slot + roff * ext, len * ext));
-                }
-            }
-            if (g > 0) {
-                for (size_t j = 1; j < n; ++j) {
-                    const int a = A[j - 1];
-                    size_t off, len;
-                    piece(j, g - 1, &off, &len);
-                    const size_t roff = off - lo(j);
-                    ops.push_back(snd(rank ^ a ^ mask, relay + (j - 1) * slot + roff * ext,
-                                      len * ext));
-                    ops.push_back(rcv(rank ^ a ^ mask, rbase + off * ext, len * ext));
-                }
-            }
-            TRY(exchange(c, ops, s));
-        }
+        TRY(multipath_exchange(c, tmp_results + (size_t) send_idx * rc * ext, rbase, D, mask,
+                               relay, slot, s, ext));
         TRY(mark(c, "exchange", s));
         TRY(combine(c, rbase, tmp_results + (size_t) recv_idx * rc * ext, (MPIX_Aint) D, dt, op,
                     s));
         TRY(mark(c, "combine", s));
         send_idx = recv_idx;
-        last_idx = recv_idx + mask;
         mask >>= 1;
     }
-    (void) last_idx;
     TRY(copy(c, rb, tmp_results + (size_t) rank * rc * ext, rc * ext, s));   // :232-240
     TRY(mark(c, "epilogue", s));
     return MPIX_REDOP_SUCCESS;
@@ -1091,8 +1093,12 @@ int bitrev(int r, int pof2)
 // (allreduce_intra_reduce_scatter_allgather.c:41-277); `direct` replaces the
 // log2(P) allgather exchanges (:191-226) by one group of P-1 direct ones --
 // the allgather only moves finished blocks, so the bits do not change.
+// `multipath` (MPIX_ALLREDUCE_RSAG_MULTIPATH) routes each reduce-scatter step
+// over every link (multipath_exchange) when P is a power of two >= 4 and the
+// blocks are equal; the relay slots live in tmp's half that the step does not
+// receive into (never read again), so the workspace stays count elements.
 int allreduce_rsag(char *rb, size_t count, MPIX_Datatype dt, MPIX_Op op, MPIX_Comm c, char *tmp,
-                   hipStream_t s, size_t ext, bool direct)
+                   hipStream_t s, size_t ext, bool direct, bool multipath = false)
 {
     const int rank = c->rank, size = c->size;
     const int pof2 = pof2_of(size), rem = size - pof2;
@@ -1136,8 +1142,18 @@ int allreduce_rsag(char *rb, size_t count, MPIX_Datatype dt, MPIX_Op op, MPIX_Co
                 send_cnt = sum(send_idx, recv_idx);
                 recv_cnt = sum(recv_idx, last_idx);
             }
-            TRY(exchange(c, {snd(real(newdst), rb + disps[send_idx] * ext, send_cnt * ext),
-                             rcv(real(newdst), tmp + disps[recv_idx] * ext, recv_cnt * ext)}, s));
+            const size_t parts = (size_t) pof2 / 2;
+            if (multipath && rem == 0 && pof2 >= 4 && count % pof2 == 0 &&
+                send_cnt >= parts * (parts - 1)) {
+                // send_cnt == recv_cnt here; relay slots fit in send_cnt elements
+                const size_t slot = (send_cnt + parts - 1) / parts * ext;
+                TRY(multipath_exchange(c, rb + disps[send_idx] * ext, tmp + disps[recv_idx] * ext,
+                                       send_cnt, mask, tmp + disps[send_idx] * ext, slot, s, ext));
+            } else {
+                TRY(exchange(c, {snd(real(newdst), rb + disps[send_idx] * ext, send_cnt * ext),
+                                 rcv(real(newdst), tmp + disps[recv_idx] * ext, recv_cnt * ext)},
+                             s));
+            }
             TRY(combine(c, tmp + disps[recv_idx] * ext, rb + disps[recv_idx] * ext,
                         (MPIX_Aint) recv_cnt, dt, op, s));
             send_idx = recv_idx;
@@ -1598,7 +1614,7 @@ int allreduce_entry(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Da
 {
     size_t ext;
     TRY(check_args(c, recvbuf, count, dt, op, &ext));
-    if (algorithm < MPIX_ALLREDUCE_AUTO || algorithm > MPIX_ALLREDUCE_RING)
+    if (algorithm < MPIX_ALLREDUCE_AUTO || algorithm > MPIX_ALLREDUCE_RSAG_MULTIPATH)
         return MPIX_REDOP_ERR_ARG;
     if (!count)
         return MPIX_REDOP_SUCCESS;
@@ -1612,7 +1628,8 @@ int allreduce_entry(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Da
                         ? MPIX_ALLREDUCE_REDUCE_SCATTER_ALLGATHER
                         : MPIX_ALLREDUCE_RECURSIVE_DOUBLING;
     if ((algorithm == MPIX_ALLREDUCE_REDUCE_SCATTER_ALLGATHER ||
-         algorithm == MPIX_ALLREDUCE_RSAG_RD_ALLGATHER) && (size_t) count < (size_t) pof2)
+         algorithm == MPIX_ALLREDUCE_RSAG_RD_ALLGATHER ||
+         algorithm == MPIX_ALLREDUCE_RSAG_MULTIPATH) && (size_t) count < (size_t) pof2)
         return MPIX_REDOP_ERR_COUNT;    // :127
     if (algorithm != MPIX_ALLREDUCE_RECURSIVE_DOUBLING && splits_message_forbidden(op))
         return MPIX_REDOP_ERR_OP;       // MPIR_Allreduce_equal uses recursive doubling only
@@ -1627,7 +1644,8 @@ int allreduce_entry(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Da
              : algorithm == MPIX_ALLREDUCE_RING
                  ? allreduce_ring(rb, (size_t) count, dt, op, c, tmp, s, ext)
                  : allreduce_rsag(rb, (size_t) count, dt, op, c, tmp, s, ext,
-                                  algorithm == MPIX_ALLREDUCE_REDUCE_SCATTER_ALLGATHER);
+                                  algorithm != MPIX_ALLREDUCE_RSAG_RD_ALLGATHER,
+                                  algorithm == MPIX_ALLREDUCE_RSAG_MULTIPATH);
     return finish(c, release_scratch(c, tmp, rc, s), s, blocking);
 }
 

@@ -15,6 +15,7 @@ hand-offs) and the HIP combine, all ranks on cuda:0 -- the same schedules
 with the product kernels, bit-identical to the oracle's simulation.
 """
 import ctypes
+import os
 import threading
 
 import numpy as np
@@ -132,7 +133,7 @@ def test_rsb_host_redscatblk3(oracle, P, algo):
 
 
 @pytest.mark.parametrize('algo', ['reduce_scatter_allgather', 'rsag_rd_allgather',
-                                  'recursive_doubling', 'ring'])
+                                  'recursive_doubling', 'ring', 'rsag_multipath'])
 @pytest.mark.parametrize('P', [1, 2, 3, 4, 7, 8, 12, 16])
 def test_allreduce_host_matches_oracle_and_kats(oracle, P, algo):
     from mpich_amd import ccl
@@ -203,6 +204,71 @@ def test_allreduce_ring_ragged_and_auto_rule(oracle, P):
         for r in range(P):
             assert outs[r].view(np.uint8).tobytes() == exp[r].tobytes(), (count, r)
     free_all(comms)
+
+
+@pytest.mark.parametrize('P,count', [(4, 4096), (8, 4096), (16, 4096), (8, 1 << 22),
+                                     (4, 4098), (8, 8), (6, 4096)])
+def test_allreduce_rsag_multipath_matches_oracle(oracle, P, count):
+    """MPIX_ALLREDUCE_RSAG_MULTIPATH: every reduce-scatter step spread over all
+    links through relays when P is a power of two >= 4 and count a multiple
+    of P (chunked relay hops at 16 MiB); ragged counts, tiny counts and
+    non-power-of-two P run the plain steps -- same bits in every case"""
+    from mpich_amd import ccl
+    sends = float_sends(P, count, 0x5EED0A00 + count)
+    outs = [np.zeros(count, np.float32) for _ in range(P)]
+    comms = host_comms(P, oracle)
+    rcs = run_ranks(comms, lambda r, c: ccl.allreduce(sends[r], outs[r], count, MPI_FLOAT,
+                                                       MPI_SUM, c, 'rsag_multipath'))
+    free_all(comms)
+    assert rcs == [0] * P
+    exp = oracle.allreduce_rabenseifner([s.view(np.uint8) for s in sends], count, MPI_FLOAT,
+                                        MPI_SUM, algorithm='reduce_scatter_allgather')
+    for r in range(P):
+        assert outs[r].tobytes() == exp[r].tobytes(), r
+
+
+def test_allreduce_rsag_multipath_uses_every_link(oracle):
+    """the exchange trace (MPIX_COLL_TRACE) of rank 0 at P = 8: the multipath
+    reduce-scatter steps post to all 7 peers, the plain ones to one partner"""
+    import subprocess
+    import sys
+    code = r'''
+import threading, numpy as np
+from mpich_amd import ccl, handles as H
+from oracle import oracle as O
+import sys
+P, count, algo = 8, 4096, sys.argv[1]
+comms = ccl.comm_create_local(P)
+for c in comms:
+    c.set_combine(O.combine_fn_address())
+sends = [np.full(count, r, np.float32) for r in range(P)]
+outs = [np.zeros(count, np.float32) for _ in range(P)]
+ts = [threading.Thread(target=lambda r=r: ccl.allreduce(sends[r], outs[r], count, H.MPI_FLOAT,
+                                                         H.MPI_SUM, comms[r], algo))
+      for r in range(P)]
+[t.start() for t in ts]
+[t.join() for t in ts]
+assert all(np.all(o == 28) for o in outs)
+'''
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    peers = {}
+    for algo in ('reduce_scatter_allgather', 'rsag_multipath'):
+        p = subprocess.run([sys.executable, '-c', code, algo], capture_output=True, text=True,
+                           cwd=root, env=dict(os.environ, MPIX_COLL_TRACE='1'), timeout=120)
+        assert p.returncode == 0, p.stderr[-3000:]
+        lines = [ln for ln in p.stderr.splitlines() if ln.startswith('[mpix_coll rank 0/8]')]
+        steps = [{int(t[1:].split(':')[0]) for t in ln.split(']')[1].split()} for ln in lines]
+        peers[algo] = steps
+    # plain: 3 reduce-scatter steps with one partner each, one allgather group to all
+    assert [len(s) for s in peers['reduce_scatter_allgather']] == [1, 1, 1, 7]
+    # multipath (one chunk at this size): per step, the partner and the 3
+    # relays first, then the 3 relayed second hops -- all 7 links per step
+    rs = peers['rsag_multipath'][:-1]
+    assert len(rs) == 6, peers['rsag_multipath']
+    for k in range(3):
+        assert len(rs[2 * k]) == 4 and len(rs[2 * k + 1]) == 3
+        assert len(rs[2 * k] | rs[2 * k + 1]) == 7
+    assert len(peers['rsag_multipath'][-1]) == 7
 
 
 def test_in_place_allreduce_and_workspace(oracle):
@@ -468,7 +534,7 @@ def test_rsb_device_local_types(oracle, dt, op, algo):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize('algo', ['reduce_scatter_allgather', 'rsag_rd_allgather',
-                                  'recursive_doubling', 'ring'])
+                                  'recursive_doubling', 'ring', 'rsag_multipath'])
 @pytest.mark.parametrize('P', [2, 3, 4, 7, 8])
 def test_allreduce_device_local_matches_oracle(oracle, P, algo):
     import torch

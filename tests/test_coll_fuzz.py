@@ -78,7 +78,7 @@ def test_reduce_scatter_random(oracle, P, case, algo, in_place, data, seed):
 @SETTINGS
 @given(P=st.integers(1, 12), case=st.sampled_from(CASES),
        algo=st.sampled_from(['reduce_scatter_allgather', 'rsag_rd_allgather',
-                             'recursive_doubling', 'ring']),
+                             'recursive_doubling', 'ring', 'rsag_multipath']),
        count=st.integers(1, 200), seed=st.integers(0, 2**31))
 def test_allreduce_random(oracle, P, case, algo, count, seed):
     from mpich_amd import ccl
@@ -183,7 +183,7 @@ def test_reduce_scatter_random_device(oracle, P, case, algo, in_place, data, see
 @GPU_SETTINGS
 @given(P=st.integers(2, 8), case=st.sampled_from(CASES),
        algo=st.sampled_from(['reduce_scatter_allgather', 'rsag_rd_allgather',
-                             'recursive_doubling', 'ring']),
+                             'recursive_doubling', 'ring', 'rsag_multipath']),
        count=st.integers(1, 20000), seed=st.integers(0, 2**31))
 def test_allreduce_random_device(oracle, P, case, algo, count, seed):
     import torch

@@ -65,7 +65,9 @@ def _worker(rank, world, port, outdir, backend, cases):
         if algo.startswith('allreduce'):
             dr = torch.empty_like(ds)
             coll.allreduce(ds, dr, world * recvcount, dt, op,
-                           allgather='recursive_doubling' if algo.endswith('_rd') else 'direct')
+                           algorithm={'allreduce': 'reduce_scatter_allgather',
+                                      'allreduce_rd': 'rsag_rd_allgather',
+                                      'allreduce_mp': 'rsag_multipath'}[algo])
         else:
             dr = torch.empty(recvcount * ext, dtype=torch.uint8, device='cuda')
             timer = [] if algo == 'recursive_halving' else None
@@ -133,7 +135,8 @@ def test_staged_pipelined_large_blocks(oracle, tmp_path):
 def test_staged_allreduce_matches_oracle(oracle, tmp_path, world):
     if not torch.cuda.is_available():
         pytest.skip('no GPU')
-    cases = [('ar', 'allreduce', 'float', 25013), ('ar_rd', 'allreduce_rd', 'float', 25013)]
+    cases = [('ar', 'allreduce', 'float', 25013), ('ar_rd', 'allreduce_rd', 'float', 25013),
+             ('ar_mp', 'allreduce_mp', 'float', 2 << 20)]    # P=4: 8 MiB parts, 2 relay chunks
     _run(oracle, tmp_path, world, 'gloo', cases)
 
 
@@ -259,4 +262,5 @@ def test_rccl_rsb_matches_oracle(oracle, tmp_path):
     cases = [('%s_%s' % (a, k), a, k, 100003 if k == 'float' else 50021)
              for a in ALGOS for k in ('float', 'pair')]
     cases.append(('ar', 'allreduce', 'float', 25013))
+    cases.append(('ar_mp', 'allreduce_mp', 'float', 25013))
     _run(oracle, tmp_path, world, 'nccl', cases)

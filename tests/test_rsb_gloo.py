@@ -153,6 +153,9 @@ def _ar_worker(rank, world, port, outdir, count, algo='reduce_scatter_allgather'
     combine = orc.combine_fn_address()
     if algo == 'recursive_doubling':
         fn = coll.allreduce_recursive_doubling
+    elif algo == 'rsag_multipath':
+        def fn(*a, **k):
+            return coll.allreduce(*a, algorithm='rsag_multipath', **k)
     else:   # second phase: one group of direct sends, or the reference's exchanges
         ag = 'recursive_doubling' if algo == 'rsag_rd_allgather' else 'direct'
 
@@ -182,14 +185,14 @@ def _ar_worker(rank, world, port, outdir, count, algo='reduce_scatter_allgather'
 
 
 @pytest.mark.parametrize('algo', ['reduce_scatter_allgather', 'rsag_rd_allgather',
-                                  'recursive_doubling'])
+                                  'recursive_doubling', 'rsag_multipath'])
 @pytest.mark.parametrize('world', [2, 3, 4, 7, 8])
 def test_allreduce_gloo(oracle, tmp_path, world, algo):
     """Rabenseifner allreduce over gloo (direct or the reference's
     recursive-doubling allgather): bit-identical on every rank to the
     oracle's simulation of the reference schedule, and all allred.c KATs
     generated for this world size pass end to end."""
-    count = 1037
+    count = 4096 if algo == 'rsag_multipath' else 1037    # multipath: P | count
     mp.spawn(_ar_worker, args=(world, _free_port(), str(tmp_path), count, algo), nprocs=world,
              join=True)
     sends = [np.load(tmp_path / ('send%d.npy' % r)) for r in range(world)]
