@@ -130,3 +130,98 @@ extern "C" int mpix_bench_chunked_async(void *fn, const void *in, void *io, int6
     *total_s = std::chrono::duration<double>(c - a).count();
     return 0;
 }
+
+__global__ void k_empty(int *p)
+{
+    if (p && threadIdx.x == 0 && blockIdx.x == 0 && p[0] == 12345)
+        p[1] = 0;
+}
+
+struct Args72 {
+    uint64_t w[9];
+};
+
+__global__ void k_empty72(const float *a, float *b, uint64_t c, uint64_t d, uint64_t e,
+                          uint32_t f, Args72 g)
+{
+    if (a && threadIdx.x == 0 && blockIdx.x == 0 && f == 12345u && g.w[0] == c + d + e)
+        b[0] = a[0];
+}
+
+// Where the per-call host cost of an asynchronous reduce goes: mean host
+// microseconds of (0) hipPointerGetAttributes on a device pointer, (1)
+// hipPointerGetAttribute(MEMORY_TYPE), (2) issuing an empty kernel
+// back to back, (3) issuing `fn` (MPIX_Reduce_local_async) back to back at
+// `count`, (4) an empty kernel + hipStreamSynchronize round trip, (5) `fn` +
+// hipStreamSynchronize round trip, (6) issuing an empty kernel with the
+// contiguous kernel's 112-byte argument block.  out[7] holds the figures.
+extern "C" int mpix_bench_launch_floor(void *fn, const void *in, void *io, int64_t count, int dt,
+                                       int op, void *stream, int reps, double *out)
+{
+    if (!fn || reps < 1 || !out)
+        return 12;
+    async_reduce_fn f = (async_reduce_fn) fn;
+    hipStream_t s = (hipStream_t) stream;
+    using clk = std::chrono::steady_clock;
+    auto us = [&](clk::time_point a, clk::time_point b) {
+        return std::chrono::duration<double, std::micro>(b - a).count() / reps;
+    };
+    hipPointerAttribute_t attr;
+    auto a = clk::now();
+    for (int i = 0; i < reps; ++i)
+        if (hipPointerGetAttributes(&attr, io) != hipSuccess)
+            return 15;
+    out[0] = us(a, clk::now());
+    unsigned int mt = 0;
+    a = clk::now();
+    for (int i = 0; i < reps; ++i)
+        if (hipPointerGetAttribute(&mt, HIP_POINTER_ATTRIBUTE_MEMORY_TYPE, (hipDeviceptr_t) io) !=
+            hipSuccess)
+            return 15;
+    out[1] = us(a, clk::now());
+    for (int pass = 0; pass < 2; ++pass) {      // pass 0 warms the launch path up
+        if (hipStreamSynchronize(s) != hipSuccess)
+            return 15;
+        a = clk::now();
+        for (int i = 0; i < reps; ++i)
+            hipLaunchKernelGGL(k_empty, dim3(1), dim3(64), 0, s, (int *) nullptr);
+        out[2] = us(a, clk::now());
+        if (hipStreamSynchronize(s) != hipSuccess)
+            return 15;
+        a = clk::now();
+        for (int i = 0; i < reps; ++i)
+            if (int rc = f(in, io, count, dt, op, stream))
+                return rc;
+        out[3] = us(a, clk::now());
+        if (hipStreamSynchronize(s) != hipSuccess)
+            return 15;
+    }
+    a = clk::now();
+    for (int i = 0; i < reps; ++i) {
+        hipLaunchKernelGGL(k_empty, dim3(1), dim3(64), 0, s, (int *) nullptr);
+        if (hipStreamSynchronize(s) != hipSuccess)
+            return 15;
+    }
+    out[4] = us(a, clk::now());
+    a = clk::now();
+    for (int i = 0; i < reps; ++i) {
+        if (int rc = f(in, io, count, dt, op, stream))
+            return rc;
+        if (hipStreamSynchronize(s) != hipSuccess)
+            return 15;
+    }
+    out[5] = us(a, clk::now());
+    Args72 g{};
+    for (int pass = 0; pass < 2; ++pass) {
+        if (hipStreamSynchronize(s) != hipSuccess)
+            return 15;
+        a = clk::now();
+        for (int i = 0; i < reps; ++i)
+            hipLaunchKernelGGL(k_empty72, dim3(1), dim3(64), 0, s, (const float *) in, (float *) io,
+                               (uint64_t) 1, (uint64_t) 2, (uint64_t) 3, 4u, g);
+        out[6] = us(a, clk::now());
+    }
+    if (hipStreamSynchronize(s) != hipSuccess)
+        return 15;
+    return 0;
+}
