@@ -688,6 +688,13 @@ def rsb_secondary(args, world, rank, dev, out):
     fill_uniform(send, 0x5EED0100 + rank)
     recv = torch.empty(recvcount, dtype=torch.float32, device=dev)
     torch.cuda.synchronize()
+    # full-size bit references: multipath must reproduce recursive halving's
+    # bits, pipelined pairwise and pull those of pairwise (same association)
+    redop.check(ccl.reduce_scatter_block(send, recv, recvcount, H.MPI_FLOAT, H.MPI_SUM, cc,
+                                         'recursive_halving'), 'MPIX_Reduce_scatter_block')
+    refs = {'recursive_halving': recv.clone()}
+    same_as = {'recursive_halving_multipath': 'recursive_halving', 'pairwise_pipelined': 'pairwise',
+               'pull': 'pairwise'}
     for algo in ('recursive_halving_multipath', 'pairwise', 'pairwise_pipelined', 'pull'):
         rc_small = 4096 + 3
         blk = torch.cat([torch.full((rc_small,), rank + i, dtype=torch.int32, device=dev)
@@ -705,6 +712,14 @@ def rsb_secondary(args, world, rank, dev, out):
             redop.check(ccl.reduce_scatter_block(send, recv, recvcount, H.MPI_FLOAT, H.MPI_SUM, cc,
                                                  algo), 'MPIX_Reduce_scatter_block')
         once()
+        bits = None
+        if algo == 'pairwise':
+            refs['pairwise'] = recv.clone()
+        elif algo in same_as:
+            same = bool(torch.equal(recv.view(torch.int32), refs[same_as[algo]].view(torch.int32)))
+            if not allreduce_scalar(1 if same else 0, dist.ReduceOp.MIN, dev):
+                raise RuntimeError('%s RSB differs from %s at the timed size' % (algo, same_as[algo]))
+            bits = same_as[algo]
         reps = max(3, min(10, args.steps))
         dist.barrier()
         torch.cuda.synchronize()
@@ -726,10 +741,11 @@ def rsb_secondary(args, world, rank, dev, out):
             link_bytes = total * 4 / world          # one block per peer link, all links at once
             links = world - 1
         out[algo] = dict(parity_redscatblk3_all_ranks=True, ms=round(t * 1e3, 3),
+                         bit_identical_to=bits,
                          busbw_GBs=round((world - 1) / world * total * 4 / t / 1e9, 2),
                          per_link_GBs=round(link_bytes / t / 1e9, 2), links_active=links,
                          frac_of_xgmi_link=round(link_bytes / t / 1e9 / XGMI_LINK_GBS, 4))
-    del send, recv
+    del send, recv, refs
     torch.cuda.empty_cache()
 
 
