@@ -694,8 +694,9 @@ def rsb_secondary(args, world, rank, dev, out):
                                          'recursive_halving'), 'MPIX_Reduce_scatter_block')
     refs = {'recursive_halving': recv.clone()}
     same_as = {'recursive_halving_multipath': 'recursive_halving', 'pairwise_pipelined': 'pairwise',
-               'pull': 'pairwise'}
-    for algo in ('recursive_halving_multipath', 'pairwise', 'pairwise_pipelined', 'pull'):
+               'pull': 'pairwise', 'recursive_halving_pull': 'recursive_halving'}
+    for algo in ('recursive_halving_multipath', 'recursive_halving_pull', 'pairwise',
+                 'pairwise_pipelined', 'pull'):
         rc_small = 4096 + 3
         blk = torch.cat([torch.full((rc_small,), rank + i, dtype=torch.int32, device=dev)
                          for i in range(world)])
@@ -737,8 +738,8 @@ def rsb_secondary(args, world, rank, dev, out):
             mp = pof2 >= 4 and pof2 == world
             link_bytes = (pof2 - 1) / pof2 * total * 4 / (world // 2 if mp else 1)
             links = world - 1 if mp else 1
-        else:
-            link_bytes = total * 4 / world          # one block per peer link, all links at once
+        else:   # pairwise family and the pulls: one block per peer link, all links at once
+            link_bytes = total * 4 / world
             links = world - 1
         out[algo] = dict(parity_redscatblk3_all_ranks=True, ms=round(t * 1e3, 3),
                          bit_identical_to=bits,

@@ -143,7 +143,15 @@ int MPIX_Comm_free(MPIX_Comm comm);
                                            pipelined in chunks; every directed link of every
                                            rank carries 1/(P/2) of the half.  Other shapes run
                                            RECURSIVE_HALVING */
-#define MPIX_RSB_LAST               MPIX_RSB_RECURSIVE_HALVING_MULTIPATH
+#define MPIX_RSB_RECURSIVE_HALVING_PULL 7  /* RECURSIVE_HALVING's association (same bits)
+                                           computed by the pull of MPIX_RSB_PULL: every rank
+                                           maps its peers' send buffers and ONE tree kernel
+                                           (MPIX_Reduce_local_tree_async) reads its block of
+                                           all P ranks over xGMI and folds them level by level
+                                           as the log2(P) halving steps would, writing recvbuf
+                                           directly.  P a power of two <= 16 and a device
+                                           communicator; otherwise RECURSIVE_HALVING */
+#define MPIX_RSB_LAST               MPIX_RSB_RECURSIVE_HALVING_PULL
 size_t MPIX_Reduce_scatter_block_workspace(MPIX_Aint recvcount, MPIX_Datatype datatype,
                                            MPIX_Comm comm, int algorithm);
 int MPIX_Reduce_scatter_block(const void *sendbuf, void *recvbuf, MPIX_Aint recvcount,

@@ -22,10 +22,12 @@ UNIQUE_ID_BYTES = 128
 
 RSB_AUTO, RSB_RECURSIVE_HALVING, RSB_PAIRWISE, RSB_PAIRWISE_SEQUENTIAL = 0, 1, 2, 3
 RSB_PAIRWISE_PIPELINED, RSB_PULL, RSB_RECURSIVE_HALVING_MULTIPATH = 4, 5, 6
+RSB_RECURSIVE_HALVING_PULL = 7
 RSB_ALGORITHMS = {'auto': RSB_AUTO, 'recursive_halving': RSB_RECURSIVE_HALVING,
                   'pairwise': RSB_PAIRWISE, 'pairwise_sequential': RSB_PAIRWISE_SEQUENTIAL,
                   'pairwise_pipelined': RSB_PAIRWISE_PIPELINED, 'pull': RSB_PULL,
-                  'recursive_halving_multipath': RSB_RECURSIVE_HALVING_MULTIPATH}
+                  'recursive_halving_multipath': RSB_RECURSIVE_HALVING_MULTIPATH,
+                  'recursive_halving_pull': RSB_RECURSIVE_HALVING_PULL}
 XPORT_DEVICE, XPORT_HOST, XPORT_STAGED = 0, 1, 2
 AR_AUTO, AR_RECURSIVE_DOUBLING, AR_RSAG, AR_RSAG_RD, AR_RING, AR_RSAG_MULTIPATH = 0, 1, 2, 3, 4, 5
 AR_ALGORITHMS = {'auto': AR_AUTO, 'recursive_doubling': AR_RECURSIVE_DOUBLING,

@@ -115,7 +115,8 @@ def reduce_scatter_block(sendbuf, recvbuf, recvcount, datatype, op, group=None,
     sendbuf holds size*recvcount elements, recvbuf recvcount; sendbuf None is
     MPI_IN_PLACE (recvbuf holds the inputs, the result lands in its first
     block).  algorithm: recursive_halving | pairwise | pairwise_sequential |
-    pairwise_pipelined | pull | auto.  combine: C combine address for host
+    pairwise_pipelined | pull | recursive_halving_multipath |
+    recursive_halving_pull | auto.  combine: C combine address for host
     buffers (no CPU compute path here).  timer: a list that receives the
     per-step breakdown [{'phase', 'ms'}] of this call (device buffers).
     Raises RedopError on an MPI error class."""

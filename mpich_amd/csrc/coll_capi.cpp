@@ -898,6 +898,7 @@ int rs_pairwise_pipelined(const char *sb, char *rb, const std::vector<size_t> &c
 }
 
 size_t rs_workspace(size_t total, size_t mine, size_t ext, int size, int algo);
+int bitrev(int r, int pof2);
 
 // What a rank publishes for MPIX_RSB_PULL: the buffer its peers read, as an
 // IPC handle + offset into its allocation (another process) or as the raw
@@ -949,8 +950,16 @@ int peer_base(MPIX_Comm c, const PullRec &r, hipStream_t s, const char **out)
 // …_intra_pairwise.c:86-100 (i = 1..P-1, source rank - i), i.e. the bits of
 // PAIRWISE; a closing barrier on the stream keeps every rank from reusing its
 // buffer before all peers have pulled from it.
+//
+// tree (MPIX_RSB_RECURSIVE_HALVING_PULL, P a power of two): the same pull,
+// but the kernel folds the P blocks as recursive halving's steps would
+// (MPIX_Reduce_local_tree_async with slot s = rank ^ bitrev(s): the first
+// step's partner rank ^ P/2 in slot 1, …recursive_halving.c:164-229), writing
+// the result straight into recvbuf: the bits of RECURSIVE_HALVING, with every
+// link busy at once and one read of each block instead of log2(P) exchange +
+// combine rounds.
 int rs_pull(const char *sb, char *rb, const std::vector<size_t> &cnts, MPIX_Datatype dt, MPIX_Op op,
-            MPIX_Comm c, hipStream_t s, size_t ext)
+            MPIX_Comm c, hipStream_t s, size_t ext, bool tree = false)
 {
     const int rank = c->rank, size = c->size;
     std::vector<size_t> disps(size, 0);
@@ -959,18 +968,21 @@ int rs_pull(const char *sb, char *rb, const std::vector<size_t> &cnts, MPIX_Data
     size_t total = 0;
     for (size_t n : cnts)
         total += n;
-    auto fallback = [&]() -> int {     // same bits: the one-group pairwise schedule
+    auto fallback = [&]() -> int {     // same bits: one-group pairwise / recursive halving
+        const int alg = tree ? MPIX_RSB_RECURSIVE_HALVING : MPIX_RSB_PAIRWISE;
         char *w;
-        TRY(workspace(c, nullptr, 0, rs_workspace(total, cnts[rank], ext, size, MPIX_RSB_PAIRWISE),
-                      s, &w));
-        return release_scratch(c, w, rs_pairwise(sb, rb, cnts, dt, op, c, w, s, ext, true), s);
+        TRY(workspace(c, nullptr, 0, rs_workspace(total, cnts[rank], ext, size, alg), s, &w));
+        return release_scratch(c, w,
+                               tree ? rs_recursive_halving(sb, rb, cnts, dt, op, c, w, s, ext)
+                                    : rs_pairwise(sb, rb, cnts, dt, op, c, w, s, ext, true),
+                               s);
     };
-    if (c->host() || c->combine)
+    if (c->host() || c->combine || (tree && (size & (size - 1))) || size > 16)
         return fallback();
     const size_t blk = cnts[rank] * ext;
     const bool in_place = sb == rb;
     char *acc = in_place ? rb + disps[rank] * ext : rb;
-    if (!in_place)
+    if (!in_place && !tree)
         TRY(copy(c, rb, sb + disps[rank] * ext, blk, s));                   // :58-64
     PullRec me;
     memset(&me, 0, sizeof me);
@@ -1007,14 +1019,26 @@ int rs_pull(const char *sb, char *rb, const std::vector<size_t> &cnts, MPIX_Data
     if (!ok)
         return fallback();
     std::vector<const void *> ins;
-    for (int i = 1; i < size; ++i) {
-        const int src = (rank - i + size) % size;
-        const char *base;
-        TRY(peer_base(c, recs[src], s, &base));
-        ins.push_back(base + disps[rank] * ext);
+    if (tree) {
+        for (int q = 0; q < size; ++q) {
+            const int src = rank ^ bitrev(q, size);
+            const char *base = sb;
+            if (src != rank)
+                TRY(peer_base(c, recs[src], s, &base));
+            ins.push_back(base + disps[rank] * ext);
+        }
+    } else {
+        for (int i = 1; i < size; ++i) {
+            const int src = (rank - i + size) % size;
+            const char *base;
+            TRY(peer_base(c, recs[src], s, &base));
+            ins.push_back(base + disps[rank] * ext);
+        }
     }
     TRY(mark(c, "publish", s));
-    if (cnts[rank])
+    if (cnts[rank] && tree)
+        TRY(MPIX_Reduce_local_tree_async(ins.data(), size, acc, (MPIX_Aint) cnts[rank], dt, op, s));
+    else if (cnts[rank])
         TRY(combine_multi(c, ins, acc, (MPIX_Aint) cnts[rank], dt, op, s));
     TRY(mark(c, "pull+combine", s));
     TRY(barrier(c, s));                 // peers done reading this rank's buffer
@@ -1063,6 +1087,8 @@ size_t rs_workspace(size_t total, size_t mine, size_t ext, int size, int algo)
             return (size - 1) * round256(mine * ext);
         case MPIX_RSB_PAIRWISE_SEQUENTIAL:
             return round256(mine * ext);
+        case MPIX_RSB_RECURSIVE_HALVING_PULL:       // other P run RECURSIVE_HALVING
+            return ((size & (size - 1)) || size > 16) ? 2 * round256(total * ext) : 0;
         default:
             return 0;
     }
@@ -1565,13 +1591,17 @@ int rs_entry(const void *sendbuf, void *recvbuf, const std::vector<size_t> &cnts
     int algo = rs_choose(algorithm, total * ext);
     if (algo == MPIX_RSB_RECURSIVE_HALVING_MULTIPATH && !multipath_shape(cnts, c->size))
         algo = MPIX_RSB_RECURSIVE_HALVING;
+    if (algo == MPIX_RSB_RECURSIVE_HALVING_PULL && ((c->size & (c->size - 1)) || c->size > 16))
+        algo = MPIX_RSB_RECURSIVE_HALVING;
     if (c->size == 1)
         return finish(c, sendbuf ? copy(c, rb, sb, cnts[0] * ext, s) : MPIX_REDOP_SUCCESS, s,
                       blocking);
     char *w;
     TRY(workspace(c, ws, ws_bytes, rs_workspace(total, cnts[c->rank], ext, c->size, algo), s, &w));
-    if (algo == MPIX_RSB_PULL)
-        return finish(c, rs_pull(sb, rb, cnts, dt, op, c, s, ext), s, blocking);
+    if (algo == MPIX_RSB_PULL || algo == MPIX_RSB_RECURSIVE_HALVING_PULL)
+        return finish(c, rs_pull(sb, rb, cnts, dt, op, c, s, ext,
+                                 algo == MPIX_RSB_RECURSIVE_HALVING_PULL),
+                      s, blocking);
     int rc = algo == MPIX_RSB_RECURSIVE_HALVING
                  ? rs_recursive_halving(sb, rb, cnts, dt, op, c, w, s, ext)
              : algo == MPIX_RSB_RECURSIVE_HALVING_MULTIPATH

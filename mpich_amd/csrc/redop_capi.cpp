@@ -1366,6 +1366,54 @@ int MPIX_Reduce_local_multi_async(const void *const *inbufs, int ninputs, void *
                                     launch_cfg(), (hipStream_t) stream)));
 }
 
+int MPIX_Reduce_local_tree_async(const void *const *inbufs, int ninputs, void *outbuf,
+                                 MPIX_Aint count, MPIX_Datatype datatype, MPIX_Op op, void *stream)
+{
+    if (ninputs < 2 || ninputs > mpix::kMaxMultiInputs || (ninputs & (ninputs - 1)) || !inbufs)
+        return set_err(MPIX_REDOP_ERR_ARG);
+    uint32_t it;
+    uint64_t ext;
+    // outbuf may be inbufs[0] itself (each element is read before it is
+    // written, by the same lane); any other overlap is refused
+    for (int q = 0; q < ninputs; ++q) {
+        const bool same = q == 0 && inbufs[0] == (const void *) outbuf;
+        int rc = validate(same ? (const void *) ((const char *) outbuf + 1) : inbufs[q], outbuf,
+                          same ? 0 : count, (uint32_t) datatype, (uint32_t) op, &it, &ext);
+        if (rc == MPIX_REDOP_SUCCESS && same && count > 0 &&
+            (uint64_t) count > ((uint64_t) 1 << 56) / ext)
+            rc = MPIX_REDOP_ERR_COUNT;
+        if (rc == MPIX_REDOP_SUCCESS && same && count > 0 &&
+            (!outbuf || outbuf == (void *) -1))
+            rc = MPIX_REDOP_ERR_BUFFER;
+        if (rc != MPIX_REDOP_SUCCESS)
+            return set_err(rc);
+    }
+    if (count == 0)
+        return set_err(MPIX_REDOP_SUCCESS);
+    uint32_t opi = (uint32_t) op & 0xf;
+    if (opi == 15)
+        return set_err(MPIX_REDOP_ERR_OP);      // EQUAL is never split or folded
+    const void *dins[mpix::kMaxMultiInputs];
+    const void *pout;
+    if (!device_accessible(outbuf, &pout))
+        return set_err(MPIX_REDOP_ERR_BUFFER);
+    for (int q = 0; q < ninputs; ++q)
+        if (!device_accessible(inbufs[q], &dins[q]))
+            return set_err(MPIX_REDOP_ERR_BUFFER);
+    if (opi == 13 || opi == 14) {   // REPLACE folds to the last slot, NO_OP to the first
+        const void *src = dins[opi == 13 ? ninputs - 1 : 0];
+        if (src == pout)
+            return set_err(MPIX_REDOP_SUCCESS);
+        return set_err(replace_rows((void *) pout, ext, src, ext, (uint64_t) count, it, ext,
+                                    (hipStream_t) stream));
+    }
+    const Entry *e = gpu_entry(opi, it);
+    if (!e || !e->tree)
+        return set_err(MPIX_REDOP_ERR_TYPE);
+    return set_err(hip_err(e->tree(dins, ninputs, (void *) pout, (uint64_t) count, params(),
+                                   launch_cfg(), (hipStream_t) stream)));
+}
+
 int MPIX_Ipc_export(const void *devptr, void *handle_out, MPIX_Aint *offset_out)
 {
     if (!devptr || !handle_out || !offset_out)

@@ -41,6 +41,8 @@ struct Entry {
     hipError_t (*iov)(const void *in, void *io, const int64_t *d_seg_off, const int64_t *d_prefix,
                       const int64_t *d_src_off, int64_t nseg, uint64_t total, const Params &,
                       const LaunchCfg &, hipStream_t);
+    hipError_t (*tree)(const void *const *ins, int k, void *out, uint64_t count, const Params &,
+                       const LaunchCfg &, hipStream_t);
 };
 
 constexpr int kMaxMultiInputs = 16;

@@ -212,6 +212,84 @@ k_elem_multi(MultiIn<typename C::unit> ins, int k, typename C::unit *__restrict_
     }
 }
 
+// Tree combine: k = 2^L operands in slots 0..k-1 folded pairwise by levels,
+// level m = 1, 2, 4, ...: slot s (bit m clear) = OP(inout = slot s, in = slot
+// s + m), result = slot 0, written to `out` (which may be slot 0's buffer).
+// With the slots holding the peers of rank r in the order
+// r ^ bitrev(s) this is the recursive-halving association of rank r's block
+// (…recursive_halving.c:164-229: each step the partner's partial is `in`, the
+// own partial `inout`), computed in one pass that reads the k blocks
+// (over xGMI for the peers') and writes one.  Unused slots (s >= k) are
+// compile-time registers whose loads and combines are skipped by uniform
+// branches, so one instantiation serves every k.
+template <class C>
+__global__ void __launch_bounds__(256)
+k_contig_tree(MultiIn<typename C::unit> ins, int k, typename C::unit *__restrict__ out,
+              uint64_t head, uint64_t npk, uint64_t tail_start, uint32_t ntail, Params prm)
+{
+    using T = typename C::unit;
+    v4u *vout = reinterpret_cast<v4u *>(out + head);
+    const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x; i < npk; i += stride) {
+        v4u v[kMaxMulti];
+#pragma unroll
+        for (int q = 0; q < kMaxMulti; ++q)
+            if (q < k)
+                v[q] = ld16<true>(reinterpret_cast<const v4u *>(ins.p[q] + head) + i);
+#pragma unroll
+        for (int m = 1; m < kMaxMulti; m <<= 1)
+#pragma unroll
+            for (int q = 0; q < kMaxMulti; q += 2 * m)
+                if (q + m < k)
+                    v[q] = combine16<C>(v[q], v[q + m], prm);
+        st16<true>(vout + i, v[0]);
+    }
+    if (blockIdx.x == 0) {
+        auto one = [&](uint64_t t) {
+            T v[kMaxMulti];
+#pragma unroll
+            for (int q = 0; q < kMaxMulti; ++q)
+                if (q < k)
+                    v[q] = ins.p[q][t];
+#pragma unroll
+            for (int m = 1; m < kMaxMulti; m <<= 1)
+#pragma unroll
+                for (int q = 0; q < kMaxMulti; q += 2 * m)
+                    if (q + m < k)
+                        v[q] = C::apply(v[q], v[q + m], prm);
+            out[t] = v[0];
+        };
+        for (uint64_t t = threadIdx.x; t < head; t += blockDim.x)
+            one(t);
+        for (uint64_t t = threadIdx.x; t < ntail; t += blockDim.x)
+            one(tail_start + t);
+    }
+}
+
+// the same fold element by element, for operands not sharing a 16-byte phase
+template <class C>
+__global__ void __launch_bounds__(256)
+k_elem_tree(MultiIn<typename C::unit> ins, int k, typename C::unit *__restrict__ out, uint64_t n,
+            Params prm)
+{
+    using T = typename C::unit;
+    const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
+    for (uint64_t t = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x; t < n; t += stride) {
+        T v[kMaxMulti];
+#pragma unroll
+        for (int q = 0; q < kMaxMulti; ++q)
+            if (q < k)
+                v[q] = ins.p[q][t];
+#pragma unroll
+        for (int m = 1; m < kMaxMulti; m <<= 1)
+#pragma unroll
+            for (int q = 0; q < kMaxMulti; q += 2 * m)
+                if (q + m < k)
+                    v[q] = C::apply(v[q], v[q + m], prm);
+        out[t] = v[0];
+    }
+}
+
 template <class C>
 __global__ void __launch_bounds__(1024)
 k_elem(const typename C::unit *__restrict__ in, typename C::unit *__restrict__ io, uint64_t n,
@@ -448,6 +526,38 @@ hipError_t launch_multi(const void *const *ins, int k, void *io, uint64_t count,
     return hipGetLastError();
 }
 
+// out = tree fold of ins[0..k-1] (k a power of two, 2..16; k_contig_tree)
+template <class C>
+hipError_t launch_tree(const void *const *ins, int k, void *out, uint64_t count, const Params &prm,
+                       const LaunchCfg &cfg, hipStream_t s)
+{
+    using T = typename C::unit;
+    constexpr uint64_t E = 16 / sizeof(T);
+    MultiIn<T> mi{};
+    uintptr_t ao = reinterpret_cast<uintptr_t>(out);
+    bool aligned = (ao % sizeof(T)) == 0;
+    for (int q = 0; q < k; ++q) {
+        mi.p[q] = static_cast<const T *>(ins[q]);
+        aligned = aligned && ((reinterpret_cast<uintptr_t>(ins[q]) & 15) == (ao & 15));
+    }
+    (void) cfg;
+    T *tout = static_cast<T *>(out);
+    if (aligned) {
+        uint64_t head = ((16 - (ao & 15)) & 15) / sizeof(T);
+        if (head > count)
+            head = count;
+        uint64_t npk = (count - head) / E;
+        uint64_t tail_start = head + npk * E;
+        uint32_t ntail = (uint32_t) (count - tail_start);
+        hipLaunchKernelGGL((k_contig_tree<C>), dim3(grid_for(256, npk, 0)), dim3(256), 0, s, mi, k,
+                           tout, head, npk, tail_start, ntail, prm);
+    } else {
+        hipLaunchKernelGGL((k_elem_tree<C>), dim3(grid_for(256 * 4, count, 0)), dim3(256), 0, s,
+                           mi, k, tout, count, prm);
+    }
+    return hipGetLastError();
+}
+
 template <class C>
 hipError_t launch_vector(const void *in, void *io, uint64_t count, uint64_t bl, uint64_t st,
                          const Params &prm, const LaunchCfg &cfg, hipStream_t s)
@@ -487,7 +597,8 @@ hipError_t launch_iov(const void *in, void *io, const int64_t *d_seg_off, const 
 
 template <class C> constexpr Entry entry()
 {
-    return Entry{&launch_contig<C>, &launch_vector<C>, &launch_multi<C>, &launch_iov<C>};
+    return Entry{&launch_contig<C>, &launch_vector<C>, &launch_multi<C>, &launch_iov<C>,
+                 &launch_tree<C>};
 }
 
 }  // namespace mpix

@@ -48,6 +48,8 @@ def lib():
             'MPIX_Reduce_local_vector_async': ([vp, vp, aint, aint, aint, i32, i32, vp], i32),
             'MPIX_Reduce_local_multi_async': ([ctypes.POINTER(vp), i32, vp, aint, i32, i32, vp],
                                               i32),
+            'MPIX_Reduce_local_tree_async': ([ctypes.POINTER(vp), i32, vp, aint, i32, i32, vp],
+                                             i32),
             'MPIX_Reduce_local_iov_async': ([vp, vp, aint, ctypes.POINTER(aint),
                                              ctypes.POINTER(aint), i32, i32, vp], i32),
             'MPIX_Reduce_local_iovec_async': ([vp, vp, aint, ctypes.POINTER(aint),
@@ -263,6 +265,16 @@ def reduce_local_multi_async(inbufs, inoutbuf, count, datatype, op, stream=None)
     return lib().MPIX_Reduce_local_multi_async(arr, len(inbufs), _addr(inoutbuf), count,
                                                H.as_c_int(datatype), H.as_c_int(op),
                                                _stream_ptr(stream))
+
+
+def reduce_local_tree_async(inbufs, outbuf, count, datatype, op, stream=None):
+    """outbuf = pairwise tree fold of the 2^L inbufs, levels m = 1, 2, 4, ...
+    (slot s = slot s OP slot s+m); outbuf may be inbufs[0]."""
+    _span_check(count, datatype, op, outbuf, *inbufs)
+    arr = (ctypes.c_void_p * len(inbufs))(*[_addr(b) for b in inbufs])
+    return lib().MPIX_Reduce_local_tree_async(arr, len(inbufs), _addr(outbuf), count,
+                                              H.as_c_int(datatype), H.as_c_int(op),
+                                              _stream_ptr(stream))
 
 
 IPC_HANDLE_BYTES = 64

@@ -133,6 +133,32 @@ def test_errors_without_gpu(R):
     assert R.MPI_Reduce_local(4096, 1 << 20, 1 << 62, H.MPI_INT, H.MPI_SUM) == H.MPI_ERR_COUNT
 
 
+def test_tree_entry_argument_errors(R):
+    """MPIX_Reduce_local_tree_async: 2..16 operands, a power of two; the output
+    may be slot 0 itself but overlap nothing else; MPIX_EQUAL is refused;
+    host (non device-accessible) buffers are MPI_ERR_BUFFER -- all before any
+    device work"""
+    import ctypes
+    from mpich_amd import handles as H
+    L = R.lib()
+
+    def call(ptrs, out, count=16, dt=H.MPI_FLOAT, op=H.MPI_SUM):
+        arr = (ctypes.c_void_p * len(ptrs))(*ptrs)
+        return L.MPIX_Reduce_local_tree_async(arr, len(ptrs), out, count, dt, op, None)
+    base = 1 << 20
+    ins = [base + i * 4096 for i in range(8)]
+    for k in (1, 3, 6, 32):
+        assert call(ins[:k] if k <= 8 else ins * 4, 1 << 24) == H.MPI_ERR_ARG, k
+    assert call(ins[:4], ins[1] + 8) == H.MPI_ERR_BUFFER           # overlaps slot 1
+    assert call(ins[:4], 1 << 24, count=-1) == H.MPI_ERR_COUNT
+    assert call(ins[:4], 1 << 24, op=H.MPI_BAND) == H.MPI_ERR_OP
+    assert call(ins[:4], 1 << 24, dt=H.MPI_BYTE, op=H.MPIX_EQUAL) == H.MPI_ERR_OP
+    assert call(ins[:4], 1 << 24, count=0) == H.MPI_SUCCESS
+    import numpy as np
+    a = [np.zeros(16, np.float32) for _ in range(4)]
+    assert call([x.ctypes.data for x in a], a[0].ctypes.data) == H.MPI_ERR_BUFFER   # host
+
+
 def test_errors_reduce_local_errors_test(R):
     """test/mpi/errors/coll/reduce_local.c:38-58: MPI_IN_PLACE as either
     buffer and inbuf == inoutbuf are MPI_ERR_BUFFER (checked before any

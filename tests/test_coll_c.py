@@ -25,6 +25,7 @@ from tests import golden_util as gu
 
 MPI_FLOAT, MPI_DOUBLE, MPI_INT = 0x4c00040a, 0x4c00080b, 0x4c000405
 MPI_2INT = 0x4c000816
+MPI_MIN = 0x58000002
 MPI_SUM, MPI_PROD, MPI_MAX, MPI_BXOR, MPI_MAXLOC = 0x58000003, 0x58000004, 0x58000001, \
     0x5800000a, 0x5800000c
 
@@ -113,7 +114,7 @@ def test_rsb_multipath_host_matches_recursive_halving(oracle, P, recvcount):
 
 
 @pytest.mark.parametrize('algo', ['recursive_halving', 'pairwise', 'auto',
-                                  'recursive_halving_multipath'])
+                                  'recursive_halving_multipath', 'recursive_halving_pull'])
 @pytest.mark.parametrize('P', [2, 3, 4, 6, 8])
 def test_rsb_host_redscatblk3(oracle, P, algo):
     """redscatblk3.c:43-56: block i of rank r holds r + i; the result on rank
@@ -479,7 +480,7 @@ def _dev_comms(P):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize('algo', ['recursive_halving', 'pairwise', 'pairwise_sequential',
-                                  'recursive_halving_multipath'])
+                                  'recursive_halving_multipath', 'recursive_halving_pull'])
 @pytest.mark.parametrize('P', [2, 3, 4, 8])
 def test_rsb_device_local_matches_oracle(oracle, P, algo):
     import torch
@@ -498,6 +499,44 @@ def test_rsb_device_local_matches_oracle(oracle, P, algo):
     exp = sim([s.view(np.uint8) for s in sends], recvcount, MPI_FLOAT, MPI_SUM)
     for r in range(P):
         assert drecv[r].cpu().numpy().tobytes() == exp[r].tobytes(), r
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('in_place', [False, True])
+@pytest.mark.parametrize('dt,op', [(MPI_FLOAT, MPI_SUM), (MPI_DOUBLE, MPI_MAX),
+                                   (MPI_DOUBLE, MPI_MIN), (MPI_2INT, MPI_MAXLOC)])
+@pytest.mark.parametrize('P', [2, 4, 8, 16])
+def test_rsb_recursive_halving_pull_matches_oracle(oracle, P, dt, op, in_place):
+    """MPIX_RSB_RECURSIVE_HALVING_PULL: one tree kernel per rank reading its
+    block of all P ranks through the mappings, bit-identical to the oracle's
+    recursive-halving simulation -- NaN payloads, +-0 and MAXLOC ties show the
+    operand roles of every level; odd recvcount puts the blocks off the
+    16-byte grid (element path); MPI_IN_PLACE lands the block at recvbuf[0]"""
+    import torch
+    from mpich_amd import ccl
+    recvcount = 40961 if P <= 8 else 4099
+    ext = oracle.extent(dt)
+    rng = np.random.default_rng(0x5EED0700 + P)
+    if dt == MPI_2INT:
+        sends = [rng.integers(0, 3, (P * recvcount, 2)).astype(np.int32) for _ in range(P)]
+    elif dt == MPI_DOUBLE:
+        sends = _special_doubles(P, P * recvcount, P)
+    else:
+        sends = float_sends(P, P * recvcount, 0x5EED0701)
+    raw = [np.ascontiguousarray(s).view(np.uint8).reshape(-1) for s in sends]
+    dsend = [torch.from_numpy(r.copy()).cuda() for r in raw]
+    drecv = dsend if in_place else [torch.zeros(recvcount * ext, dtype=torch.uint8, device='cuda')
+                                    for _ in range(P)]
+    torch.cuda.synchronize()
+    comms = _dev_comms(P)
+    rcs = run_ranks(comms, lambda r, c: ccl.reduce_scatter_block(
+        None if in_place else dsend[r], drecv[r], recvcount, dt, op, c, 'recursive_halving_pull'))
+    free_all(comms)
+    assert rcs == [0] * P
+    exp = oracle.rsb_recursive_halving(raw, recvcount, dt, op)
+    for r in range(P):
+        got = drecv[r].cpu().numpy()[:recvcount * ext]
+        assert got.tobytes() == exp[r].tobytes(), r
 
 
 @pytest.mark.gpu

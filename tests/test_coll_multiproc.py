@@ -108,7 +108,8 @@ def _run(oracle, tmp_path, world, backend, cases):
     _check(oracle, tmp_path, world, cases)
 
 
-ALGOS = ('recursive_halving', 'pairwise', 'pairwise_pipelined', 'pull', 'recursive_halving_multipath')
+ALGOS = ('recursive_halving', 'pairwise', 'pairwise_pipelined', 'pull', 'recursive_halving_multipath',
+         'recursive_halving_pull')
 
 
 @pytest.mark.parametrize('world', [2, 3, 4, 8])

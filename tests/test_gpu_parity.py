@@ -557,6 +557,72 @@ def test_multi_input_combine(R, H, oracle, k, dtname, opname):
                        opname, ext) == 0
 
 
+def _special_f64(rng, n):
+    """doubles with NaN (two payloads), +-0, +-Inf mixed in: MAX/MIN pick by
+    operand role, so the tree's inout/in assignment shows in the bits"""
+    x = rng.uniform(-1, 1, n)
+    pick = rng.integers(0, 8, n)
+    x[pick == 0] = 0.0
+    x[pick == 1] = -0.0
+    x[pick == 2] = np.frombuffer(np.array([0x7ff8000000000001], np.uint64).tobytes(), np.float64)[0]
+    x[pick == 3] = np.frombuffer(np.array([0xfff8000000000abc], np.uint64).tobytes(), np.float64)[0]
+    x[pick == 4] = np.inf
+    return x
+
+
+@pytest.mark.parametrize('k', [2, 4, 8, 16])
+@pytest.mark.parametrize('dtname,opname', [('MPI_FLOAT', 'MPI_SUM'), ('MPI_DOUBLE', 'MPI_MAX'),
+                                           ('MPI_DOUBLE', 'MPI_MIN'), ('MPI_INT', 'MPI_PROD'),
+                                           ('MPI_2INT', 'MPI_MAXLOC'), ('MPI_DOUBLE_INT', 'MPI_MINLOC'),
+                                           ('MPIX_BFLOAT16', 'MPI_SUM'),
+                                           ('MPI_C_DOUBLE_COMPLEX', 'MPI_PROD'),
+                                           ('MPI_FLOAT', 'MPI_REPLACE'), ('MPI_FLOAT', 'MPI_NO_OP')])
+def test_tree_combine(R, H, oracle, k, dtname, opname):
+    """MPIX_Reduce_local_tree_async == the level-by-level fold done with
+    MPI_Reduce_local calls (slot s = slot s OP slot s+m, m = 1, 2, 4, ...):
+    bit-exact, NaN payloads and +-0 included; packet path, unaligned element
+    path and in place (out = slot 0)"""
+    dt, op = getattr(H, dtname), getattr(H, opname)
+    ext = R.datatype_extent(dt)
+    for n, off, in_place in ((100003, 0, False), (4097, 4 if ext % 8 else 8, False),
+                             (65536 + 5, 0, True)):
+        rng = np.random.default_rng(k * 7919 + n + (1 if in_place else 0))
+        nb = n * ext + 64
+
+        def mk():
+            if dtname in ('MPI_INT', 'MPI_2INT'):
+                return rng.integers(0, 4, nb // 4).astype(np.int32).view(np.uint8)
+            if dtname == 'MPI_DOUBLE_INT':      # {double value; int loc} + pad: ties likely
+                a = np.zeros(nb // 16, dtype=[('v', '<f8'), ('l', '<i4'), ('p', '<i4')])
+                a['v'] = rng.integers(0, 3, a.size)
+                a['l'] = rng.integers(0, 50, a.size)
+                return a.view(np.uint8).copy()
+            if dtname == 'MPIX_BFLOAT16':
+                return (rng.integers(0, 1 << 16, nb // 2).astype(np.uint16) & 0x7f7f).view(np.uint8)
+            if dtname == 'MPI_DOUBLE' or 'COMPLEX' in dtname:
+                return _special_f64(rng, nb // 8).view(np.uint8) if dtname == 'MPI_DOUBLE' else \
+                    rng.uniform(-1, 1, nb // 8).view(np.uint8)
+            return rng.uniform(-1, 1, nb // 4).astype(np.float32).view(np.uint8)
+        ins = [mk() for _ in range(k)]
+        v = [x[off:off + n * ext].copy() for x in ins]
+        m = 1
+        while m < k:
+            for q in range(0, k, 2 * m):
+                oracle.reduce_local(v[q + m], v[q], n, dt, op)
+            m *= 2
+        exp = v[0]
+        dins = [dev(x) for x in ins]
+        if in_place:
+            dout, oo = dins[0], off
+        else:
+            dout, oo = dev(np.zeros(nb, np.uint8)), off
+        rc = R.reduce_local_tree_async([d.data_ptr() + off for d in dins], dout.data_ptr() + oo, n,
+                                       dt, op)
+        assert rc == 0, rc
+        got = host(dout)[oo:oo + n * ext]
+        assert got.tobytes() == exp.tobytes(), (n, off, in_place)
+
+
 def test_concurrent_callers(R, H, oracle):
     """MPIR_Reduce_local is reentrant (called with the global CS held by
     different threads under MPI_THREAD_MULTIPLE): per-thread streams, no

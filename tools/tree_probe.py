@@ -1,0 +1,71 @@
+"""HBM rate of the multi-input kernels on one GPU: the tree fold
+(MPIX_Reduce_local_tree_async, k slots -> one output) and the in-order fold
+(MPIX_Reduce_local_multi_async, inout + k inputs), fp32 SUM, k blocks of
+`--mib` MiB each.  Bytes per launch: tree (k + 1) x block, multi (k + 2) x
+block.  Prints one JSON line.  Usage: python tools/tree_probe.py [--mib 256]"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from mpich_amd import handles as H  # noqa: E402
+from mpich_amd import redop  # noqa: E402
+
+
+def timed(fn, s, reps=20):
+    fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record(s)
+    for _ in range(reps):
+        fn()
+    e1.record(s)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e-3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--mib', type=int, default=256)
+    ap.add_argument('--out', default=None)
+    a = ap.parse_args()
+    n = a.mib * (1 << 20) // 4
+    s = torch.cuda.Stream()
+    rows = []
+    with torch.cuda.stream(s):
+        for k in (2, 4, 8, 16):
+            blocks = [torch.rand(n, device='cuda') for _ in range(k)]
+            out = torch.empty(n, device='cuda')
+            acc = torch.empty(n, device='cuda')
+            torch.cuda.synchronize()
+            ptrs = [b.data_ptr() for b in blocks]
+
+            def tree():
+                redop.check(redop.reduce_local_tree_async(ptrs, out.data_ptr(), n, H.MPI_FLOAT,
+                                                          H.MPI_SUM, stream=s.cuda_stream),
+                            'tree')
+
+            def multi():
+                redop.check(redop.reduce_local_multi_async(ptrs[1:], acc.data_ptr(), n,
+                                                           H.MPI_FLOAT, H.MPI_SUM,
+                                                           stream=s.cuda_stream), 'multi')
+            tt, tm = timed(tree, s), timed(multi, s)
+            bt, bm = (k + 1) * n * 4, (k + 1) * n * 4      # multi: inout + k-1 inputs
+            rows.append(dict(k=k, block_MiB=a.mib, tree_ms=round(tt * 1e3, 4),
+                             tree_GBs=round(bt / tt / 1e9, 1), multi_ms=round(tm * 1e3, 4),
+                             multi_GBs=round(bm / tm / 1e9, 1)))
+            del blocks, out, acc
+            torch.cuda.empty_cache()
+    line = json.dumps({'tree_probe': rows})
+    print(line)
+    if a.out:
+        with open(a.out, 'w') as f:
+            f.write(line + '\n')
+
+
+if __name__ == '__main__':
+    main()
