@@ -781,18 +781,20 @@ def allreduce_secondary(args, world, rank, dev, res):
                       lambda: redop.check(ccl.allreduce(send, recv, n, H.MPI_FLOAT, H.MPI_SUM, cc,
                                                         'rsag_multipath', workspace=ws),
                                           'MPIX_Allreduce')),
+                     ('c_pull',
+                      lambda: redop.check(ccl.allreduce(send, recv, n, H.MPI_FLOAT, H.MPI_SUM, cc,
+                                                        'pull'), 'MPIX_Allreduce')),
                      ('rccl_all_reduce', lambda: (recv.copy_(send), dist.all_reduce(recv)))):
         if name == 'rccl_all_reduce' and dist.get_backend() != 'nccl':
             continue
         fn()
         if name == 'c_reduce_scatter_allgather':
             ref = recv.clone()
-        elif name == 'c_rsag_multipath':    # same association, so the same bits
+        elif name in ('c_rsag_multipath', 'c_pull'):    # same association, so the same bits
             same = bool(torch.equal(recv.view(torch.int32), ref.view(torch.int32)))
             if not allreduce_scalar(1 if same else 0, dist.ReduceOp.MIN, dev):
-                raise RuntimeError('rsag_multipath allreduce differs from reduce_scatter_allgather')
-            res['rsag_multipath_bit_identical_all_ranks'] = True
-            del ref
+                raise RuntimeError('%s allreduce differs from reduce_scatter_allgather' % name)
+            res['%s_bit_identical_all_ranks' % name[2:]] = True
         reps = max(3, min(10, args.steps))
         dist.barrier()
         torch.cuda.synchronize()
@@ -804,7 +806,7 @@ def allreduce_secondary(args, world, rank, dev, res):
         t = allreduce_scalar((time.perf_counter() - t0) / reps, dist.ReduceOp.MAX, dev)
         res[name] = dict(ms=round(t * 1e3, 3),
                          busbw_GBs=round(2 * (world - 1) / world * n * 4 / t / 1e9, 2))
-    del send, recv, ws
+    del send, recv, ws, ref
     torch.cuda.empty_cache()
 
 

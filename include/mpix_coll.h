@@ -226,6 +226,14 @@ int MPIX_Exscan_async(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_
                                                    through relays (P a power of two >= 4,
                                                    count a multiple of P; else plain steps);
                                                    same bits */
+#define MPIX_ALLREDUCE_PULL                 6   /* REDUCE_SCATTER_ALLGATHER's association (same
+                                                   bits) as two pulls over hipIpc mappings: ONE
+                                                   tree kernel reads this rank's block of every
+                                                   rank's input (MPIX_Reduce_local_tree_async),
+                                                   then ONE copy kernel reads every peer's
+                                                   finished block (MPIX_Copy_multi_async); no
+                                                   workspace.  P a power of two <= 16 on a device
+                                                   communicator, else REDUCE_SCATTER_ALLGATHER */
 size_t MPIX_Allreduce_workspace(MPIX_Aint count, MPIX_Datatype datatype, MPIX_Comm comm);
 int MPIX_Allreduce(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Datatype datatype,
                    MPIX_Op op, MPIX_Comm comm, int algorithm, void *workspace,

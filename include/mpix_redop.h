@@ -238,6 +238,13 @@ int MPIX_Reduce_local_tree_async(const void *const *inbufs, int ninputs, void *o
                                  MPIX_Aint count, MPIX_Datatype datatype, MPIX_Op op,
                                  void *stream);
 
+/* n <= 16 independent copies dsts[q] <- srcs[q] (bytes[q] each) in ONE
+ * stream-ordered launch, all running at once -- the allgather step of a pull
+ * schedule, whose P-1 sources sit behind P-1 different xGMI links.
+ * Device-accessible, non-overlapping pairs; zero-byte entries are skipped. */
+int MPIX_Copy_multi_async(const void *const *srcs, void *const *dsts, const MPIX_Aint *bytes,
+                          int n, void *stream);
+
 /* ---- peer memory for the fused pull + combine ----
  * The reference maps peer GPU buffers with hipIpc* in its shm/ipc path
  * (src/mpl/src/gpu/mpl_gpu_hip.c:174-204).  Here a rank exports the

@@ -30,9 +30,10 @@ RSB_ALGORITHMS = {'auto': RSB_AUTO, 'recursive_halving': RSB_RECURSIVE_HALVING,
                   'recursive_halving_pull': RSB_RECURSIVE_HALVING_PULL}
 XPORT_DEVICE, XPORT_HOST, XPORT_STAGED = 0, 1, 2
 AR_AUTO, AR_RECURSIVE_DOUBLING, AR_RSAG, AR_RSAG_RD, AR_RING, AR_RSAG_MULTIPATH = 0, 1, 2, 3, 4, 5
+AR_PULL = 6
 AR_ALGORITHMS = {'auto': AR_AUTO, 'recursive_doubling': AR_RECURSIVE_DOUBLING,
                  'reduce_scatter_allgather': AR_RSAG, 'rsag_rd_allgather': AR_RSAG_RD,
-                 'ring': AR_RING, 'rsag_multipath': AR_RSAG_MULTIPATH}
+                 'ring': AR_RING, 'rsag_multipath': AR_RSAG_MULTIPATH, 'pull': AR_PULL}
 
 _lib = None
 

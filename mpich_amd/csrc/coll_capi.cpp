@@ -357,7 +357,7 @@ int mark(MPIX_Comm c, const char *label, hipStream_t s)
 }
 
 // one published record per rank (barrier tokens are 1-byte records)
-constexpr size_t kRec = 128;
+constexpr size_t kRec = 256;
 
 int token_buffer(MPIX_Comm c, hipStream_t s)
 {
@@ -912,6 +912,28 @@ struct PullRec {
 };
 static_assert(sizeof(PullRec) <= kRec, "pull record size");
 
+// this rank's record for `p`; valid = 0 when the allocation cannot be
+// exported (every rank then sees it and takes the fallback)
+void pull_record(MPIX_Comm c, const void *p, PullRec *me)
+{
+    memset(me, 0, sizeof *me);
+    me->raw = reinterpret_cast<uint64_t>(p);
+    me->valid = 1;
+    if (c->kind == K_LOCAL_DEV)
+        return;
+    hipDeviceptr_t base = nullptr;
+    size_t bytes = 0;
+    hipIpcMemHandle_t h;
+    if (hipMemGetAddressRange(&base, &bytes, (hipDeviceptr_t) p) != hipSuccess ||
+        hipIpcGetMemHandle(&h, (void *) base) != hipSuccess) {
+        (void) hipGetLastError();
+        me->valid = 0;
+    } else {
+        memcpy(me->handle, &h, sizeof h);
+        me->offset = (int64_t) (static_cast<const char *>(p) - static_cast<const char *>((void *) base));
+    }
+}
+
 // the peer allocation behind `r`, mapped once and cached by handle (a
 // communicator holds at most kMaxMaps mappings; past that the cache is
 // dropped after the stream has drained the kernels that used them)
@@ -985,22 +1007,7 @@ int rs_pull(const char *sb, char *rb, const std::vector<size_t> &cnts, MPIX_Data
     if (!in_place && !tree)
         TRY(copy(c, rb, sb + disps[rank] * ext, blk, s));                   // :58-64
     PullRec me;
-    memset(&me, 0, sizeof me);
-    me.raw = reinterpret_cast<uint64_t>(sb);
-    me.valid = 1;
-    if (c->kind != K_LOCAL_DEV) {
-        hipDeviceptr_t base = nullptr;
-        size_t bytes = 0;
-        hipIpcMemHandle_t h;
-        if (hipMemGetAddressRange(&base, &bytes, (hipDeviceptr_t) sb) != hipSuccess ||
-            hipIpcGetMemHandle(&h, (void *) base) != hipSuccess) {
-            (void) hipGetLastError();
-            me.valid = 0;       // every rank sees it and takes the fallback
-        } else {
-            memcpy(me.handle, &h, sizeof h);
-            me.offset = (int64_t) (sb - static_cast<const char *>((void *) base));
-        }
-    }
+    pull_record(c, sb, &me);
     HTRY(hipStreamSynchronize(s));      // this rank's inputs complete before anyone reads them
     std::vector<char> all;
     TRY(allgather_records(c, &me, sizeof me, &all, s));
@@ -1228,6 +1235,96 @@ int allreduce_rsag(char *rb, size_t count, MPIX_Datatype dt, MPIX_Op op, MPIX_Co
         else
             TRY(exchange(c, {rcv(rank + 1, rb, nb)}, s));
     }
+    return MPIX_REDOP_SUCCESS;
+}
+
+// MPIX_ALLREDUCE_PULL: the Rabenseifner allreduce's association (same bits as
+// REDUCE_SCATTER_ALLGATHER) as two pulls over the IPC mappings, P a power of
+// two <= 16 on a device communicator.  Reduce-scatter: rank r owns block
+// bitrev(r) (the halving steps of :138-189 keep the half selected by bit 0,
+// then bit 1, ...), which recursive halving with masks 1, 2, 4, ... folds as
+// MPIX_Reduce_local_tree_async does with slot s = r ^ s; ONE tree kernel reads
+// that block of every rank's input and writes it into recvbuf.  Allgather:
+// after a barrier, ONE copy kernel reads every peer's finished block from its
+// recvbuf (MPIX_Copy_multi_async).  A closing barrier keeps every rank's
+// buffers in place until its peers are done.  No sendbuf -> recvbuf copy and
+// no workspace.  Other shapes: the sendbuf copy + REDUCE_SCATTER_ALLGATHER.
+int allreduce_rsag(char *rb, size_t count, MPIX_Datatype dt, MPIX_Op op, MPIX_Comm c, char *tmp,
+                   hipStream_t s, size_t ext, bool direct, bool multipath);
+
+int allreduce_pull(const char *sendbuf, char *rb, size_t count, MPIX_Datatype dt, MPIX_Op op,
+                   MPIX_Comm c, void *ws, size_t ws_bytes, hipStream_t s, size_t ext)
+{
+    const int rank = c->rank, size = c->size;
+    const size_t nb = count * ext;
+    auto fallback = [&]() -> int {
+        if (sendbuf)
+            TRY(copy(c, rb, sendbuf, nb, s));
+        char *tmp;
+        TRY(workspace(c, ws, ws_bytes, round256(nb), s, &tmp));
+        return release_scratch(c, tmp, allreduce_rsag(rb, count, dt, op, c, tmp, s, ext, true,
+                                                      false), s);
+    };
+    if (c->host() || c->combine || (size & (size - 1)) || size > 16)
+        return fallback();
+    const char *in = sendbuf ? sendbuf : rb;
+    std::vector<size_t> cnts(size), disps(size, 0);
+    for (int i = 0; i < size; ++i)
+        cnts[i] = count / size + ((size_t) i < count % size ? 1 : 0);
+    for (int i = 1; i < size; ++i)
+        disps[i] = disps[i - 1] + cnts[i - 1];
+    struct Recs {
+        PullRec in, out;
+    } me;
+    static_assert(sizeof(Recs) <= kRec, "allreduce pull records");
+    pull_record(c, in, &me.in);
+    pull_record(c, rb, &me.out);
+    TRY(mark(c, "start", s));
+    HTRY(hipStreamSynchronize(s));      // inputs complete before anyone reads them
+    std::vector<char> all;
+    TRY(allgather_records(c, &me, sizeof me, &all, s));
+    std::vector<Recs> recs(size);
+    bool ok = true;
+    for (int q = 0; q < size; ++q) {
+        memcpy(&recs[q], all.data() + kRec * (size_t) q, sizeof(Recs));
+        ok &= recs[q].in.valid == 1 && recs[q].out.valid == 1;
+    }
+    if (!ok)
+        return fallback();
+    TRY(mark(c, "publish", s));
+    const int mine = bitrev(rank, size);
+    std::vector<const void *> ins(size);
+    for (int q = 0; q < size; ++q) {
+        const int src = rank ^ q;
+        const char *base = in;
+        if (src != rank)
+            TRY(peer_base(c, recs[src].in, s, &base));
+        ins[q] = base + disps[mine] * ext;
+    }
+    if (cnts[mine])
+        TRY(MPIX_Reduce_local_tree_async(ins.data(), size, rb + disps[mine] * ext,
+                                         (MPIX_Aint) cnts[mine], dt, op, s));
+    TRY(mark(c, "reduce-scatter pull", s));
+    TRY(barrier(c, s));                 // every block final (and every input read)
+    std::vector<const void *> srcs;
+    std::vector<void *> dsts;
+    std::vector<MPIX_Aint> bytes;
+    for (int q = 0; q < size; ++q) {
+        if (q == rank)
+            continue;
+        const int b = bitrev(q, size);
+        const char *base;
+        TRY(peer_base(c, recs[q].out, s, &base));
+        srcs.push_back(base + disps[b] * ext);
+        dsts.push_back(rb + disps[b] * ext);
+        bytes.push_back((MPIX_Aint) (cnts[b] * ext));
+    }
+    for (size_t lo = 0; lo < srcs.size(); lo += 16) {
+        const int n = (int) std::min<size_t>(16, srcs.size() - lo);
+        TRY(MPIX_Copy_multi_async(srcs.data() + lo, dsts.data() + lo, bytes.data() + lo, n, s));
+    }
+    TRY(mark(c, "allgather pull", s));
+    TRY(barrier(c, s));                 // peers done reading this rank's buffers
     return MPIX_REDOP_SUCCESS;
 }
 
@@ -1644,7 +1741,7 @@ int allreduce_entry(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Da
 {
     size_t ext;
     TRY(check_args(c, recvbuf, count, dt, op, &ext));
-    if (algorithm < MPIX_ALLREDUCE_AUTO || algorithm > MPIX_ALLREDUCE_RSAG_MULTIPATH)
+    if (algorithm < MPIX_ALLREDUCE_AUTO || algorithm > MPIX_ALLREDUCE_PULL)
         return MPIX_REDOP_ERR_ARG;
     if (!count)
         return MPIX_REDOP_SUCCESS;
@@ -1659,10 +1756,15 @@ int allreduce_entry(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Da
                         : MPIX_ALLREDUCE_RECURSIVE_DOUBLING;
     if ((algorithm == MPIX_ALLREDUCE_REDUCE_SCATTER_ALLGATHER ||
          algorithm == MPIX_ALLREDUCE_RSAG_RD_ALLGATHER ||
-         algorithm == MPIX_ALLREDUCE_RSAG_MULTIPATH) && (size_t) count < (size_t) pof2)
+         algorithm == MPIX_ALLREDUCE_RSAG_MULTIPATH || algorithm == MPIX_ALLREDUCE_PULL) &&
+        (size_t) count < (size_t) pof2)
         return MPIX_REDOP_ERR_COUNT;    // :127
     if (algorithm != MPIX_ALLREDUCE_RECURSIVE_DOUBLING && splits_message_forbidden(op))
         return MPIX_REDOP_ERR_OP;       // MPIR_Allreduce_equal uses recursive doubling only
+    if (algorithm == MPIX_ALLREDUCE_PULL && c->size > 1)
+        return finish(c, allreduce_pull(static_cast<const char *>(sendbuf), rb, (size_t) count, dt,
+                                        op, c, ws, ws_bytes, s, ext),
+                      s, blocking);
     if (sendbuf)
         TRY(copy(c, rb, sendbuf, nb, s));
     if (c->size == 1)

@@ -82,6 +82,61 @@ hipError_t launch_equal(const void *in, void *io, uint64_t n, hipStream_t s)
     return hipGetLastError();
 }
 
+// Up to kMaxMultiInputs independent copies in one launch (blockIdx.y picks
+// the segment): the allgather step of a pull schedule reads P-1 peers' blocks
+// over P-1 links at once instead of P-1 stream-serialised copies.  16-byte
+// packets where source and destination share a 16-byte phase, bytes otherwise.
+struct CopySegs {
+    const unsigned char *src[kMaxMultiInputs];
+    unsigned char *dst[kMaxMultiInputs];
+    uint64_t bytes[kMaxMultiInputs];
+};
+
+__global__ void __launch_bounds__(256) k_copy_multi(CopySegs sg)
+{
+    const int q = blockIdx.y;
+    const unsigned char *src = sg.src[q];
+    unsigned char *dst = sg.dst[q];
+    const uint64_t n = sg.bytes[q];
+    const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
+    const uint64_t t0 = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    const uintptr_t as = reinterpret_cast<uintptr_t>(src) & 15, ad = reinterpret_cast<uintptr_t>(dst) & 15;
+    if (as == ad) {
+        const uint64_t head = ((16 - ad) & 15) < n ? ((16 - ad) & 15) : n;
+        const uint64_t npk = (n - head) / 16;
+        const v4u *vs = reinterpret_cast<const v4u *>(src + head);
+        v4u *vd = reinterpret_cast<v4u *>(dst + head);
+        for (uint64_t k = t0; k < npk; k += stride)
+            st16<true>(vd + k, ld16<true>(vs + k));
+        if (blockIdx.x == 0) {
+            for (uint64_t t = threadIdx.x; t < head; t += blockDim.x)
+                dst[t] = src[t];
+            for (uint64_t t = head + npk * 16 + threadIdx.x; t < n; t += blockDim.x)
+                dst[t] = src[t];
+        }
+    } else {
+        for (uint64_t k = t0; k < n; k += stride)
+            dst[k] = src[k];
+    }
+}
+
+hipError_t launch_copy_multi(const void *const *srcs, void *const *dsts, const uint64_t *bytes,
+                             int n, hipStream_t s)
+{
+    CopySegs sg{};
+    uint64_t most = 0;
+    for (int q = 0; q < n; ++q) {
+        sg.src[q] = static_cast<const unsigned char *>(srcs[q]);
+        sg.dst[q] = static_cast<unsigned char *>(dsts[q]);
+        sg.bytes[q] = bytes[q];
+        most = bytes[q] > most ? bytes[q] : most;
+    }
+    // about 2048 workgroups in all: each segment's share of the 256 CUs
+    unsigned gx = grid_for(256ull * 16 * 4, most, (int) (2048 / (unsigned) n));
+    hipLaunchKernelGGL(k_copy_multi, dim3(gx, (unsigned) n), dim3(256), 0, s, sg);
+    return hipGetLastError();
+}
+
 const Entry *lookup_int(int raw, int opi)
 {
     switch ((unsigned) raw) {

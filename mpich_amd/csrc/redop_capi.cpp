@@ -1414,6 +1414,34 @@ int MPIX_Reduce_local_tree_async(const void *const *inbufs, int ninputs, void *o
                                    launch_cfg(), (hipStream_t) stream)));
 }
 
+int MPIX_Copy_multi_async(const void *const *srcs, void *const *dsts, const MPIX_Aint *bytes,
+                          int n, void *stream)
+{
+    if (n < 0 || n > mpix::kMaxMultiInputs || (n && (!srcs || !dsts || !bytes)))
+        return set_err(MPIX_REDOP_ERR_ARG);
+    const void *ds[mpix::kMaxMultiInputs];
+    void *dd[mpix::kMaxMultiInputs];
+    uint64_t nb[mpix::kMaxMultiInputs];
+    int m = 0;
+    for (int q = 0; q < n; ++q) {
+        if (bytes[q] < 0)
+            return set_err(MPIX_REDOP_ERR_COUNT);
+        if (bytes[q] == 0)
+            continue;
+        if (!srcs[q] || !dsts[q] || overlaps(srcs[q], dsts[q], (uint64_t) bytes[q]))
+            return set_err(MPIX_REDOP_ERR_BUFFER);
+        const void *pd;
+        if (!device_accessible(srcs[q], &ds[m]) || !device_accessible(dsts[q], &pd))
+            return set_err(MPIX_REDOP_ERR_BUFFER);
+        dd[m] = (void *) pd;
+        nb[m++] = (uint64_t) bytes[q];
+    }
+    if (!m)
+        return set_err(MPIX_REDOP_SUCCESS);
+    launch_cfg();
+    return set_err(hip_err(mpix::launch_copy_multi(ds, dd, nb, m, (hipStream_t) stream)));
+}
+
 int MPIX_Ipc_export(const void *devptr, void *handle_out, MPIX_Aint *offset_out)
 {
     if (!devptr || !handle_out || !offset_out)

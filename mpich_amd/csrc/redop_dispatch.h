@@ -57,6 +57,10 @@ const Entry *lookup_pair(int raw, int opi);
 // MPIX_EQUAL on an MPI_BYTE buffer of n >= 8 bytes (opequal.c:20-35)
 hipError_t launch_equal(const void *in, void *io, uint64_t n, hipStream_t s);
 
+// up to kMaxMultiInputs independent device copies in one launch
+hipError_t launch_copy_multi(const void *const *srcs, void *const *dsts, const uint64_t *bytes,
+                             int n, hipStream_t s);
+
 // compile-time unroll of the packet kernel (packets per lane per operand)
 int unroll();
 

@@ -159,6 +159,32 @@ def test_tree_entry_argument_errors(R):
     assert call([x.ctypes.data for x in a], a[0].ctypes.data) == H.MPI_ERR_BUFFER   # host
 
 
+def test_copy_multi_argument_errors(R):
+    """MPIX_Copy_multi_async: at most 16 segments, byte counts >= 0, no
+    overlapping pair, host memory refused -- all before any device work"""
+    import ctypes
+    import numpy as np
+    from mpich_amd import handles as H
+    L = R.lib()
+    vp = ctypes.c_void_p
+    L.MPIX_Copy_multi_async.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(vp),
+                                        ctypes.POINTER(ctypes.c_ssize_t), ctypes.c_int, vp]
+
+    def call(triples):
+        n = len(triples)
+        return L.MPIX_Copy_multi_async((vp * max(n, 1))(*[t[0] for t in triples]),
+                                       (vp * max(n, 1))(*[t[1] for t in triples]),
+                                       (ctypes.c_ssize_t * max(n, 1))(*[t[2] for t in triples]),
+                                       n, None)
+    assert call([(1 << 20, 1 << 21, 64)] * 17) == H.MPI_ERR_ARG
+    assert call([(1 << 20, 1 << 21, -1)]) == H.MPI_ERR_COUNT
+    assert call([(1 << 20, (1 << 20) + 8, 64)]) == H.MPI_ERR_BUFFER
+    assert call([(1 << 20, 1 << 21, 0)]) == H.MPI_SUCCESS
+    assert call([]) == H.MPI_SUCCESS
+    a, b = np.zeros(16, np.uint8), np.zeros(16, np.uint8)
+    assert call([(a.ctypes.data, b.ctypes.data, 16)]) == H.MPI_ERR_BUFFER
+
+
 def test_errors_reduce_local_errors_test(R):
     """test/mpi/errors/coll/reduce_local.c:38-58: MPI_IN_PLACE as either
     buffer and inbuf == inoutbuf are MPI_ERR_BUFFER (checked before any

@@ -134,7 +134,7 @@ def test_rsb_host_redscatblk3(oracle, P, algo):
 
 
 @pytest.mark.parametrize('algo', ['reduce_scatter_allgather', 'rsag_rd_allgather',
-                                  'recursive_doubling', 'ring', 'rsag_multipath'])
+                                  'recursive_doubling', 'ring', 'rsag_multipath', 'pull'])
 @pytest.mark.parametrize('P', [1, 2, 3, 4, 7, 8, 12, 16])
 def test_allreduce_host_matches_oracle_and_kats(oracle, P, algo):
     from mpich_amd import ccl
@@ -156,8 +156,7 @@ def test_allreduce_host_matches_oracle_and_kats(oracle, P, algo):
     for case in gu.load_cases():
         if case['nranks'] != P or not case['name'].startswith('allred '):
             continue
-        if algo.startswith('r') and algo != 'recursive_doubling' and algo != 'ring' and \
-                case['count'] < pof2:
+        if algo not in ('recursive_doubling', 'ring') and case['count'] < pof2:
             continue
         ext = len(case['expected']) // case['count']
         outs = [np.zeros(case['count'] * ext, np.uint8) for _ in range(P)]
@@ -573,7 +572,7 @@ def test_rsb_device_local_types(oracle, dt, op, algo):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize('algo', ['reduce_scatter_allgather', 'rsag_rd_allgather',
-                                  'recursive_doubling', 'ring', 'rsag_multipath'])
+                                  'recursive_doubling', 'ring', 'rsag_multipath', 'pull'])
 @pytest.mark.parametrize('P', [2, 3, 4, 7, 8])
 def test_allreduce_device_local_matches_oracle(oracle, P, algo):
     import torch
@@ -594,6 +593,72 @@ def test_allreduce_device_local_matches_oracle(oracle, P, algo):
         algorithm=algo if algo in ('recursive_doubling', 'ring') else 'reduce_scatter_allgather')
     for r in range(P):
         assert drecv[r].cpu().numpy().tobytes() == exp[r].tobytes(), r
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('in_place', [False, True])
+@pytest.mark.parametrize('dt,op', [(MPI_FLOAT, MPI_SUM), (MPI_DOUBLE, MPI_MAX),
+                                   (MPI_2INT, MPI_MAXLOC)])
+@pytest.mark.parametrize('P', [2, 4, 8, 16])
+def test_allreduce_pull_matches_oracle(oracle, P, dt, op, in_place):
+    """MPIX_ALLREDUCE_PULL: a tree kernel per rank over every rank's input
+    (rank r owns block bitrev(r)), then one copy kernel gathering the peers'
+    blocks -- the bits of the Rabenseifner schedule, with NaN/+-0 and MAXLOC
+    ties showing every operand role; ragged blocks (count % P != 0) and
+    MPI_IN_PLACE"""
+    import torch
+    from mpich_amd import ccl
+    count = 30011 if P <= 8 else 4103
+    ext = oracle.extent(dt)
+    rng = np.random.default_rng(0x5EED0800 + P)
+    if dt == MPI_2INT:
+        sends = [rng.integers(0, 3, (count, 2)).astype(np.int32) for _ in range(P)]
+    elif dt == MPI_DOUBLE:
+        sends = _special_doubles(P, count, 3 * P)
+    else:
+        sends = float_sends(P, count, 0x5EED0801)
+    raw = [np.ascontiguousarray(s).view(np.uint8).reshape(-1) for s in sends]
+    dsend = [torch.from_numpy(r.copy()).cuda() for r in raw]
+    drecv = dsend if in_place else [torch.zeros(count * ext, dtype=torch.uint8, device='cuda')
+                                    for _ in range(P)]
+    torch.cuda.synchronize()
+    comms = _dev_comms(P)
+    rcs = run_ranks(comms, lambda r, c: ccl.allreduce(None if in_place else dsend[r], drecv[r],
+                                                       count, dt, op, c, 'pull'))
+    free_all(comms)
+    assert rcs == [0] * P
+    exp = oracle.allreduce_rabenseifner(raw, count, dt, op, algorithm='reduce_scatter_allgather')
+    for r in range(P):
+        assert drecv[r].cpu().numpy().tobytes() == exp[r].tobytes(), r
+
+
+@pytest.mark.gpu
+def test_copy_multi():
+    """MPIX_Copy_multi_async: up to 16 independent copies in one launch,
+    16-byte-phase-matched and mismatched pairs, empty entries skipped"""
+    import torch
+    from mpich_amd import redop
+    L = redop.lib()
+    src = torch.randint(0, 256, (1 << 22,), dtype=torch.uint8, device='cuda')
+    dst = torch.zeros(1 << 22, dtype=torch.uint8, device='cuda')
+    segs = [(0, 0, 1000003), (1000003 + 16, 1100000, 65536), (1300001, 1300001, 5),
+            (2000000, 2000003, 77777), (3000000, 3000000, 0)] + \
+        [(3100000 + 40000 * i, 3100000 + 40000 * i + (i % 3), 30000 + i) for i in range(11)]
+    assert len(segs) == 16
+    torch.cuda.synchronize()
+    vp = ctypes.c_void_p
+    srcs = (vp * 16)(*[src.data_ptr() + a for a, _, _ in segs])
+    dsts = (vp * 16)(*[dst.data_ptr() + b for _, b, _ in segs])
+    nb = (ctypes.c_ssize_t * 16)(*[n for _, _, n in segs])
+    L.MPIX_Copy_multi_async.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(vp),
+                                        ctypes.POINTER(ctypes.c_ssize_t), ctypes.c_int, vp]
+    assert L.MPIX_Copy_multi_async(srcs, dsts, nb, 16, None) == 0
+    torch.cuda.synchronize()
+    s, d = src.cpu().numpy(), dst.cpu().numpy()
+    exp = np.zeros_like(d)
+    for a, b, n in segs:
+        exp[b:b + n] = s[a:a + n]
+    assert np.array_equal(d, exp)
 
 
 @pytest.mark.gpu

@@ -78,13 +78,14 @@ def test_reduce_scatter_random(oracle, P, case, algo, in_place, data, seed):
 @SETTINGS
 @given(P=st.integers(1, 12), case=st.sampled_from(CASES),
        algo=st.sampled_from(['reduce_scatter_allgather', 'rsag_rd_allgather',
-                             'recursive_doubling', 'ring', 'rsag_multipath']),
+                             'recursive_doubling', 'ring', 'rsag_multipath', 'pull']),
        count=st.integers(1, 200), seed=st.integers(0, 2**31))
 def test_allreduce_random(oracle, P, case, algo, count, seed):
     from mpich_amd import ccl
     dt, op, ext = case
     pof2 = 1 << (P.bit_length() - 1)
-    if algo.startswith('r') and algo != 'recursive_doubling' and count < pof2:
+    if (algo.startswith('r') or algo == 'pull') and algo != 'recursive_doubling' and \
+            count < pof2:
         count = pof2            # the reference asserts count >= pof2 there
     sends = _inputs(P, count, case, seed)
     sim = algo if algo in ('recursive_doubling', 'ring') else 'reduce_scatter_allgather'
@@ -183,14 +184,15 @@ def test_reduce_scatter_random_device(oracle, P, case, algo, in_place, data, see
 @GPU_SETTINGS
 @given(P=st.integers(2, 8), case=st.sampled_from(CASES),
        algo=st.sampled_from(['reduce_scatter_allgather', 'rsag_rd_allgather',
-                             'recursive_doubling', 'ring', 'rsag_multipath']),
+                             'recursive_doubling', 'ring', 'rsag_multipath', 'pull']),
        count=st.integers(1, 20000), seed=st.integers(0, 2**31))
 def test_allreduce_random_device(oracle, P, case, algo, count, seed):
     import torch
     from mpich_amd import ccl
     dt, op, ext = case
     pof2 = 1 << (P.bit_length() - 1)
-    if algo.startswith('r') and algo != 'recursive_doubling' and count < pof2:
+    if (algo.startswith('r') or algo == 'pull') and algo != 'recursive_doubling' and \
+            count < pof2:
         count = pof2
     sends = _inputs(P, count, case, seed)
     sim = algo if algo in ('recursive_doubling', 'ring') else 'reduce_scatter_allgather'

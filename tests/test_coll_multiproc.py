@@ -67,7 +67,8 @@ def _worker(rank, world, port, outdir, backend, cases):
             coll.allreduce(ds, dr, world * recvcount, dt, op,
                            algorithm={'allreduce': 'reduce_scatter_allgather',
                                       'allreduce_rd': 'rsag_rd_allgather',
-                                      'allreduce_mp': 'rsag_multipath'}[algo])
+                                      'allreduce_mp': 'rsag_multipath',
+                                      'allreduce_pull': 'pull'}[algo])
         else:
             dr = torch.empty(recvcount * ext, dtype=torch.uint8, device='cuda')
             timer = [] if algo == 'recursive_halving' else None
@@ -137,7 +138,8 @@ def test_staged_allreduce_matches_oracle(oracle, tmp_path, world):
     if not torch.cuda.is_available():
         pytest.skip('no GPU')
     cases = [('ar', 'allreduce', 'float', 25013), ('ar_rd', 'allreduce_rd', 'float', 25013),
-             ('ar_mp', 'allreduce_mp', 'float', 2 << 20)]    # P=4: 8 MiB parts, 2 relay chunks
+             ('ar_mp', 'allreduce_mp', 'float', 2 << 20),    # P=4: 8 MiB parts, 2 relay chunks
+             ('ar_pull', 'allreduce_pull', 'float', 25013)]
     _run(oracle, tmp_path, world, 'gloo', cases)
 
 
@@ -264,4 +266,5 @@ def test_rccl_rsb_matches_oracle(oracle, tmp_path):
              for a in ALGOS for k in ('float', 'pair')]
     cases.append(('ar', 'allreduce', 'float', 25013))
     cases.append(('ar_mp', 'allreduce_mp', 'float', 25013))
+    cases.append(('ar_pull', 'allreduce_pull', 'float', 25013))
     _run(oracle, tmp_path, world, 'nccl', cases)
