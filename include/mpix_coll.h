@@ -234,6 +234,7 @@ int MPIX_Exscan_async(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_
                                                    finished block (MPIX_Copy_multi_async); no
                                                    workspace.  P a power of two <= 16 on a device
                                                    communicator, else REDUCE_SCATTER_ALLGATHER */
+#define MPIX_ALLREDUCE_LAST                 MPIX_ALLREDUCE_PULL
 size_t MPIX_Allreduce_workspace(MPIX_Aint count, MPIX_Datatype datatype, MPIX_Comm comm);
 int MPIX_Allreduce(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Datatype datatype,
                    MPIX_Op op, MPIX_Comm comm, int algorithm, void *workspace,

@@ -1741,7 +1741,7 @@ int allreduce_entry(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Da
 {
     size_t ext;
     TRY(check_args(c, recvbuf, count, dt, op, &ext));
-    if (algorithm < MPIX_ALLREDUCE_AUTO || algorithm > MPIX_ALLREDUCE_PULL)
+    if (algorithm < MPIX_ALLREDUCE_AUTO || algorithm > MPIX_ALLREDUCE_LAST)
         return MPIX_REDOP_ERR_ARG;
     if (!count)
         return MPIX_REDOP_SUCCESS;

@@ -242,7 +242,7 @@ int main(void)
             run(P, rsb_rank, algo, 37, 1);
             run(P, rs_ragged_rank, algo, 0, 0);
         }
-        for (int algo = MPIX_ALLREDUCE_AUTO; algo <= MPIX_ALLREDUCE_RING; ++algo) {
+        for (int algo = MPIX_ALLREDUCE_AUTO; algo <= MPIX_ALLREDUCE_LAST; ++algo) {
             run(P, allreduce_rank, algo, 1031, 0);
             run(P, allreduce_rank, algo, 64, 1);
         }
