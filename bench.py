@@ -695,8 +695,9 @@ def rsb_secondary(args, world, rank, dev, out):
     refs = {'recursive_halving': recv.clone()}
     same_as = {'recursive_halving_multipath': 'recursive_halving', 'pairwise_pipelined': 'pairwise',
                'pull': 'pairwise', 'recursive_halving_pull': 'recursive_halving'}
-    for algo in ('recursive_halving_multipath', 'recursive_halving_pull', 'pairwise',
-                 'pairwise_pipelined', 'pull'):
+    # the IPC pulls last: a platform that cannot map peer memory loses only them
+    for algo in ('recursive_halving_multipath', 'pairwise', 'pairwise_pipelined',
+                 'recursive_halving_pull', 'pull'):
         rc_small = 4096 + 3
         blk = torch.cat([torch.full((rc_small,), rank + i, dtype=torch.int32, device=dev)
                          for i in range(world)])
@@ -781,10 +782,10 @@ def allreduce_secondary(args, world, rank, dev, res):
                       lambda: redop.check(ccl.allreduce(send, recv, n, H.MPI_FLOAT, H.MPI_SUM, cc,
                                                         'rsag_multipath', workspace=ws),
                                           'MPIX_Allreduce')),
+                     ('rccl_all_reduce', lambda: (recv.copy_(send), dist.all_reduce(recv))),
                      ('c_pull',
                       lambda: redop.check(ccl.allreduce(send, recv, n, H.MPI_FLOAT, H.MPI_SUM, cc,
-                                                        'pull'), 'MPIX_Allreduce')),
-                     ('rccl_all_reduce', lambda: (recv.copy_(send), dist.all_reduce(recv)))):
+                                                        'pull'), 'MPIX_Allreduce'))):
         if name == 'rccl_all_reduce' and dist.get_backend() != 'nccl':
             continue
         fn()
