@@ -122,17 +122,20 @@ int MPIX_Comm_free(MPIX_Comm comm);
                                            largest block each; below 8 MiB it is PAIRWISE):
                                            chunk k's combine, on a second stream, overlaps
                                            chunk k+1's group; same bits as PAIRWISE */
-#define MPIX_RSB_PULL               5   /* fused pull + combine: every rank maps
-                                           its peers' send buffers (hipIpc, as the reference's
-                                           GPU ipc path does, mpl_gpu_hip.c:174-204; ranks of a
-                                           local communicator share the address space) and ONE
-                                           multi-input kernel reads its block of all P-1 peers
-                                           over xGMI, folding them in the pairwise order: no
-                                           receive buffer, no copy, same bits as PAIRWISE.  A
-                                           barrier before (inputs complete) and after (peers done
-                                           reading).  Device buffers from hipMalloc; a host
-                                           communicator, or a buffer some rank cannot export,
-                                           runs PAIRWISE instead (same bits) */
+#define MPIX_RSB_PULL               5   /* fused pull + combine: ONE
+                                           multi-input kernel reads this rank's block of all P-1
+                                           peers over xGMI, folding them in the pairwise order:
+                                           no receive buffer, same bits as PAIRWISE.  Across
+                                           processes each rank copies its input into a pull
+                                           window -- library-owned device memory exported once
+                                           with hipIpc (as the reference's GPU ipc path maps
+                                           peers, mpl_gpu_hip.c:174-204), mapped once by every
+                                           peer and verified by a nonce read back through the
+                                           mapping; ranks of a local communicator read each
+                                           other's buffers directly.  A barrier before (inputs
+                                           ready) and after (peers done reading).  A host
+                                           communicator, or windows that cannot be mapped and
+                                           verified on every rank, run PAIRWISE (same bits) */
 #define MPIX_RSB_RECURSIVE_HALVING_MULTIPATH 6  /* RECURSIVE_HALVING's schedule and association
                                            (same bits), each step's exchange routed over all
                                            xGMI links: with P a power of two >= 4 and equal
@@ -147,8 +150,9 @@ int MPIX_Comm_free(MPIX_Comm comm);
                                            computed by the pull of MPIX_RSB_PULL: every rank
                                            maps its peers' send buffers and ONE tree kernel
                                            (MPIX_Reduce_local_tree_async) reads its block of
-                                           all P ranks over xGMI and folds them level by level
-                                           as the log2(P) halving steps would, writing recvbuf
+                                           all P ranks over xGMI (pull windows, as
+                                           MPIX_RSB_PULL) and folds them level by level as the
+                                           log2(P) halving steps would, writing recvbuf
                                            directly.  P a power of two <= 16 and a device
                                            communicator; otherwise RECURSIVE_HALVING */
 #define MPIX_RSB_LAST               MPIX_RSB_RECURSIVE_HALVING_PULL
@@ -227,12 +231,12 @@ int MPIX_Exscan_async(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_
                                                    count a multiple of P; else plain steps);
                                                    same bits */
 #define MPIX_ALLREDUCE_PULL                 6   /* REDUCE_SCATTER_ALLGATHER's association (same
-                                                   bits) as two pulls over hipIpc mappings: ONE
-                                                   tree kernel reads this rank's block of every
-                                                   rank's input (MPIX_Reduce_local_tree_async),
-                                                   then ONE copy kernel reads every peer's
-                                                   finished block (MPIX_Copy_multi_async); no
-                                                   workspace.  P a power of two <= 16 on a device
+                                                   bits) as two pulls (pull windows, as
+                                                   MPIX_RSB_PULL): ONE tree kernel reads this
+                                                   rank's block of every rank's input
+                                                   (MPIX_Reduce_local_tree_async), then ONE copy
+                                                   kernel reads every peer's finished block
+                                                   (MPIX_Copy_multi_async); no workspace.  P a power of two <= 16 on a device
                                                    communicator, else REDUCE_SCATTER_ALLGATHER */
 #define MPIX_ALLREDUCE_LAST                 MPIX_ALLREDUCE_PULL
 size_t MPIX_Allreduce_workspace(MPIX_Aint count, MPIX_Datatype datatype, MPIX_Comm comm);

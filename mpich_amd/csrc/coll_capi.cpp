@@ -30,6 +30,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <random>
 #include <string>
 #include <tuple>
 #include <utility>
@@ -102,7 +103,12 @@ struct MPIX_Comm_s {
     size_t stage_bytes = 0;
     hipEvent_t stage_ev = nullptr;     // recorded after the copies out of the staging memory
     char *tok = nullptr;               // barrier tokens / published records, (1 + size) slots
-    std::map<std::string, void *> ipc_maps;    // peer allocations mapped by MPIX_RSB_PULL
+    char *win = nullptr;               // pull window (header + data), see ensure_windows
+    size_t win_bytes = 0;
+    std::vector<char *> win_old;       // outgrown / rejected windows, freed with the comm
+    std::vector<const char *> peer_win;    // peers' windows, mapped and verified
+    std::vector<void *> peer_map;
+    bool win_broken = false;           // pulls given up on this communicator
     bool timing = false;               // MPIX_Comm_set_step_timing
     std::vector<std::pair<std::string, hipEvent_t>> marks;
     bool host() const { return kind == K_LOCAL_HOST || (kind == K_CUSTOM && device < 0); }
@@ -900,78 +906,155 @@ int rs_pairwise_pipelined(const char *sb, char *rb, const std::vector<size_t> &c
 size_t rs_workspace(size_t total, size_t mine, size_t ext, int size, int algo);
 int bitrev(int r, int pof2);
 
-// What a rank publishes for MPIX_RSB_PULL: the buffer its peers read, as an
-// IPC handle + offset into its allocation (another process) or as the raw
-// address (a local communicator: the ranks share the address space).
-struct PullRec {
+// ---- pull windows --------------------------------------------------------
+// The pulls read peers' memory directly.  Ranks that are threads of one
+// process (K_LOCAL_DEV) share the address space and read each other's user
+// buffers.  Across processes the memory must be mapped through hipIpc, and
+// mapping the USER buffers per call is not safe on this platform: once
+// allocations have been freed and re-made, a freshly opened handle can map
+// another allocation -- an earlier one, another rank's, even the opener's own
+// (tools/ipc_multi_probe.py: 19 of 58 reads wrong at 4 ranks on one GPU,
+// profiles/r02_ipc_multi_probe.json).  So every rank keeps a WINDOW: device
+// memory the library owns, exported once, mapped once by every peer, and
+// verified at mapping time -- its 256-byte header carries a random 128-bit
+// nonce that each peer reads back through its mapping and compares with the
+// published one; the ranks then agree that all mappings are right, or retry
+// with a new window (up to 3 times; the rejected ones stay allocated so their
+// identity is never reused), or give the pulls up for this communicator
+// (they run the RCCL-transport schedules instead, with the same bits).  A
+// call copies its input into the window (one local HBM pass), and peers read
+// it from there.  Windows grow (never shrink) to the largest message; an
+// outgrown one stays allocated until MPIX_Comm_free for the same reason.
+constexpr size_t kWinHdr = 256;
+
+struct WinRec {
+    int32_t valid;
+    int32_t pad;
+    uint64_t bytes;
+    uint64_t nonce[2];
+    char handle[sizeof(hipIpcMemHandle_t)];
+};
+static_assert(sizeof(WinRec) <= kRec, "window record size");
+
+struct LocalRec {   // K_LOCAL_DEV: the raw address
     int32_t valid;
     int32_t pad;
     uint64_t raw;
-    int64_t offset;
-    char handle[sizeof(hipIpcMemHandle_t)];
 };
-static_assert(sizeof(PullRec) <= kRec, "pull record size");
 
-// this rank's record for `p`; valid = 0 when the allocation cannot be
-// exported (every rank then sees it and takes the fallback)
-void pull_record(MPIX_Comm c, const void *p, PullRec *me)
+void close_peer_windows(MPIX_Comm c)
 {
-    memset(me, 0, sizeof *me);
-    me->raw = reinterpret_cast<uint64_t>(p);
-    me->valid = 1;
-    if (c->kind == K_LOCAL_DEV)
-        return;
-    hipDeviceptr_t base = nullptr;
-    size_t bytes = 0;
-    hipIpcMemHandle_t h;
-    if (hipMemGetAddressRange(&base, &bytes, (hipDeviceptr_t) p) != hipSuccess ||
-        hipIpcGetMemHandle(&h, (void *) base) != hipSuccess) {
-        (void) hipGetLastError();
-        me->valid = 0;
-    } else {
-        memcpy(me->handle, &h, sizeof h);
-        me->offset = (int64_t) (static_cast<const char *>(p) - static_cast<const char *>((void *) base));
-    }
+    for (void *m : c->peer_map)
+        if (m)
+            (void) hipIpcCloseMemHandle(m);
+    c->peer_map.assign(c->size, nullptr);
+    c->peer_win.assign(c->size, nullptr);
 }
 
-// the peer allocation behind `r`, mapped once and cached by handle (a
-// communicator holds at most kMaxMaps mappings; past that the cache is
-// dropped after the stream has drained the kernels that used them)
-int peer_base(MPIX_Comm c, const PullRec &r, hipStream_t s, const char **out)
+// Every rank's window holds at least `need` data bytes and every peer's is
+// mapped and verified (*ok), or the pulls are off for this communicator
+// (*ok = false on every rank).  Collective: every rank calls it with the same
+// `need` (the message size), so all ranks grow at the same calls.
+int ensure_windows(MPIX_Comm c, size_t need, hipStream_t s, bool *ok)
 {
-    if (c->kind == K_LOCAL_DEV) {
-        *out = reinterpret_cast<const char *>(r.raw);
+    *ok = false;
+    if (c->win_broken)
+        return MPIX_REDOP_SUCCESS;
+    if (c->win && c->win_bytes >= need) {
+        *ok = true;
         return MPIX_REDOP_SUCCESS;
     }
-    constexpr size_t kMaxMaps = 64;
-    std::string key(r.handle, sizeof r.handle);
-    auto it = c->ipc_maps.find(key);
-    if (it == c->ipc_maps.end()) {
-        if (c->ipc_maps.size() >= kMaxMaps) {
-            HTRY(hipStreamSynchronize(s));
-            for (auto &m : c->ipc_maps)
-                (void) hipIpcCloseMemHandle(m.second);
-            c->ipc_maps.clear();
+    const size_t bytes = std::max(need, c->win_bytes * 2 > need ? c->win_bytes * 2 : need);
+    std::random_device rd;
+    for (int attempt = 0; attempt < 3; ++attempt) {
+        void *w = nullptr;
+        WinRec me;
+        memset(&me, 0, sizeof me);
+        if (hipMalloc(&w, kWinHdr + bytes) == hipSuccess) {
+            me.nonce[0] = ((uint64_t) rd() << 32) ^ rd() ^ ((uint64_t) c->rank << 48);
+            me.nonce[1] = ((uint64_t) rd() << 32) ^ rd() ^ (uint64_t) attempt;
+            hipIpcMemHandle_t h;
+            if (hipMemcpy(w, me.nonce, sizeof me.nonce, hipMemcpyHostToDevice) == hipSuccess &&
+                hipIpcGetMemHandle(&h, w) == hipSuccess) {
+                memcpy(me.handle, &h, sizeof h);
+                me.valid = 1;
+                me.bytes = bytes;
+            }
         }
-        hipIpcMemHandle_t h;
-        memcpy(&h, r.handle, sizeof h);
-        void *base = nullptr;
-        HTRY(hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess));
-        it = c->ipc_maps.emplace(key, base).first;
+        (void) hipGetLastError();
+        std::vector<char> all;
+        TRY(allgather_records(c, &me, sizeof me, &all, s));
+        HTRY(hipStreamSynchronize(s));      // nothing in flight reads the old mappings
+        close_peer_windows(c);
+        int good = me.valid;
+        for (int q = 0; q < c->size && good; ++q) {
+            if (q == c->rank)
+                continue;
+            WinRec r;
+            memcpy(&r, all.data() + kRec * (size_t) q, sizeof r);
+            if (!r.valid || r.bytes < need) {
+                good = 0;
+                break;
+            }
+            hipIpcMemHandle_t h;
+            memcpy(&h, r.handle, sizeof h);
+            void *m = nullptr;
+            uint64_t seen[2] = {0, 0};
+            if (hipIpcOpenMemHandle(&m, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+                (void) hipGetLastError();
+                good = 0;
+                break;
+            }
+            c->peer_map[q] = m;
+            c->peer_win[q] = static_cast<const char *>(m);
+            if (hipMemcpy(seen, m, sizeof seen, hipMemcpyDeviceToHost) != hipSuccess ||
+                seen[0] != r.nonce[0] || seen[1] != r.nonce[1]) {
+                (void) hipGetLastError();
+                good = 0;
+            }
+        }
+        // agreement: every rank's mappings verified, or nobody uses them
+        std::vector<char> votes;
+        TRY(allgather_records(c, &good, sizeof good, &votes, s));
+        bool all_good = true;
+        for (int q = 0; q < c->size; ++q) {
+            int v;
+            memcpy(&v, votes.data() + kRec * (size_t) q, sizeof v);
+            all_good = all_good && v == 1;
+        }
+        if (coll_trace())
+            fprintf(stderr, "[mpix_coll rank %d] pull window %zu B attempt %d: mine %d, all %d\n",
+                    c->rank, bytes, attempt, good, (int) all_good);
+        if (all_good) {
+            if (c->win)
+                c->win_old.push_back(c->win);
+            c->win = static_cast<char *>(w);
+            c->win_bytes = bytes;
+            *ok = true;
+            return MPIX_REDOP_SUCCESS;
+        }
+        close_peer_windows(c);
+        if (w)
+            c->win_old.push_back(static_cast<char *>(w));     // never reused, see above
+        if (c->win) {       // the old windows stay mapped by nobody: re-map them next time
+            c->win_old.push_back(c->win);
+            c->win = nullptr;
+            c->win_bytes = 0;
+        }
     }
-    *out = static_cast<const char *>(it->second) + r.offset;
+    c->win_broken = true;
     return MPIX_REDOP_SUCCESS;
 }
 
 // MPIX_RSB_PULL: the pairwise schedule with the transport and the receive
-// buffers folded into the combine.  Every rank publishes the buffer holding
-// its inputs; after the stream has finished writing it (hipStreamSynchronize:
-// complete and visible to other devices) the records are all-gathered, which
-// is also the "inputs ready" barrier; ONE multi-input kernel then reads block
-// `rank` of every peer through the mappings in the order of
+// buffers folded into the combine.  Every rank's inputs become readable by
+// its peers -- in its pull window (another process: copied in, then a
+// stream-ordered barrier) or in place (threads of one process: the address
+// is all-gathered after the stream has finished writing the inputs) -- and
+// ONE multi-input kernel reads block `rank` of every peer in the order of
 // …_intra_pairwise.c:86-100 (i = 1..P-1, source rank - i), i.e. the bits of
 // PAIRWISE; a closing barrier on the stream keeps every rank from reusing its
-// buffer before all peers have pulled from it.
+// window / buffer before all peers have pulled from it.
 //
 // tree (MPIX_RSB_RECURSIVE_HALVING_PULL, P a power of two): the same pull,
 // but the kernel folds the P blocks as recursive halving's steps would
@@ -1004,43 +1087,42 @@ int rs_pull(const char *sb, char *rb, const std::vector<size_t> &cnts, MPIX_Data
     const size_t blk = cnts[rank] * ext;
     const bool in_place = sb == rb;
     char *acc = in_place ? rb + disps[rank] * ext : rb;
-    if (!in_place && !tree)
-        TRY(copy(c, rb, sb + disps[rank] * ext, blk, s));                   // :58-64
-    PullRec me;
-    pull_record(c, sb, &me);
-    HTRY(hipStreamSynchronize(s));      // this rank's inputs complete before anyone reads them
-    std::vector<char> all;
-    TRY(allgather_records(c, &me, sizeof me, &all, s));
-    std::vector<PullRec> recs(size);
-    bool ok = true;
-    for (int q = 0; q < size; ++q) {
-        memcpy(&recs[q], all.data() + kRec * (size_t) q, sizeof(PullRec));
-        ok &= recs[q].valid == 1;
-    }
-    if (coll_trace()) {
-        std::string line = "[mpix_coll rank " + std::to_string(rank) + "] pull records:";
-        for (int q = 0; q < size; ++q)
-            line += " " + std::to_string(recs[q].valid) + "/" + std::to_string(recs[q].offset);
-        fprintf(stderr, "%s\n", line.c_str());
-    }
-    if (!ok)
-        return fallback();
-    std::vector<const void *> ins;
-    if (tree) {
+    std::vector<const char *> bases(size, sb);  // where each rank's inputs are read
+    if (c->kind == K_LOCAL_DEV) {
+        // threads of one process: the user buffers themselves
+        LocalRec me{1, 0, reinterpret_cast<uint64_t>(sb)};
+        HTRY(hipStreamSynchronize(s));  // this rank's inputs complete before anyone reads them
+        std::vector<char> all;
+        TRY(allgather_records(c, &me, sizeof me, &all, s));
         for (int q = 0; q < size; ++q) {
-            const int src = rank ^ bitrev(q, size);
-            const char *base = sb;
-            if (src != rank)
-                TRY(peer_base(c, recs[src], s, &base));
-            ins.push_back(base + disps[rank] * ext);
+            LocalRec r;
+            memcpy(&r, all.data() + kRec * (size_t) q, sizeof r);
+            bases[q] = reinterpret_cast<const char *>(r.raw);
         }
     } else {
-        for (int i = 1; i < size; ++i) {
-            const int src = (rank - i + size) % size;
-            const char *base;
-            TRY(peer_base(c, recs[src], s, &base));
-            ins.push_back(base + disps[rank] * ext);
-        }
+        bool ok;
+        TRY(ensure_windows(c, total * ext, s, &ok));
+        if (!ok)
+            return fallback();
+        // the blocks the peers read (this rank's own block is read from sb)
+        char *wd = c->win + kWinHdr;
+        TRY(copy(c, wd, sb, disps[rank] * ext, s));
+        TRY(copy(c, wd + (disps[rank] + cnts[rank]) * ext, sb + (disps[rank] + cnts[rank]) * ext,
+                 (total - disps[rank] - cnts[rank]) * ext, s));
+        TRY(barrier(c, s));             // every window filled
+        for (int q = 0; q < size; ++q)
+            if (q != rank)
+                bases[q] = c->peer_win[q] + kWinHdr;
+    }
+    if (!in_place && !tree)
+        TRY(copy(c, rb, sb + disps[rank] * ext, blk, s));                   // :58-64
+    std::vector<const void *> ins;
+    if (tree) {
+        for (int q = 0; q < size; ++q)
+            ins.push_back(bases[rank ^ bitrev(q, size)] + disps[rank] * ext);
+    } else {
+        for (int i = 1; i < size; ++i)
+            ins.push_back(bases[(rank - i + size) % size] + disps[rank] * ext);
     }
     TRY(mark(c, "publish", s));
     if (cnts[rank] && tree)
@@ -1048,7 +1130,7 @@ int rs_pull(const char *sb, char *rb, const std::vector<size_t> &cnts, MPIX_Data
     else if (cnts[rank])
         TRY(combine_multi(c, ins, acc, (MPIX_Aint) cnts[rank], dt, op, s));
     TRY(mark(c, "pull+combine", s));
-    TRY(barrier(c, s));                 // peers done reading this rank's buffer
+    TRY(barrier(c, s));                 // peers done reading this rank's buffer / window
     if (in_place && rank != 0) {
         if (disps[rank] * ext < blk) {
             char *w;
@@ -1244,11 +1326,12 @@ int allreduce_rsag(char *rb, size_t count, MPIX_Datatype dt, MPIX_Op op, MPIX_Co
 // bitrev(r) (the halving steps of :138-189 keep the half selected by bit 0,
 // then bit 1, ...), which recursive halving with masks 1, 2, 4, ... folds as
 // MPIX_Reduce_local_tree_async does with slot s = r ^ s; ONE tree kernel reads
-// that block of every rank's input and writes it into recvbuf.  Allgather:
-// after a barrier, ONE copy kernel reads every peer's finished block from its
-// recvbuf (MPIX_Copy_multi_async).  A closing barrier keeps every rank's
-// buffers in place until its peers are done.  No sendbuf -> recvbuf copy and
-// no workspace.  Other shapes: the sendbuf copy + REDUCE_SCATTER_ALLGATHER.
+// that block of every rank's input (peers' from their pull windows, or from
+// their buffers for threads of one process) and writes it out.  Allgather:
+// after a barrier, ONE copy kernel reads every peer's finished block
+// (MPIX_Copy_multi_async).  A closing barrier keeps every rank's window /
+// buffers in place until its peers are done.  No workspace.  Other shapes:
+// the sendbuf copy + REDUCE_SCATTER_ALLGATHER.
 int allreduce_rsag(char *rb, size_t count, MPIX_Datatype dt, MPIX_Op op, MPIX_Comm c, char *tmp,
                    hipStream_t s, size_t ext, bool direct, bool multipath);
 
@@ -1273,49 +1356,58 @@ int allreduce_pull(const char *sendbuf, char *rb, size_t count, MPIX_Datatype dt
         cnts[i] = count / size + ((size_t) i < count % size ? 1 : 0);
     for (int i = 1; i < size; ++i)
         disps[i] = disps[i - 1] + cnts[i - 1];
-    struct Recs {
-        PullRec in, out;
-    } me;
-    static_assert(sizeof(Recs) <= kRec, "allreduce pull records");
-    pull_record(c, in, &me.in);
-    pull_record(c, rb, &me.out);
-    TRY(mark(c, "start", s));
-    HTRY(hipStreamSynchronize(s));      // inputs complete before anyone reads them
-    std::vector<char> all;
-    TRY(allgather_records(c, &me, sizeof me, &all, s));
-    std::vector<Recs> recs(size);
-    bool ok = true;
-    for (int q = 0; q < size; ++q) {
-        memcpy(&recs[q], all.data() + kRec * (size_t) q, sizeof(Recs));
-        ok &= recs[q].in.valid == 1 && recs[q].out.valid == 1;
-    }
-    if (!ok)
-        return fallback();
-    TRY(mark(c, "publish", s));
     const int mine = bitrev(rank, size);
-    std::vector<const void *> ins(size);
-    for (int q = 0; q < size; ++q) {
-        const int src = rank ^ q;
-        const char *base = in;
-        if (src != rank)
-            TRY(peer_base(c, recs[src].in, s, &base));
-        ins[q] = base + disps[mine] * ext;
+    // in_base[q]: where rank q's input is read; out_base[q]: where its
+    // reduced block is read in the allgather; out: where this rank's goes
+    std::vector<const char *> in_base(size, in), out_base(size, rb);
+    char *out = rb + disps[mine] * ext;
+    TRY(mark(c, "start", s));
+    if (c->kind == K_LOCAL_DEV) {     // threads of one process: the user buffers
+        struct Recs {
+            LocalRec in, out;
+        } me{{1, 0, reinterpret_cast<uint64_t>(in)}, {1, 0, reinterpret_cast<uint64_t>(rb)}};
+        static_assert(sizeof(Recs) <= kRec, "allreduce pull records");
+        HTRY(hipStreamSynchronize(s));  // inputs complete before anyone reads them
+        std::vector<char> all;
+        TRY(allgather_records(c, &me, sizeof me, &all, s));
+        for (int q = 0; q < size; ++q) {
+            Recs r;
+            memcpy(&r, all.data() + kRec * (size_t) q, sizeof r);
+            in_base[q] = reinterpret_cast<const char *>(r.in.raw);
+            out_base[q] = reinterpret_cast<const char *>(r.out.raw);
+        }
+    } else {                            // processes: the pull windows
+        bool ok;
+        TRY(ensure_windows(c, nb, s, &ok));
+        if (!ok)
+            return fallback();
+        char *wd = c->win + kWinHdr;
+        TRY(copy(c, wd, in, disps[mine] * ext, s));     // every block but this rank's own
+        TRY(copy(c, wd + (disps[mine] + cnts[mine]) * ext, in + (disps[mine] + cnts[mine]) * ext,
+                 nb - (disps[mine] + cnts[mine]) * ext, s));
+        TRY(barrier(c, s));             // every window filled
+        for (int q = 0; q < size; ++q)
+            if (q != rank)
+                in_base[q] = out_base[q] = c->peer_win[q] + kWinHdr;
+        out = wd + disps[mine] * ext;   // peers read it from the window
     }
+    TRY(mark(c, "publish", s));
+    std::vector<const void *> ins(size);
+    for (int q = 0; q < size; ++q)
+        ins[q] = in_base[rank ^ q] + disps[mine] * ext;
     if (cnts[mine])
-        TRY(MPIX_Reduce_local_tree_async(ins.data(), size, rb + disps[mine] * ext,
-                                         (MPIX_Aint) cnts[mine], dt, op, s));
+        TRY(MPIX_Reduce_local_tree_async(ins.data(), size, out, (MPIX_Aint) cnts[mine], dt, op, s));
     TRY(mark(c, "reduce-scatter pull", s));
     TRY(barrier(c, s));                 // every block final (and every input read)
     std::vector<const void *> srcs;
     std::vector<void *> dsts;
     std::vector<MPIX_Aint> bytes;
     for (int q = 0; q < size; ++q) {
-        if (q == rank)
-            continue;
         const int b = bitrev(q, size);
-        const char *base;
-        TRY(peer_base(c, recs[q].out, s, &base));
-        srcs.push_back(base + disps[b] * ext);
+        const char *src = q == rank ? out : out_base[q] + disps[b] * ext;
+        if (src == rb + disps[b] * ext)
+            continue;                   // this rank's block already in place
+        srcs.push_back(src);
         dsts.push_back(rb + disps[b] * ext);
         bytes.push_back((MPIX_Aint) (cnts[b] * ext));
     }
@@ -2004,8 +2096,13 @@ int MPIX_Comm_free(MPIX_Comm comm)
             (void) hipHostFree(comm->stage);
         if (comm->tok)
             (void) hipFree(comm->tok);
-        for (auto &m : comm->ipc_maps)
-            (void) hipIpcCloseMemHandle(m.second);
+        for (void *m : comm->peer_map)
+            if (m)
+                (void) hipIpcCloseMemHandle(m);
+        if (comm->win)
+            (void) hipFree(comm->win);
+        for (char *w : comm->win_old)
+            (void) hipFree(w);
         for (auto &m : comm->marks)
             (void) hipEventDestroy(m.second);
     } else {

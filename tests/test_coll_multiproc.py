@@ -133,6 +133,61 @@ def test_staged_pipelined_large_blocks(oracle, tmp_path):
     _run(oracle, tmp_path, 2, 'gloo', cases)
 
 
+def _churn_worker(rank, world, port, outdir):
+    import torch.distributed as dist
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from mpich_amd import coll
+    MPI_INT = 0x4c000405
+    n = 65536 + 7
+    bad = []
+    for it in range(4):
+        for algo in ('pull', 'recursive_halving_pull', 'allreduce_pull'):
+            # block i of rank r holds r + i + 100 * it (redscatblk3.c:43-48), in a
+            # fresh allocation each time: the previous one went back to the
+            # driver, so a peer's cached mapping of it would read stale data
+            blk = torch.cat([torch.full((n,), rank + i + 100 * it, dtype=torch.int32, device='cuda')
+                             for i in range(world)])
+            torch.cuda.synchronize()
+            if algo == 'allreduce_pull':
+                out = torch.empty_like(blk)
+                coll.allreduce(blk, out, world * n, MPI_INT, MPI_SUM, algorithm='pull')
+                exp = torch.cat([torch.full((n,), sum(q + i + 100 * it for q in range(world)),
+                                            dtype=torch.int32, device='cuda')
+                                 for i in range(world)])
+            else:
+                out = torch.empty(n, dtype=torch.int32, device='cuda')
+                coll.reduce_scatter_block(blk, out, n, MPI_INT, MPI_SUM, algorithm=algo)
+                exp = torch.full((n,), world * rank + world * (world - 1) // 2 + world * 100 * it,
+                                 dtype=torch.int32, device='cuda')
+            torch.cuda.synchronize()
+            if not torch.equal(out, exp):
+                bad.append('%s@%d' % (algo, it))
+            dist.barrier()          # every peer done with this round's buffers
+            del blk, out, exp
+            torch.cuda.empty_cache()
+    with open(os.path.join(outdir, 'churn%d.txt' % rank), 'w') as f:
+        f.write(' '.join(bad))
+    dist.barrier()
+    coll.free_comms()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world', [2, 4])
+def test_staged_pulls_with_buffer_churn(tmp_path, world):
+    """the pulls map peers' allocations once and cache the mappings: a buffer
+    freed back to the driver and re-made (likely at the same address, maybe
+    with the same IPC handle bytes) must not be read through the old mapping
+    -- the published allocation identity invalidates it"""
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    mp.spawn(_churn_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    for r in range(world):
+        assert open(tmp_path / ('churn%d.txt' % r)).read() == '', r
+
+
 @pytest.mark.parametrize('world', [3, 4])
 def test_staged_allreduce_matches_oracle(oracle, tmp_path, world):
     if not torch.cuda.is_available():
