@@ -980,6 +980,11 @@ int ensure_windows(MPIX_Comm c, size_t need, hipStream_t s, bool *ok)
                 me.valid = 1;
                 me.bytes = bytes;
             }
+            // test hook: this rank publishes a nonce its window does not hold, as
+            // a mapping of the wrong memory would show it to the peers
+            const char *fault = getenv("MPIX_COLL_WINDOW_FAULT");
+            if (fault && atoi(fault) == c->rank)
+                me.nonce[1] ^= 1;
         }
         (void) hipGetLastError();
         std::vector<char> all;

@@ -188,6 +188,26 @@ def test_staged_pulls_with_buffer_churn(tmp_path, world):
         assert open(tmp_path / ('churn%d.txt' % r)).read() == '', r
 
 
+def _fault_worker(rank, world, port, outdir):
+    os.environ['MPIX_COLL_WINDOW_FAULT'] = '1'      # rank 1's window fails verification
+    _worker(rank, world, port, outdir, 'gloo',
+            [('pull_f', 'pull', 'float', 40009), ('rhp_f', 'recursive_halving_pull', 'float', 40009),
+             ('arp_f', 'allreduce_pull', 'float', 40009)])
+
+
+def test_staged_pull_window_verification_failure(oracle, tmp_path):
+    """a window whose nonce does not read back on every peer: all ranks retry
+    (3 times), then agree to give the pulls up and run the RCCL-transport
+    schedules -- same bits as the oracle, nobody hangs"""
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    world = 4
+    mp.spawn(_fault_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    _check(oracle, tmp_path, world,
+           [('pull_f', 'pull', 'float', 40009), ('rhp_f', 'recursive_halving_pull', 'float', 40009),
+            ('arp_f', 'allreduce_pull', 'float', 40009)])
+
+
 @pytest.mark.parametrize('world', [3, 4])
 def test_staged_allreduce_matches_oracle(oracle, tmp_path, world):
     if not torch.cuda.is_available():
