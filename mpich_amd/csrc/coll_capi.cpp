@@ -471,6 +471,25 @@ int combine_multi(MPIX_Comm c, const std::vector<const void *> &ins, void *inout
     return MPIX_REDOP_SUCCESS;
 }
 
+int combine_to(MPIX_Comm c, const void *a, const void *b, void *out, MPIX_Aint count,
+               MPIX_Datatype dt, MPIX_Op op, hipStream_t s, size_t ext)
+{
+    if (out == a || count == 0)
+        return count ? combine(c, b, out, count, dt, op, s) : MPIX_REDOP_SUCCESS;
+    if (!c->combine && !c->host()) {
+        const void *ins[2] = {a, b};
+        return MPIX_Reduce_local_tree_async(ins, 2, out, count, dt, op, s);
+    }
+    TRY(copy(c, out, a, (size_t) count * ext, s));
+    return combine(c, b, out, count, dt, op, s);
+}
+
+// out = a OP b (a in the inout role, b in the in role) without first copying
+// a into out: one 2-slot tree kernel (MPIX_Reduce_local_tree_async); host /
+// custom-combine communicators copy, then combine -- the same operands either way
+int combine_to(MPIX_Comm c, const void *a, const void *b, void *out, MPIX_Aint count,
+               MPIX_Datatype dt, MPIX_Op op, hipStream_t s, size_t ext);
+
 // The communicator's scratch is shared by every collective issued on it, on
 // any stream: a new user is ordered behind the previous one on the device
 // (stream wait on scratch_ev, no host sync), and the buffer is only freed
@@ -587,10 +606,18 @@ int rs_recursive_halving(const char *sb, char *rb, const std::vector<size_t> &cn
         return MPIX_REDOP_SUCCESS;
     char *tmp_results = ws;
     char *tmp_recvbuf = ws + round256(total * ext);
-    TRY(mark(c, "start", s));
-    TRY(copy(c, tmp_results, sb, total * ext, s));                         // :91-96
-    TRY(mark(c, "local copy", s));
     const int pof2 = pof2_of(size), rem = size - pof2;
+    // P a power of two: no up-front copy of sendbuf into tmp_results (:91-96);
+    // the first step reads its halves from sendbuf and writes the combined
+    // half into tmp_results, the last writes this rank's block into recvbuf
+    // -- the same operands in the same roles, one HBM pass of the whole
+    // vector less
+    const bool direct = rem == 0;
+    TRY(mark(c, "start", s));
+    if (!direct) {
+        TRY(copy(c, tmp_results, sb, total * ext, s));                     // :91-96
+        TRY(mark(c, "local copy", s));
+    }
     int newrank;
     if (rank < 2 * rem) {                                                   // :110-137
         if (rank % 2 == 0) {
@@ -620,6 +647,7 @@ int rs_recursive_halving(const char *sb, char *rb, const std::vector<size_t> &cn
             return t;
         };
         int mask = pof2 >> 1, send_idx = 0, recv_idx = 0, last_idx = pof2;
+        bool in_rb = false;         // this rank's block already written to recvbuf
         while (mask > 0) {
             int newdst = newrank ^ mask;
             int dst = newdst < rem ? newdst * 2 + 1 : newdst + rem;
@@ -633,18 +661,25 @@ int rs_recursive_halving(const char *sb, char *rb, const std::vector<size_t> &cn
                 send_cnt = sum(send_idx, recv_idx);
                 recv_cnt = sum(recv_idx, last_idx);
             }
+            const char *cur = direct && mask == pof2 >> 1 ? sb : tmp_results;
             // zero-length legs are skipped on both sides (:188-208)
-            TRY(exchange(c, {snd(dst, tmp_results + newdisps[send_idx] * ext, send_cnt * ext),
+            TRY(exchange(c, {snd(dst, cur + newdisps[send_idx] * ext, send_cnt * ext),
                              rcv(dst, tmp_recvbuf + newdisps[recv_idx] * ext, recv_cnt * ext)}, s));
             TRY(mark(c, "exchange", s));
-            TRY(combine(c, tmp_recvbuf + newdisps[recv_idx] * ext,
-                        tmp_results + newdisps[recv_idx] * ext, (MPIX_Aint) recv_cnt, dt, op, s));
+            char *out = tmp_results + newdisps[recv_idx] * ext;
+            if (direct && mask == 1 && recv_idx == newrank) {
+                out = rb;           // the last step's half is this rank's block
+                in_rb = true;
+            }
+            TRY(combine_to(c, cur + newdisps[recv_idx] * ext, tmp_recvbuf + newdisps[recv_idx] * ext,
+                           out, (MPIX_Aint) recv_cnt, dt, op, s, ext));
             TRY(mark(c, "combine", s));
             send_idx = recv_idx;
             last_idx = recv_idx + mask;
             mask >>= 1;
         }
-        TRY(copy(c, rb, tmp_results + disps[rank] * ext, cnts[rank] * ext, s));   // :232-240
+        if (!in_rb)
+            TRY(copy(c, rb, tmp_results + disps[rank] * ext, cnts[rank] * ext, s));   // :232-240
     }
     if (rank < 2 * rem) {                                                   // :245-262
         if (rank % 2)
@@ -754,27 +789,35 @@ int rs_recursive_halving_multipath(const char *sb, char *rb, const std::vector<s
     char *tmp_recvbuf = ws + round256(total * ext);
     char *relay = tmp_recvbuf + round256(total * ext);     // (P/2 - 1) part slots
     const size_t slot = round256(rc * ext);                 // a part is at most one block
+    // as rs_recursive_halving with P a power of two: the first step reads
+    // sendbuf, the last writes this rank's block into recvbuf (no copies)
     TRY(mark(c, "start", s));
-    TRY(copy(c, tmp_results, sb, total * ext, s));                         // :91-96
-    TRY(mark(c, "local copy", s));
     int mask = size >> 1, send_idx = 0, recv_idx = 0;
+    bool in_rb = false;
     while (mask > 0) {
         if (rank < (rank ^ mask))
             send_idx = recv_idx + mask;
         else
             recv_idx = send_idx + mask;
         const size_t D = (size_t) mask * rc;             // both halves, every rank
+        const char *cur = mask == size >> 1 ? sb : tmp_results;
         char *rbase = tmp_recvbuf + (size_t) recv_idx * rc * ext;
-        TRY(multipath_exchange(c, tmp_results + (size_t) send_idx * rc * ext, rbase, D, mask,
-                               relay, slot, s, ext));
+        TRY(multipath_exchange(c, cur + (size_t) send_idx * rc * ext, rbase, D, mask, relay, slot,
+                               s, ext));
         TRY(mark(c, "exchange", s));
-        TRY(combine(c, rbase, tmp_results + (size_t) recv_idx * rc * ext, (MPIX_Aint) D, dt, op,
-                    s));
+        char *out = tmp_results + (size_t) recv_idx * rc * ext;
+        if (mask == 1 && recv_idx == rank) {
+            out = rb;
+            in_rb = true;
+        }
+        TRY(combine_to(c, cur + (size_t) recv_idx * rc * ext, rbase, out, (MPIX_Aint) D, dt, op, s,
+                       ext));
         TRY(mark(c, "combine", s));
         send_idx = recv_idx;
         mask >>= 1;
     }
-    TRY(copy(c, rb, tmp_results + (size_t) rank * rc * ext, rc * ext, s));   // :232-240
+    if (!in_rb)
+        TRY(copy(c, rb, tmp_results + (size_t) rank * rc * ext, rc * ext, s));   // :232-240
     TRY(mark(c, "epilogue", s));
     return MPIX_REDOP_SUCCESS;
 }
