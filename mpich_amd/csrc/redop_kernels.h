@@ -222,39 +222,47 @@ k_elem_multi(MultiIn<typename C::unit> ins, int k, typename C::unit *__restrict_
 // (over xGMI for the peers') and writes one.  Unused slots (s >= k) are
 // compile-time registers whose loads and combines are skipped by uniform
 // branches, so one instantiation serves every k.
-template <class C>
+template <class C, int KMAX, int U>
 __global__ void __launch_bounds__(256)
 k_contig_tree(MultiIn<typename C::unit> ins, int k, typename C::unit *__restrict__ out,
               uint64_t head, uint64_t npk, uint64_t tail_start, uint32_t ntail, Params prm)
 {
     using T = typename C::unit;
     v4u *vout = reinterpret_cast<v4u *>(out + head);
-    const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x; i < npk; i += stride) {
-        v4u v[kMaxMulti];
+    const uint64_t nt = blockDim.x;
+    const uint64_t stride = (uint64_t) gridDim.x * nt * U;
+    for (uint64_t i = (uint64_t) blockIdx.x * nt * U + threadIdx.x; i < npk; i += stride) {
+        v4u v[U][KMAX];
 #pragma unroll
-        for (int q = 0; q < kMaxMulti; ++q)
-            if (q < k)
-                v[q] = ld16<true>(reinterpret_cast<const v4u *>(ins.p[q] + head) + i);
+        for (int u = 0; u < U; ++u)
 #pragma unroll
-        for (int m = 1; m < kMaxMulti; m <<= 1)
+            for (int q = 0; q < KMAX; ++q)
+                if (q < k && i + u * nt < npk)
+                    v[u][q] = ld16<true>(reinterpret_cast<const v4u *>(ins.p[q] + head) + i + u * nt);
 #pragma unroll
-            for (int q = 0; q < kMaxMulti; q += 2 * m)
-                if (q + m < k)
-                    v[q] = combine16<C>(v[q], v[q + m], prm);
-        st16<true>(vout + i, v[0]);
+        for (int u = 0; u < U; ++u) {
+            if (i + u * nt >= npk)
+                continue;
+#pragma unroll
+            for (int m = 1; m < KMAX; m <<= 1)
+#pragma unroll
+                for (int q = 0; q < KMAX; q += 2 * m)
+                    if (q + m < k)
+                        v[u][q] = combine16<C>(v[u][q], v[u][q + m], prm);
+            st16<true>(vout + i + u * nt, v[u][0]);
+        }
     }
     if (blockIdx.x == 0) {
         auto one = [&](uint64_t t) {
-            T v[kMaxMulti];
+            T v[KMAX];
 #pragma unroll
-            for (int q = 0; q < kMaxMulti; ++q)
+            for (int q = 0; q < KMAX; ++q)
                 if (q < k)
                     v[q] = ins.p[q][t];
 #pragma unroll
-            for (int m = 1; m < kMaxMulti; m <<= 1)
+            for (int m = 1; m < KMAX; m <<= 1)
 #pragma unroll
-                for (int q = 0; q < kMaxMulti; q += 2 * m)
+                for (int q = 0; q < KMAX; q += 2 * m)
                     if (q + m < k)
                         v[q] = C::apply(v[q], v[q + m], prm);
             out[t] = v[0];
@@ -549,8 +557,12 @@ hipError_t launch_tree(const void *const *ins, int k, void *out, uint64_t count,
         uint64_t npk = (count - head) / E;
         uint64_t tail_start = head + npk * E;
         uint32_t ntail = (uint32_t) (count - tail_start);
-        hipLaunchKernelGGL((k_contig_tree<C>), dim3(grid_for(256, npk, 0)), dim3(256), 0, s, mi, k,
-                           tout, head, npk, tail_start, ntail, prm);
+        if (k == 2)     // out = a OP b: the contiguous kernel's 4 packets per lane
+            hipLaunchKernelGGL((k_contig_tree<C, 2, 4>), dim3(grid_for(256 * 4, npk, 0)),
+                               dim3(256), 0, s, mi, k, tout, head, npk, tail_start, ntail, prm);
+        else
+            hipLaunchKernelGGL((k_contig_tree<C, kMaxMulti, 1>), dim3(grid_for(256, npk, 0)),
+                               dim3(256), 0, s, mi, k, tout, head, npk, tail_start, ntail, prm);
     } else {
         hipLaunchKernelGGL((k_elem_tree<C>), dim3(grid_for(256 * 4, count, 0)), dim3(256), 0, s,
                            mi, k, tout, count, prm);
