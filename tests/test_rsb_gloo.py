@@ -192,6 +192,8 @@ def test_allreduce_gloo(oracle, tmp_path, world, algo):
     recursive-doubling allgather): bit-identical on every rank to the
     oracle's simulation of the reference schedule, and all allred.c KATs
     generated for this world size pass end to end."""
+    if algo == 'rsag_multipath' and world not in (4, 8):
+        pytest.skip('other P run the plain steps (the fallback is covered in test_coll_c)')
     count = 4096 if algo == 'rsag_multipath' else 1037    # multipath: P | count
     mp.spawn(_ar_worker, args=(world, _free_port(), str(tmp_path), count, algo), nprocs=world,
              join=True)
