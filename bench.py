@@ -694,10 +694,21 @@ def rsb_secondary(args, world, rank, dev, out):
                                          'recursive_halving'), 'MPIX_Reduce_scatter_block')
     refs = {'recursive_halving': recv.clone()}
     same_as = {'recursive_halving_multipath': 'recursive_halving', 'pairwise_pipelined': 'pairwise',
-               'pull': 'pairwise', 'recursive_halving_pull': 'recursive_halving'}
-    # the IPC pulls last: a platform that cannot map peer memory loses only them
-    for algo in ('recursive_halving_multipath', 'pairwise', 'pairwise_pipelined',
-                 'recursive_halving_pull', 'pull'):
+               'pull': 'pairwise', 'recursive_halving_pull': 'recursive_halving',
+               'recursive_halving_pull_shared': 'recursive_halving'}
+    # the IPC pulls last: a platform that cannot map peer memory loses only them;
+    # the last reads its input from symmetric memory (MPIX_Comm_alloc_shared)
+    # in place, without the copy into the pull window
+    legs = [(a, a, False) for a in ('recursive_halving_multipath', 'pairwise', 'pairwise_pipelined',
+                                    'recursive_halving_pull', 'pull')]
+    legs.append(('recursive_halving_pull_shared', 'recursive_halving_pull', True))
+    shared = None
+    for name, algo, on_shared in legs:
+        if on_shared and shared is None:
+            shared = cc.shared_tensor(total, torch.float32)
+            shared.copy_(send)
+            torch.cuda.synchronize()
+        src = shared if on_shared else send
         rc_small = 4096 + 3
         blk = torch.cat([torch.full((rc_small,), rank + i, dtype=torch.int32, device=dev)
                          for i in range(world)])
@@ -711,17 +722,17 @@ def rsb_secondary(args, world, rank, dev, out):
             raise RuntimeError('%s RSB fails the redscatblk3 closed form' % algo)
 
         def once():
-            redop.check(ccl.reduce_scatter_block(send, recv, recvcount, H.MPI_FLOAT, H.MPI_SUM, cc,
+            redop.check(ccl.reduce_scatter_block(src, recv, recvcount, H.MPI_FLOAT, H.MPI_SUM, cc,
                                                  algo), 'MPIX_Reduce_scatter_block')
         once()
         bits = None
-        if algo == 'pairwise':
+        if name == 'pairwise':
             refs['pairwise'] = recv.clone()
-        elif algo in same_as:
-            same = bool(torch.equal(recv.view(torch.int32), refs[same_as[algo]].view(torch.int32)))
+        elif name in same_as:
+            same = bool(torch.equal(recv.view(torch.int32), refs[same_as[name]].view(torch.int32)))
             if not allreduce_scalar(1 if same else 0, dist.ReduceOp.MIN, dev):
-                raise RuntimeError('%s RSB differs from %s at the timed size' % (algo, same_as[algo]))
-            bits = same_as[algo]
+                raise RuntimeError('%s RSB differs from %s at the timed size' % (name, same_as[name]))
+            bits = same_as[name]
         reps = max(3, min(10, args.steps))
         dist.barrier()
         torch.cuda.synchronize()
@@ -742,12 +753,14 @@ def rsb_secondary(args, world, rank, dev, out):
         else:   # pairwise family and the pulls: one block per peer link, all links at once
             link_bytes = total * 4 / world
             links = world - 1
-        out[algo] = dict(parity_redscatblk3_all_ranks=True, ms=round(t * 1e3, 3),
+        out[name] = dict(parity_redscatblk3_all_ranks=True, ms=round(t * 1e3, 3),
                          bit_identical_to=bits,
                          busbw_GBs=round((world - 1) / world * total * 4 / t / 1e9, 2),
                          per_link_GBs=round(link_bytes / t / 1e9, 2), links_active=links,
                          frac_of_xgmi_link=round(link_bytes / t / 1e9 / XGMI_LINK_GBS, 4))
-    del send, recv, refs
+    if shared is not None:
+        cc.free_shared(shared.data_ptr())
+    del send, recv, refs, shared
     torch.cuda.empty_cache()
 
 
@@ -774,6 +787,7 @@ def allreduce_secondary(args, world, rank, dev, res):
     ws = torch.empty(n * 4, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
     res.update(parity_allred_sum_test_1_all_ranks=True, bytes_per_rank=n * 4, P=world)
+    sh_in = sh_out = None
     for name, fn in (('c_reduce_scatter_allgather',
                       lambda: redop.check(ccl.allreduce(send, recv, n, H.MPI_FLOAT, H.MPI_SUM, cc,
                                                         'reduce_scatter_allgather', workspace=ws),
@@ -785,14 +799,23 @@ def allreduce_secondary(args, world, rank, dev, res):
                      ('rccl_all_reduce', lambda: (recv.copy_(send), dist.all_reduce(recv))),
                      ('c_pull',
                       lambda: redop.check(ccl.allreduce(send, recv, n, H.MPI_FLOAT, H.MPI_SUM, cc,
-                                                        'pull'), 'MPIX_Allreduce'))):
+                                                        'pull'), 'MPIX_Allreduce')),
+                     ('c_pull_shared',     # input and result in symmetric memory: no window copy
+                      lambda: redop.check(ccl.allreduce(sh_in, sh_out, n, H.MPI_FLOAT, H.MPI_SUM,
+                                                        cc, 'pull'), 'MPIX_Allreduce'))):
         if name == 'rccl_all_reduce' and dist.get_backend() != 'nccl':
             continue
+        if name == 'c_pull_shared':
+            sh_in = cc.shared_tensor(n, torch.float32)
+            sh_out = cc.shared_tensor(n, torch.float32)
+            sh_in.copy_(send)
+            torch.cuda.synchronize()
         fn()
         if name == 'c_reduce_scatter_allgather':
             ref = recv.clone()
-        elif name in ('c_rsag_multipath', 'c_pull'):    # same association, so the same bits
-            same = bool(torch.equal(recv.view(torch.int32), ref.view(torch.int32)))
+        elif name in ('c_rsag_multipath', 'c_pull', 'c_pull_shared'):  # same association
+            got = sh_out if name == 'c_pull_shared' else recv
+            same = bool(torch.equal(got.view(torch.int32), ref.view(torch.int32)))
             if not allreduce_scalar(1 if same else 0, dist.ReduceOp.MIN, dev):
                 raise RuntimeError('%s allreduce differs from reduce_scatter_allgather' % name)
             res['%s_bit_identical_all_ranks' % name[2:]] = True
@@ -807,7 +830,10 @@ def allreduce_secondary(args, world, rank, dev, res):
         t = allreduce_scalar((time.perf_counter() - t0) / reps, dist.ReduceOp.MAX, dev)
         res[name] = dict(ms=round(t * 1e3, 3),
                          busbw_GBs=round(2 * (world - 1) / world * n * 4 / t / 1e9, 2))
-    del send, recv, ws, ref
+    if sh_in is not None:
+        cc.free_shared(sh_in.data_ptr())
+        cc.free_shared(sh_out.data_ptr())
+    del send, recv, ws, ref, sh_in, sh_out
     torch.cuda.empty_cache()
 
 

@@ -255,6 +255,20 @@ int MPIX_Comm_set_stream(MPIX_Comm comm, void *stream);
  * reached its own barrier). */
 int MPIX_Comm_barrier(MPIX_Comm comm);
 
+/* Symmetric device memory for the pull schedules (as NCCL's registered user
+ * buffers): every rank calls MPIX_Comm_alloc_shared together with the same
+ * `bytes`; each gets `bytes` of device memory that is exported once, mapped
+ * by every peer and verified through the mapping (the nonce check of the
+ * pull windows).  A pull schedule (MPIX_RSB_PULL,
+ * MPIX_RSB_RECURSIVE_HALVING_PULL, MPIX_ALLREDUCE_PULL) whose buffers lie in
+ * such memory at the same offset on every rank reads the peers' copies in
+ * place, without first copying its input into the pull window.  Collective;
+ * MPI_ERR_OTHER on every rank if no verified mapping could be made.
+ * MPIX_Comm_free_shared is collective too; the memory itself is released by
+ * MPIX_Comm_free. */
+int MPIX_Comm_alloc_shared(MPIX_Comm comm, size_t bytes, void **ptr);
+int MPIX_Comm_free_shared(MPIX_Comm comm, void *ptr);
+
 /* Per-step breakdown of the device schedules: with
  * timing on, every exchange and combine step of the next collectives records
  * a HIP event on the collective's stream; MPIX_Comm_step_times() (after the

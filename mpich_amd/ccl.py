@@ -68,6 +68,8 @@ def lib():
             'MPIX_Comm_set_combine': ([vp, vp], i32),
             'MPIX_Comm_set_stream': ([vp, vp], i32),
             'MPIX_Comm_barrier': ([vp], i32),
+            'MPIX_Comm_alloc_shared': ([vp, sz, ctypes.POINTER(vp)], i32),
+            'MPIX_Comm_free_shared': ([vp, vp], i32),
             'MPIX_Comm_set_step_timing': ([vp, i32], i32),
             'MPIX_Comm_step_times': ([vp, ctypes.POINTER(ctypes.c_double), vp, i32,
                                       ctypes.POINTER(i32)], i32),
@@ -145,6 +147,35 @@ class Comm:
 
     def barrier(self):
         redop.check(lib().MPIX_Comm_barrier(self.h), 'MPIX_Comm_barrier')
+
+    def alloc_shared(self, nbytes):
+        """collective MPIX_Comm_alloc_shared: the device address of `nbytes` of
+        symmetric memory the pull schedules read in place"""
+        p = ctypes.c_void_p()
+        redop.check(lib().MPIX_Comm_alloc_shared(self.h, nbytes, ctypes.byref(p)),
+                    'MPIX_Comm_alloc_shared')
+        return p.value
+
+    def shared_tensor(self, numel, dtype):
+        """a torch tensor over fresh shared memory of `numel` elements
+        (collective; the memory lives until free_shared / free)"""
+        import torch
+        esize = torch.empty((), dtype=dtype).element_size()
+        ptr = self.alloc_shared(numel * esize)
+        typestr = {torch.float32: '<f4', torch.float64: '<f8', torch.int32: '<i4',
+                   torch.int64: '<i8', torch.uint8: '|u1'}[dtype]
+
+        class _Dev:     # __cuda_array_interface__ v3: how torch adopts device memory
+            __cuda_array_interface__ = {'shape': (numel,), 'typestr': typestr,
+                                        'data': (ptr, False), 'version': 3}
+        t = torch.as_tensor(_Dev(), device='cuda')
+        assert t.data_ptr() == ptr
+        return t
+
+    def free_shared(self, ptr):
+        """collective MPIX_Comm_free_shared (an address from alloc_shared or a
+        shared_tensor's data_ptr())"""
+        redop.check(lib().MPIX_Comm_free_shared(self.h, ptr), 'MPIX_Comm_free_shared')
 
     def set_step_timing(self, enable=True):
         redop.check(lib().MPIX_Comm_set_step_timing(self.h, 1 if enable else 0),

@@ -106,9 +106,14 @@ struct MPIX_Comm_s {
     char *win = nullptr;               // pull window (header + data), see ensure_windows
     size_t win_bytes = 0;
     std::vector<char *> win_old;       // outgrown / rejected windows, freed with the comm
-    std::vector<const char *> peer_win;    // peers' windows, mapped and verified
-    std::vector<void *> peer_map;
+    std::vector<void *> peer_map;      // peers' pull windows, mapped and verified
     bool win_broken = false;           // pulls given up on this communicator
+    struct Shared {                    // MPIX_Comm_alloc_shared windows
+        char *base;                    // header + bytes
+        size_t bytes;
+        std::vector<void *> maps;      // peers' copies, mapped and verified
+    };
+    std::vector<Shared> shared;
     bool timing = false;               // MPIX_Comm_set_step_timing
     std::vector<std::pair<std::string, hipEvent_t>> marks;
     bool host() const { return kind == K_LOCAL_HOST || (kind == K_CUSTOM && device < 0); }
@@ -985,29 +990,24 @@ struct LocalRec {   // K_LOCAL_DEV: the raw address
     uint64_t raw;
 };
 
-void close_peer_windows(MPIX_Comm c)
+void close_maps(std::vector<void *> *maps)
 {
-    for (void *m : c->peer_map)
+    for (void *m : *maps)
         if (m)
             (void) hipIpcCloseMemHandle(m);
-    c->peer_map.assign(c->size, nullptr);
-    c->peer_win.assign(c->size, nullptr);
+    maps->clear();
 }
 
-// Every rank's window holds at least `need` data bytes and every peer's is
-// mapped and verified (*ok), or the pulls are off for this communicator
-// (*ok = false on every rank).  Collective: every rank calls it with the same
-// `need` (the message size), so all ranks grow at the same calls.
-int ensure_windows(MPIX_Comm c, size_t need, hipStream_t s, bool *ok)
+// Collective: a new device allocation of kWinHdr + `bytes` on every rank,
+// exported, mapped by every peer (maps[q]) and verified through the mapping
+// by the nonce in its header, with every rank agreeing on the outcome.  On a
+// failed verification all ranks retry (3 attempts; the rejected allocations
+// stay allocated, in win_old, so their identity is never reused).  *w = NULL
+// on every rank when no attempt succeeded.
+int verified_window(MPIX_Comm c, size_t bytes, hipStream_t s, char **w_out,
+                    std::vector<void *> *maps)
 {
-    *ok = false;
-    if (c->win_broken)
-        return MPIX_REDOP_SUCCESS;
-    if (c->win && c->win_bytes >= need) {
-        *ok = true;
-        return MPIX_REDOP_SUCCESS;
-    }
-    const size_t bytes = std::max(need, c->win_bytes * 2 > need ? c->win_bytes * 2 : need);
+    *w_out = nullptr;
     std::random_device rd;
     for (int attempt = 0; attempt < 3; ++attempt) {
         void *w = nullptr;
@@ -1032,15 +1032,14 @@ int ensure_windows(MPIX_Comm c, size_t need, hipStream_t s, bool *ok)
         (void) hipGetLastError();
         std::vector<char> all;
         TRY(allgather_records(c, &me, sizeof me, &all, s));
-        HTRY(hipStreamSynchronize(s));      // nothing in flight reads the old mappings
-        close_peer_windows(c);
+        maps->assign(c->size, nullptr);
         int good = me.valid;
         for (int q = 0; q < c->size && good; ++q) {
             if (q == c->rank)
                 continue;
             WinRec r;
             memcpy(&r, all.data() + kRec * (size_t) q, sizeof r);
-            if (!r.valid || r.bytes < need) {
+            if (!r.valid || r.bytes < bytes) {
                 good = 0;
                 break;
             }
@@ -1053,8 +1052,7 @@ int ensure_windows(MPIX_Comm c, size_t need, hipStream_t s, bool *ok)
                 good = 0;
                 break;
             }
-            c->peer_map[q] = m;
-            c->peer_win[q] = static_cast<const char *>(m);
+            (*maps)[q] = m;
             if (hipMemcpy(seen, m, sizeof seen, hipMemcpyDeviceToHost) != hipSuccess ||
                 seen[0] != r.nonce[0] || seen[1] != r.nonce[1]) {
                 (void) hipGetLastError();
@@ -1074,23 +1072,96 @@ int ensure_windows(MPIX_Comm c, size_t need, hipStream_t s, bool *ok)
             fprintf(stderr, "[mpix_coll rank %d] pull window %zu B attempt %d: mine %d, all %d\n",
                     c->rank, bytes, attempt, good, (int) all_good);
         if (all_good) {
-            if (c->win)
-                c->win_old.push_back(c->win);
-            c->win = static_cast<char *>(w);
-            c->win_bytes = bytes;
-            *ok = true;
+            *w_out = static_cast<char *>(w);
             return MPIX_REDOP_SUCCESS;
         }
-        close_peer_windows(c);
+        close_maps(maps);
         if (w)
             c->win_old.push_back(static_cast<char *>(w));     // never reused, see above
-        if (c->win) {       // the old windows stay mapped by nobody: re-map them next time
-            c->win_old.push_back(c->win);
-            c->win = nullptr;
-            c->win_bytes = 0;
+    }
+    return MPIX_REDOP_SUCCESS;
+}
+
+// Every rank's pull window holds at least `need` data bytes and every peer's
+// is mapped and verified (*ok), or the pulls are off for this communicator
+// (*ok = false on every rank).  Collective: every rank calls it with the same
+// `need` (the message size), so all ranks grow at the same calls.
+int ensure_windows(MPIX_Comm c, size_t need, hipStream_t s, bool *ok)
+{
+    *ok = false;
+    if (c->win_broken)
+        return MPIX_REDOP_SUCCESS;
+    if (c->win && c->win_bytes >= need) {
+        *ok = true;
+        return MPIX_REDOP_SUCCESS;
+    }
+    HTRY(hipStreamSynchronize(s));      // nothing in flight reads the old mappings
+    close_maps(&c->peer_map);
+    if (c->win) {                       // outgrown: kept allocated, see above
+        c->win_old.push_back(c->win);
+        c->win = nullptr;
+        c->win_bytes = 0;
+    }
+    const size_t bytes = std::max(need, 2 * c->win_bytes);
+    char *w;
+    TRY(verified_window(c, bytes, s, &w, &c->peer_map));
+    if (!w) {
+        c->win_broken = true;
+        return MPIX_REDOP_SUCCESS;
+    }
+    c->win = w;
+    c->win_bytes = bytes;
+    *ok = true;
+    return MPIX_REDOP_SUCCESS;
+}
+
+// The shared window (MPIX_Comm_alloc_shared) holding [p, p + bytes), and p's
+// offset in it; -1 if none.
+int64_t shared_of(MPIX_Comm c, const void *p, size_t bytes, int64_t *off)
+{
+    const char *x = static_cast<const char *>(p);
+    for (size_t i = 0; i < c->shared.size(); ++i) {
+        const char *b = c->shared[i].base + kWinHdr;
+        if (x >= b && x + bytes <= b + c->shared[i].bytes) {
+            *off = x - b;
+            return (int64_t) i;
         }
     }
-    c->win_broken = true;
+    *off = 0;
+    return -1;
+}
+
+// Do all ranks hold `n` buffers (ps[i], bytes[i]) in the same shared windows
+// at the same offsets?  Then a pull reads the peers' copies in place (no copy
+// into the pull window).  Collective once the communicator has shared windows:
+// the ranks compare (window, offset) records, after their streams have
+// finished writing the buffers -- the "inputs ready" point of the pull.
+int shared_direct(MPIX_Comm c, int n, const void *const *ps, const size_t *bytes, hipStream_t s,
+                  bool *direct, std::vector<int64_t> *where)
+{
+    *direct = false;
+    if (c->shared.empty() || c->kind == K_LOCAL_DEV)
+        return MPIX_REDOP_SUCCESS;
+    int64_t me[4] = {-1, 0, -1, 0};
+    for (int i = 0; i < n && i < 2; ++i)
+        me[2 * i] = shared_of(c, ps[i], bytes[i], &me[2 * i + 1]);
+    HTRY(hipStreamSynchronize(s));
+    std::vector<char> all;
+    TRY(allgather_records(c, me, sizeof me, &all, s));
+    bool same = true;
+    for (int q = 0; q < c->size && same; ++q) {
+        int64_t r[4];
+        memcpy(r, all.data() + kRec * (size_t) q, sizeof r);
+        for (int i = 0; i < 2 * n; ++i)
+            same = same && r[i] == me[i];
+    }
+    for (int i = 0; i < n; ++i)
+        same = same && me[2 * i] >= 0;
+    *direct = same;
+    where->assign(me, me + 2 * n);
+    if (coll_trace())
+        fprintf(stderr, "[mpix_coll rank %d] shared-window pull: %s\n", c->rank,
+                same ? "direct" : "copy");
     return MPIX_REDOP_SUCCESS;
 }
 
@@ -1148,19 +1219,31 @@ int rs_pull(const char *sb, char *rb, const std::vector<size_t> &cnts, MPIX_Data
             bases[q] = reinterpret_cast<const char *>(r.raw);
         }
     } else {
-        bool ok;
-        TRY(ensure_windows(c, total * ext, s, &ok));
-        if (!ok)
-            return fallback();
-        // the blocks the peers read (this rank's own block is read from sb)
-        char *wd = c->win + kWinHdr;
-        TRY(copy(c, wd, sb, disps[rank] * ext, s));
-        TRY(copy(c, wd + (disps[rank] + cnts[rank]) * ext, sb + (disps[rank] + cnts[rank]) * ext,
-                 (total - disps[rank] - cnts[rank]) * ext, s));
-        TRY(barrier(c, s));             // every window filled
-        for (int q = 0; q < size; ++q)
-            if (q != rank)
-                bases[q] = c->peer_win[q] + kWinHdr;
+        bool direct;
+        std::vector<int64_t> where;
+        const void *ps[1] = {sb};
+        const size_t nbs[1] = {total * ext};
+        TRY(shared_direct(c, 1, ps, nbs, s, &direct, &where));
+        if (direct) {                   // every rank's input in a shared window: read in place
+            for (int q = 0; q < size; ++q)
+                if (q != rank)
+                    bases[q] = static_cast<const char *>(c->shared[where[0]].maps[q]) + kWinHdr +
+                               where[1];
+        } else {
+            bool ok;
+            TRY(ensure_windows(c, total * ext, s, &ok));
+            if (!ok)
+                return fallback();
+            // the blocks the peers read (this rank's own block is read from sb)
+            char *wd = c->win + kWinHdr;
+            TRY(copy(c, wd, sb, disps[rank] * ext, s));
+            TRY(copy(c, wd + (disps[rank] + cnts[rank]) * ext, sb + (disps[rank] + cnts[rank]) * ext,
+                     (total - disps[rank] - cnts[rank]) * ext, s));
+            TRY(barrier(c, s));         // every window filled
+            for (int q = 0; q < size; ++q)
+                if (q != rank)
+                    bases[q] = static_cast<const char *>(c->peer_map[q]) + kWinHdr;
+        }
     }
     if (!in_place && !tree)
         TRY(copy(c, rb, sb + disps[rank] * ext, blk, s));                   // :58-64
@@ -1424,20 +1507,36 @@ int allreduce_pull(const char *sendbuf, char *rb, size_t count, MPIX_Datatype dt
             in_base[q] = reinterpret_cast<const char *>(r.in.raw);
             out_base[q] = reinterpret_cast<const char *>(r.out.raw);
         }
-    } else {                            // processes: the pull windows
-        bool ok;
-        TRY(ensure_windows(c, nb, s, &ok));
-        if (!ok)
-            return fallback();
-        char *wd = c->win + kWinHdr;
-        TRY(copy(c, wd, in, disps[mine] * ext, s));     // every block but this rank's own
-        TRY(copy(c, wd + (disps[mine] + cnts[mine]) * ext, in + (disps[mine] + cnts[mine]) * ext,
-                 nb - (disps[mine] + cnts[mine]) * ext, s));
-        TRY(barrier(c, s));             // every window filled
-        for (int q = 0; q < size; ++q)
-            if (q != rank)
-                in_base[q] = out_base[q] = c->peer_win[q] + kWinHdr;
-        out = wd + disps[mine] * ext;   // peers read it from the window
+    } else {                            // processes
+        bool direct;
+        std::vector<int64_t> where;
+        const void *ps[2] = {in, rb};
+        const size_t nbs[2] = {nb, nb};
+        TRY(shared_direct(c, 2, ps, nbs, s, &direct, &where));
+        if (direct) {                   // input and result in shared windows: in place
+            for (int q = 0; q < size; ++q) {
+                if (q == rank)
+                    continue;
+                in_base[q] = static_cast<const char *>(c->shared[where[0]].maps[q]) + kWinHdr +
+                             where[1];
+                out_base[q] = static_cast<const char *>(c->shared[where[2]].maps[q]) + kWinHdr +
+                              where[3];
+            }
+        } else {                        // the pull windows
+            bool ok;
+            TRY(ensure_windows(c, nb, s, &ok));
+            if (!ok)
+                return fallback();
+            char *wd = c->win + kWinHdr;
+            TRY(copy(c, wd, in, disps[mine] * ext, s));     // every block but this rank's own
+            TRY(copy(c, wd + (disps[mine] + cnts[mine]) * ext, in + (disps[mine] + cnts[mine]) * ext,
+                     nb - (disps[mine] + cnts[mine]) * ext, s));
+            TRY(barrier(c, s));         // every window filled
+            for (int q = 0; q < size; ++q)
+                if (q != rank)
+                    in_base[q] = out_base[q] = static_cast<const char *>(c->peer_map[q]) + kWinHdr;
+            out = wd + disps[mine] * ext;   // peers read it from the window
+        }
     }
     TRY(mark(c, "publish", s));
     std::vector<const void *> ins(size);
@@ -2060,6 +2159,49 @@ int MPIX_Comm_barrier(MPIX_Comm comm)
     return finish(comm, barrier(comm, s), s, true);
 }
 
+int MPIX_Comm_alloc_shared(MPIX_Comm comm, size_t bytes, void **ptr)
+{
+    if (!comm || !ptr)
+        return MPIX_REDOP_ERR_ARG;
+    *ptr = nullptr;
+    if (comm->host())
+        return MPIX_REDOP_ERR_ARG;
+    TRY(set_device(comm));
+    hipStream_t s = stream_of(comm->stream ? comm->stream : comm->own_stream);
+    MPIX_Comm_s::Shared sh{nullptr, bytes, {}};
+    if (comm->kind == K_LOCAL_DEV || comm->size == 1) {
+        // one address space: plain device memory (the pulls read peers directly)
+        void *p = nullptr;
+        HTRY(hipMalloc(&p, kWinHdr + bytes));
+        sh.base = static_cast<char *>(p);
+    } else {
+        TRY(verified_window(comm, bytes, s, &sh.base, &sh.maps));
+        if (!sh.base)
+            return MPIX_REDOP_ERR_OTHER;    // every rank: no verified mapping
+    }
+    comm->shared.push_back(std::move(sh));
+    *ptr = comm->shared.back().base + kWinHdr;
+    return MPIX_REDOP_SUCCESS;
+}
+
+int MPIX_Comm_free_shared(MPIX_Comm comm, void *ptr)
+{
+    if (!comm)
+        return MPIX_REDOP_ERR_ARG;
+    for (size_t i = 0; i < comm->shared.size(); ++i) {
+        if (comm->shared[i].base + kWinHdr != ptr)
+            continue;
+        TRY(MPIX_Comm_barrier(comm));   // every peer done with every copy
+        close_maps(&comm->shared[i].maps);
+        // kept allocated until MPIX_Comm_free: a freed allocation's identity
+        // must not come back (see verified_window)
+        comm->win_old.push_back(comm->shared[i].base);
+        comm->shared.erase(comm->shared.begin() + (long) i);
+        return MPIX_REDOP_SUCCESS;
+    }
+    return MPIX_REDOP_ERR_BUFFER;
+}
+
 int MPIX_Comm_set_step_timing(MPIX_Comm comm, int enable)
 {
     if (!comm)
@@ -2144,13 +2286,15 @@ int MPIX_Comm_free(MPIX_Comm comm)
             (void) hipHostFree(comm->stage);
         if (comm->tok)
             (void) hipFree(comm->tok);
-        for (void *m : comm->peer_map)
-            if (m)
-                (void) hipIpcCloseMemHandle(m);
+        close_maps(&comm->peer_map);
         if (comm->win)
             (void) hipFree(comm->win);
         for (char *w : comm->win_old)
             (void) hipFree(w);
+        for (auto &sh : comm->shared) {
+            close_maps(&sh.maps);
+            (void) hipFree(sh.base);
+        }
         for (auto &m : comm->marks)
             (void) hipEventDestroy(m.second);
     } else {

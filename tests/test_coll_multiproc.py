@@ -188,6 +188,62 @@ def test_staged_pulls_with_buffer_churn(tmp_path, world):
         assert open(tmp_path / ('churn%d.txt' % r)).read() == '', r
 
 
+def _shared_worker(rank, world, port, outdir):
+    import torch.distributed as dist
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    os.environ['MPIX_COLL_TRACE'] = '1'
+    torch.cuda.set_device(0)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    trace = open(os.path.join(outdir, 'trace%d.txt' % rank), 'w')
+    os.dup2(trace.fileno(), 2)          # the library's trace lines land in the file
+    from mpich_amd import coll
+    c = coll.comm_for(None, True)
+    n = 40009
+    send, dt, op = _inputs(rank, world, n, 'float')
+    sh = c.shared_tensor(world * n, torch.float32)      # symmetric memory
+    out_sh = c.shared_tensor(world * n, torch.float32)
+    sh.copy_(torch.from_numpy(send))
+    torch.cuda.synchronize()
+    res = {}
+    for algo in ('pull', 'recursive_halving_pull'):
+        r = torch.empty(n, dtype=torch.float32, device='cuda')
+        coll.reduce_scatter_block(sh, r, n, dt, op, algorithm=algo)
+        res[algo] = r.cpu().numpy()
+    coll.allreduce(sh, out_sh, world * n, dt, op, algorithm='pull')      # both shared
+    res['allreduce_pull'] = out_sh.cpu().numpy()
+    torch.cuda.synchronize()
+    for name, v in res.items():
+        np.save(os.path.join(outdir, 'sh_%s_recv%d.npy' % (name, rank)), v)
+    np.save(os.path.join(outdir, 'sh_send%d.npy' % rank), send)
+    c.free_shared(sh.data_ptr())
+    dist.barrier()
+    coll.free_comms()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world', [2, 4])
+def test_staged_pulls_on_shared_memory(oracle, tmp_path, world):
+    """MPIX_Comm_alloc_shared: with every rank's buffers in symmetric shared
+    memory the pulls read the peers' copies in place (the trace says
+    'direct'), bit-identical to the oracle's schedules"""
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    mp.spawn(_shared_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    n = 40009
+    raw = [np.load(tmp_path / ('sh_send%d.npy' % r)).view(np.uint8) for r in range(world)]
+    exp = {'pull': oracle.rsb_pairwise(raw, n, MPI_FLOAT, MPI_SUM),
+           'recursive_halving_pull': oracle.rsb_recursive_halving(raw, n, MPI_FLOAT, MPI_SUM),
+           'allreduce_pull': oracle.allreduce_rabenseifner(raw, world * n, MPI_FLOAT, MPI_SUM)}
+    for name, e in exp.items():
+        for r in range(world):
+            got = np.load(tmp_path / ('sh_%s_recv%d.npy' % (name, r)))
+            assert got.tobytes() == e[r].tobytes(), (name, r)
+    for r in range(world):
+        t = open(tmp_path / ('trace%d.txt' % r)).read()
+        assert t.count('shared-window pull: direct') == 3, t[-2000:]
+
+
 def _fault_worker(rank, world, port, outdir):
     os.environ['MPIX_COLL_WINDOW_FAULT'] = '1'      # rank 1's window fails verification
     _worker(rank, world, port, outdir, 'gloo',
