@@ -471,6 +471,46 @@ def test_barrier_and_custom_memory_kinds(oracle, P):
                                      ctypes.byref(h)) == 12     # MPI_ERR_ARG
 
 
+def test_shared_memory_argument_errors(oracle):
+    """MPIX_Comm_alloc_shared is for device communicators (a host one gets
+    MPI_ERR_ARG and no memory); MPIX_Comm_free_shared of an address it did not
+    hand out is MPI_ERR_BUFFER"""
+    from mpich_amd import ccl
+    L = ccl.lib()
+    comms = host_comms(1, oracle)
+    p = ctypes.c_void_p(1)
+    assert L.MPIX_Comm_alloc_shared(comms[0].h, 4096, ctypes.byref(p)) == 12
+    assert not p.value
+    assert L.MPIX_Comm_alloc_shared(comms[0].h, 4096, None) == 12
+    assert L.MPIX_Comm_free_shared(comms[0].h, 4096) == 1
+    free_all(comms)
+
+
+@pytest.mark.gpu
+def test_shared_memory_local_communicator(oracle):
+    """threads of one process: MPIX_Comm_alloc_shared is plain device memory
+    (the pulls read peers' buffers directly anyway); a pull over it matches
+    the oracle, and free_shared / free release it"""
+    import torch
+    from mpich_amd import ccl
+    P, n = 4, 4099
+    comms = _dev_comms(P)
+    sh = [c.shared_tensor(P * n, torch.float32) for c in comms]
+    sends = float_sends(P, P * n, 0x5EED0900)
+    for t, x in zip(sh, sends):
+        t.copy_(torch.from_numpy(x))
+    out = [torch.zeros(n, dtype=torch.float32, device='cuda') for _ in range(P)]
+    torch.cuda.synchronize()
+    rcs = run_ranks(comms, lambda r, c: ccl.reduce_scatter_block(
+        sh[r], out[r], n, MPI_FLOAT, MPI_SUM, c, 'recursive_halving_pull'))
+    assert rcs == [0] * P
+    exp = oracle.rsb_recursive_halving([x.view(np.uint8) for x in sends], n, MPI_FLOAT, MPI_SUM)
+    for r in range(P):
+        assert out[r].cpu().numpy().tobytes() == exp[r].tobytes(), r
+    run_ranks(comms, lambda r, c: c.free_shared(sh[r].data_ptr()))
+    free_all(comms)
+
+
 # ------------------------------------------------------------------ GPU
 def _dev_comms(P):
     from mpich_amd import ccl
