@@ -224,16 +224,20 @@ int MPIX_Reduce_local_multi_async(const void *const *inbufs, int ninputs, void *
                                   MPIX_Aint count, MPIX_Datatype datatype, MPIX_Op op,
                                   void *stream);
 
-/* Tree form: outbuf = the pairwise tree fold of ninputs = 2^L operands
+/* Tree form: outbuf = the pairwise tree fold of ninputs = 2^L slots
  * (2 <= ninputs <= 16), level by level m = 1, 2, 4, ...:
  *   slot s (bit m of s clear) = slot s OP slot s+m   (slot s is inout)
- * and outbuf = slot 0.  Holding the block of rank r ^ bitrev(s) in slot s,
+ * and outbuf = slot 0.  inbufs[0] must be given; a NULL slot s > 0 is absent:
+ * at its level the partner passes through unchanged (the first level of the
+ * reference's fold of a non-power-of-two world, where only the paired ranks
+ * combine).  Holding the block of rank r ^ bitrev(s) in slot s,
  * this is the association recursive halving gives rank r's block
  * (reduce_scatter_block_intra_recursive_halving.c:164-229, P a power of
  * two), so a schedule that can read every peer's block computes the
- * reference's bits in one pass.  outbuf may be inbufs[0] (in place); no other
- * overlap.  REPLACE yields the last slot, NO_OP the first; MPIX_EQUAL is
- * refused (MPI_ERR_OP).  Device-accessible buffers; stream-ordered. */
+ * reference's bits in one pass.  outbuf may be one of the slots exactly (in
+ * place); no partial overlap.  REPLACE yields the last present slot, NO_OP
+ * the first; MPIX_EQUAL is refused (MPI_ERR_OP).  Device-accessible buffers;
+ * stream-ordered. */
 int MPIX_Reduce_local_tree_async(const void *const *inbufs, int ninputs, void *outbuf,
                                  MPIX_Aint count, MPIX_Datatype datatype, MPIX_Op op,
                                  void *stream);

@@ -1201,7 +1201,7 @@ int rs_pull(const char *sb, char *rb, const std::vector<size_t> &cnts, MPIX_Data
                                     : rs_pairwise(sb, rb, cnts, dt, op, c, w, s, ext, true),
                                s);
     };
-    if (c->host() || c->combine || (tree && (size & (size - 1))) || size > 16)
+    if (c->host() || c->combine || size > 16)
         return fallback();
     const size_t blk = cnts[rank] * ext;
     const bool in_place = sb == rb;
@@ -1249,15 +1249,31 @@ int rs_pull(const char *sb, char *rb, const std::vector<size_t> &cnts, MPIX_Data
         TRY(copy(c, rb, sb + disps[rank] * ext, blk, s));                   // :58-64
     std::vector<const void *> ins;
     if (tree) {
-        for (int q = 0; q < size; ++q)
-            ins.push_back(bases[rank ^ bitrev(q, size)] + disps[rank] * ext);
+        // slot s: rank ^ bitrev(s) (P a power of two); otherwise the
+        // reference's fold (:110-137) is the first level -- slot pair (2t, 2t+1)
+        // is new rank v = nr ^ bitrev(t): inout the odd rank 2v + 1, in the even
+        // 2v, or new rank v's own input alone -- and its block holds this rank's
+        const int pof2 = pof2_of(size), rem = size - pof2;
+        const int nr = rank < 2 * rem ? rank / 2 : rank - rem;
+        const int k = rem ? 2 * pof2 : pof2;
+        for (int sl = 0; sl < k; ++sl) {
+            int src;
+            if (!rem) {
+                src = rank ^ bitrev(sl, size);
+            } else {
+                const int v = nr ^ bitrev(sl / 2, pof2), j = sl % 2;
+                src = v < rem ? (j ? 2 * v : 2 * v + 1) : (j ? -1 : v + rem);
+            }
+            ins.push_back(src < 0 ? nullptr : bases[src] + disps[rank] * ext);
+        }
     } else {
         for (int i = 1; i < size; ++i)
             ins.push_back(bases[(rank - i + size) % size] + disps[rank] * ext);
     }
     TRY(mark(c, "publish", s));
     if (cnts[rank] && tree)
-        TRY(MPIX_Reduce_local_tree_async(ins.data(), size, acc, (MPIX_Aint) cnts[rank], dt, op, s));
+        TRY(MPIX_Reduce_local_tree_async(ins.data(), (int) ins.size(), acc, (MPIX_Aint) cnts[rank],
+                                         dt, op, s));
     else if (cnts[rank])
         TRY(combine_multi(c, ins, acc, (MPIX_Aint) cnts[rank], dt, op, s));
     TRY(mark(c, "pull+combine", s));
@@ -1307,8 +1323,8 @@ size_t rs_workspace(size_t total, size_t mine, size_t ext, int size, int algo)
             return (size - 1) * round256(mine * ext);
         case MPIX_RSB_PAIRWISE_SEQUENTIAL:
             return round256(mine * ext);
-        case MPIX_RSB_RECURSIVE_HALVING_PULL:       // other P run RECURSIVE_HALVING
-            return ((size & (size - 1)) || size > 16) ? 2 * round256(total * ext) : 0;
+        case MPIX_RSB_RECURSIVE_HALVING_PULL:       // P > 16 runs RECURSIVE_HALVING
+            return size > 16 ? 2 * round256(total * ext) : 0;
         default:
             return 0;
     }
@@ -1479,19 +1495,25 @@ int allreduce_pull(const char *sendbuf, char *rb, size_t count, MPIX_Datatype dt
         return release_scratch(c, tmp, allreduce_rsag(rb, count, dt, op, c, tmp, s, ext, true,
                                                       false), s);
     };
-    if (c->host() || c->combine || (size & (size - 1)) || size > 16)
+    if (c->host() || c->combine || size > 16)
         return fallback();
     const char *in = sendbuf ? sendbuf : rb;
-    std::vector<size_t> cnts(size), disps(size, 0);
-    for (int i = 0; i < size; ++i)
-        cnts[i] = count / size + ((size_t) i < count % size ? 1 : 0);
-    for (int i = 1; i < size; ++i)
+    // the reference's layout (:85-127): P - pof2 even/odd pairs fold first (the
+    // odd rank keeps going as new rank i), then pof2 new ranks share pof2
+    // blocks; new rank v owns block bitrev(v)
+    const int pof2 = pof2_of(size), rem = size - pof2;
+    std::vector<size_t> cnts(pof2), disps(pof2, 0);
+    for (int i = 0; i < pof2; ++i)
+        cnts[i] = count / pof2 + ((size_t) i < count % pof2 ? 1 : 0);
+    for (int i = 1; i < pof2; ++i)
         disps[i] = disps[i - 1] + cnts[i - 1];
-    const int mine = bitrev(rank, size);
+    auto real = [rem](int v) { return v < rem ? 2 * v + 1 : v + rem; };
+    const int nr = rank < 2 * rem ? (rank % 2 ? rank / 2 : -1) : rank - rem;
+    const int mine = nr >= 0 ? bitrev(nr, pof2) : -1;     // -1: a folded-away even rank
     // in_base[q]: where rank q's input is read; out_base[q]: where its
     // reduced block is read in the allgather; out: where this rank's goes
     std::vector<const char *> in_base(size, in), out_base(size, rb);
-    char *out = rb + disps[mine] * ext;
+    char *out = mine >= 0 ? rb + disps[mine] * ext : nullptr;
     TRY(mark(c, "start", s));
     if (c->kind == K_LOCAL_DEV) {     // threads of one process: the user buffers
         struct Recs {
@@ -1528,29 +1550,49 @@ int allreduce_pull(const char *sendbuf, char *rb, size_t count, MPIX_Datatype dt
             if (!ok)
                 return fallback();
             char *wd = c->win + kWinHdr;
-            TRY(copy(c, wd, in, disps[mine] * ext, s));     // every block but this rank's own
-            TRY(copy(c, wd + (disps[mine] + cnts[mine]) * ext, in + (disps[mine] + cnts[mine]) * ext,
-                     nb - (disps[mine] + cnts[mine]) * ext, s));
+            if (mine >= 0) {            // every block but this rank's own (only it reads that)
+                TRY(copy(c, wd, in, disps[mine] * ext, s));
+                TRY(copy(c, wd + (disps[mine] + cnts[mine]) * ext,
+                         in + (disps[mine] + cnts[mine]) * ext,
+                         nb - (disps[mine] + cnts[mine]) * ext, s));
+                out = wd + disps[mine] * ext;   // peers read it from the window
+            } else {
+                TRY(copy(c, wd, in, nb, s));
+            }
             TRY(barrier(c, s));         // every window filled
             for (int q = 0; q < size; ++q)
                 if (q != rank)
                     in_base[q] = out_base[q] = static_cast<const char *>(c->peer_map[q]) + kWinHdr;
-            out = wd + disps[mine] * ext;   // peers read it from the window
         }
     }
     TRY(mark(c, "publish", s));
-    std::vector<const void *> ins(size);
-    for (int q = 0; q < size; ++q)
-        ins[q] = in_base[rank ^ q] + disps[mine] * ext;
-    if (cnts[mine])
-        TRY(MPIX_Reduce_local_tree_async(ins.data(), size, out, (MPIX_Aint) cnts[mine], dt, op, s));
+    if (mine >= 0 && cnts[mine]) {
+        // slot s of the tree: without a fold, rank nr ^ s (masks 1, 2, ...:
+        // :138-189); with one, slot pair (2t, 2t + 1) is new rank v = nr ^ t's
+        // fold -- inout the odd rank 2v + 1, in the even 2v (:94-108) -- or
+        // new rank v's own input alone
+        const int k = rem ? 2 * pof2 : pof2;
+        std::vector<const void *> ins(k, nullptr);
+        for (int sl = 0; sl < k; ++sl) {
+            int src;
+            if (!rem) {
+                src = nr ^ sl;
+            } else {
+                const int v = nr ^ (sl / 2), j = sl % 2;
+                src = v < rem ? (j ? 2 * v : 2 * v + 1) : (j ? -1 : v + rem);
+            }
+            if (src >= 0)
+                ins[sl] = in_base[src] + disps[mine] * ext;
+        }
+        TRY(MPIX_Reduce_local_tree_async(ins.data(), k, out, (MPIX_Aint) cnts[mine], dt, op, s));
+    }
     TRY(mark(c, "reduce-scatter pull", s));
     TRY(barrier(c, s));                 // every block final (and every input read)
     std::vector<const void *> srcs;
     std::vector<void *> dsts;
     std::vector<MPIX_Aint> bytes;
-    for (int q = 0; q < size; ++q) {
-        const int b = bitrev(q, size);
+    for (int v = 0; v < pof2; ++v) {
+        const int q = real(v), b = bitrev(v, pof2);
         const char *src = q == rank ? out : out_base[q] + disps[b] * ext;
         if (src == rb + disps[b] * ext)
             continue;                   // this rank's block already in place
@@ -1563,7 +1605,7 @@ int allreduce_pull(const char *sendbuf, char *rb, size_t count, MPIX_Datatype dt
         TRY(MPIX_Copy_multi_async(srcs.data() + lo, dsts.data() + lo, bytes.data() + lo, n, s));
     }
     TRY(mark(c, "allgather pull", s));
-    TRY(barrier(c, s));                 // peers done reading this rank's buffers
+    TRY(barrier(c, s));                 // peers done reading this rank's window / buffers
     return MPIX_REDOP_SUCCESS;
 }
 
@@ -1927,7 +1969,7 @@ int rs_entry(const void *sendbuf, void *recvbuf, const std::vector<size_t> &cnts
     int algo = rs_choose(algorithm, total * ext);
     if (algo == MPIX_RSB_RECURSIVE_HALVING_MULTIPATH && !multipath_shape(cnts, c->size))
         algo = MPIX_RSB_RECURSIVE_HALVING;
-    if (algo == MPIX_RSB_RECURSIVE_HALVING_PULL && ((c->size & (c->size - 1)) || c->size > 16))
+    if (algo == MPIX_RSB_RECURSIVE_HALVING_PULL && c->size > 16)
         algo = MPIX_RSB_RECURSIVE_HALVING;
     if (c->size == 1)
         return finish(c, sendbuf ? copy(c, rb, sb, cnts[0] * ext, s) : MPIX_REDOP_SUCCESS, s,

@@ -1369,14 +1369,18 @@ int MPIX_Reduce_local_multi_async(const void *const *inbufs, int ninputs, void *
 int MPIX_Reduce_local_tree_async(const void *const *inbufs, int ninputs, void *outbuf,
                                  MPIX_Aint count, MPIX_Datatype datatype, MPIX_Op op, void *stream)
 {
-    if (ninputs < 2 || ninputs > mpix::kMaxMultiInputs || (ninputs & (ninputs - 1)) || !inbufs)
+    if (ninputs < 2 || ninputs > mpix::kMaxMultiInputs || (ninputs & (ninputs - 1)) || !inbufs ||
+        !inbufs[0])
         return set_err(MPIX_REDOP_ERR_ARG);
     uint32_t it;
     uint64_t ext;
-    // outbuf may be inbufs[0] itself (each element is read before it is
-    // written, by the same lane); any other overlap is refused
+    // outbuf may be one of the slots itself (each lane reads all its slots'
+    // elements before it writes that element); any partial overlap is
+    // refused.  Slots 1..k-1 may be NULL: absent (the partner passes through).
     for (int q = 0; q < ninputs; ++q) {
-        const bool same = q == 0 && inbufs[0] == (const void *) outbuf;
+        if (!inbufs[q])
+            continue;
+        const bool same = inbufs[q] == (const void *) outbuf;
         int rc = validate(same ? (const void *) ((const char *) outbuf + 1) : inbufs[q], outbuf,
                           same ? 0 : count, (uint32_t) datatype, (uint32_t) op, &it, &ext);
         if (rc == MPIX_REDOP_SUCCESS && same && count > 0 &&
@@ -1397,11 +1401,16 @@ int MPIX_Reduce_local_tree_async(const void *const *inbufs, int ninputs, void *o
     const void *pout;
     if (!device_accessible(outbuf, &pout))
         return set_err(MPIX_REDOP_ERR_BUFFER);
-    for (int q = 0; q < ninputs; ++q)
-        if (!device_accessible(inbufs[q], &dins[q]))
+    int last = 0;
+    for (int q = 0; q < ninputs; ++q) {
+        dins[q] = nullptr;
+        if (inbufs[q] && !device_accessible(inbufs[q], &dins[q]))
             return set_err(MPIX_REDOP_ERR_BUFFER);
-    if (opi == 13 || opi == 14) {   // REPLACE folds to the last slot, NO_OP to the first
-        const void *src = dins[opi == 13 ? ninputs - 1 : 0];
+        if (inbufs[q])
+            last = q;
+    }
+    if (opi == 13 || opi == 14) {   // REPLACE folds to the last present slot, NO_OP to the first
+        const void *src = dins[opi == 13 ? last : 0];
         if (src == pout)
             return set_err(MPIX_REDOP_SUCCESS);
         return set_err(replace_rows((void *) pout, ext, src, ext, (uint64_t) count, it, ext,

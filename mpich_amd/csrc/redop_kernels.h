@@ -212,43 +212,60 @@ k_elem_multi(MultiIn<typename C::unit> ins, int k, typename C::unit *__restrict_
     }
 }
 
-// Tree combine: k = 2^L operands in slots 0..k-1 folded pairwise by levels,
-// level m = 1, 2, 4, ...: slot s (bit m clear) = OP(inout = slot s, in = slot
-// s + m), result = slot 0, written to `out` (which may be slot 0's buffer).
-// With the slots holding the peers of rank r in the order
-// r ^ bitrev(s) this is the recursive-halving association of rank r's block
-// (…recursive_halving.c:164-229: each step the partner's partial is `in`, the
-// own partial `inout`), computed in one pass that reads the k blocks
-// (over xGMI for the peers') and writes one.  Unused slots (s >= k) are
-// compile-time registers whose loads and combines are skipped by uniform
-// branches, so one instantiation serves every k.
+// Tree combine: k = 2^L slots folded pairwise by levels, level m = 1, 2, 4,
+// ...: slot s (bit m clear) = OP(inout = slot s, in = slot s + m), result =
+// slot 0, written to `out` (which may be slot 0's buffer).  With the slots
+// holding the peers of rank r in the order r ^ bitrev(s) this is the
+// recursive-halving association of rank r's block (…recursive_halving.c:
+// 164-229: each step the partner's partial is `in`, the own partial
+// `inout`), computed in one pass that reads the k blocks (over xGMI for the
+// peers') and writes one.  `pres` marks the slots that hold an operand: an
+// absent slot's partner passes through unchanged (the reference's fold of a
+// non-power-of-two world, where half of the first level has no partner).
+// Unused slots (s >= k) are compile-time registers whose loads and combines
+// are skipped by uniform branches, so one instantiation serves every k.
+template <int KMAX, class V, class F>
+__device__ __forceinline__ void tree_fold(V *v, int k, uint32_t pres, F f)
+{
+#pragma unroll
+    for (int m = 1; m < KMAX; m <<= 1) {
+#pragma unroll
+        for (int q = 0; q < KMAX; q += 2 * m)
+            if (q + m < k) {
+                const bool a = (pres >> q) & 1u, b = (pres >> (q + m)) & 1u;
+                if (a && b)
+                    v[q] = f(v[q], v[q + m]);
+                else if (b)
+                    v[q] = v[q + m];
+            }
+        pres |= pres >> m;
+    }
+}
+
 template <class C, int KMAX, int U>
 __global__ void __launch_bounds__(256)
-k_contig_tree(MultiIn<typename C::unit> ins, int k, typename C::unit *__restrict__ out,
+k_contig_tree(MultiIn<typename C::unit> ins, int k, uint32_t pres, typename C::unit *__restrict__ out,
               uint64_t head, uint64_t npk, uint64_t tail_start, uint32_t ntail, Params prm)
 {
     using T = typename C::unit;
     v4u *vout = reinterpret_cast<v4u *>(out + head);
     const uint64_t nt = blockDim.x;
     const uint64_t stride = (uint64_t) gridDim.x * nt * U;
+    auto cv = [&](v4u a, v4u b) { return combine16<C>(a, b, prm); };
+    auto ce = [&](T a, T b) { return C::apply(a, b, prm); };
     for (uint64_t i = (uint64_t) blockIdx.x * nt * U + threadIdx.x; i < npk; i += stride) {
         v4u v[U][KMAX];
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
             for (int q = 0; q < KMAX; ++q)
-                if (q < k && i + u * nt < npk)
+                if (q < k && ((pres >> q) & 1u) && i + u * nt < npk)
                     v[u][q] = ld16<true>(reinterpret_cast<const v4u *>(ins.p[q] + head) + i + u * nt);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (i + u * nt >= npk)
                 continue;
-#pragma unroll
-            for (int m = 1; m < KMAX; m <<= 1)
-#pragma unroll
-                for (int q = 0; q < KMAX; q += 2 * m)
-                    if (q + m < k)
-                        v[u][q] = combine16<C>(v[u][q], v[u][q + m], prm);
+            tree_fold<KMAX>(v[u], k, pres, cv);
             st16<true>(vout + i + u * nt, v[u][0]);
         }
     }
@@ -257,14 +274,9 @@ k_contig_tree(MultiIn<typename C::unit> ins, int k, typename C::unit *__restrict
             T v[KMAX];
 #pragma unroll
             for (int q = 0; q < KMAX; ++q)
-                if (q < k)
+                if (q < k && ((pres >> q) & 1u))
                     v[q] = ins.p[q][t];
-#pragma unroll
-            for (int m = 1; m < KMAX; m <<= 1)
-#pragma unroll
-                for (int q = 0; q < KMAX; q += 2 * m)
-                    if (q + m < k)
-                        v[q] = C::apply(v[q], v[q + m], prm);
+            tree_fold<KMAX>(v, k, pres, ce);
             out[t] = v[0];
         };
         for (uint64_t t = threadIdx.x; t < head; t += blockDim.x)
@@ -277,23 +289,19 @@ k_contig_tree(MultiIn<typename C::unit> ins, int k, typename C::unit *__restrict
 // the same fold element by element, for operands not sharing a 16-byte phase
 template <class C>
 __global__ void __launch_bounds__(256)
-k_elem_tree(MultiIn<typename C::unit> ins, int k, typename C::unit *__restrict__ out, uint64_t n,
-            Params prm)
+k_elem_tree(MultiIn<typename C::unit> ins, int k, uint32_t pres, typename C::unit *__restrict__ out,
+            uint64_t n, Params prm)
 {
     using T = typename C::unit;
+    auto ce = [&](T a, T b) { return C::apply(a, b, prm); };
     const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
     for (uint64_t t = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x; t < n; t += stride) {
         T v[kMaxMulti];
 #pragma unroll
         for (int q = 0; q < kMaxMulti; ++q)
-            if (q < k)
+            if (q < k && ((pres >> q) & 1u))
                 v[q] = ins.p[q][t];
-#pragma unroll
-        for (int m = 1; m < kMaxMulti; m <<= 1)
-#pragma unroll
-            for (int q = 0; q < kMaxMulti; q += 2 * m)
-                if (q + m < k)
-                    v[q] = C::apply(v[q], v[q + m], prm);
+        tree_fold<kMaxMulti>(v, k, pres, ce);
         out[t] = v[0];
     }
 }
@@ -534,7 +542,8 @@ hipError_t launch_multi(const void *const *ins, int k, void *io, uint64_t count,
     return hipGetLastError();
 }
 
-// out = tree fold of ins[0..k-1] (k a power of two, 2..16; k_contig_tree)
+// out = tree fold of ins[0..k-1] (k a power of two, 2..16; k_contig_tree);
+// a NULL slot is absent (its partner passes through)
 template <class C>
 hipError_t launch_tree(const void *const *ins, int k, void *out, uint64_t count, const Params &prm,
                        const LaunchCfg &cfg, hipStream_t s)
@@ -544,8 +553,12 @@ hipError_t launch_tree(const void *const *ins, int k, void *out, uint64_t count,
     MultiIn<T> mi{};
     uintptr_t ao = reinterpret_cast<uintptr_t>(out);
     bool aligned = (ao % sizeof(T)) == 0;
+    uint32_t pres = 0;
     for (int q = 0; q < k; ++q) {
         mi.p[q] = static_cast<const T *>(ins[q]);
+        if (!ins[q])
+            continue;
+        pres |= 1u << q;
         aligned = aligned && ((reinterpret_cast<uintptr_t>(ins[q]) & 15) == (ao & 15));
     }
     (void) cfg;
@@ -559,13 +572,15 @@ hipError_t launch_tree(const void *const *ins, int k, void *out, uint64_t count,
         uint32_t ntail = (uint32_t) (count - tail_start);
         if (k == 2)     // out = a OP b: the contiguous kernel's 4 packets per lane
             hipLaunchKernelGGL((k_contig_tree<C, 2, 4>), dim3(grid_for(256 * 4, npk, 0)),
-                               dim3(256), 0, s, mi, k, tout, head, npk, tail_start, ntail, prm);
+                               dim3(256), 0, s, mi, k, pres, tout, head, npk, tail_start, ntail,
+                               prm);
         else
             hipLaunchKernelGGL((k_contig_tree<C, kMaxMulti, 1>), dim3(grid_for(256, npk, 0)),
-                               dim3(256), 0, s, mi, k, tout, head, npk, tail_start, ntail, prm);
+                               dim3(256), 0, s, mi, k, pres, tout, head, npk, tail_start, ntail,
+                               prm);
     } else {
         hipLaunchKernelGGL((k_elem_tree<C>), dim3(grid_for(256 * 4, count, 0)), dim3(256), 0, s,
-                           mi, k, tout, count, prm);
+                           mi, k, pres, tout, count, prm);
     }
     return hipGetLastError();
 }

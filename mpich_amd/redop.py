@@ -269,9 +269,10 @@ def reduce_local_multi_async(inbufs, inoutbuf, count, datatype, op, stream=None)
 
 def reduce_local_tree_async(inbufs, outbuf, count, datatype, op, stream=None):
     """outbuf = pairwise tree fold of the 2^L inbufs, levels m = 1, 2, 4, ...
-    (slot s = slot s OP slot s+m); outbuf may be inbufs[0]."""
-    _span_check(count, datatype, op, outbuf, *inbufs)
-    arr = (ctypes.c_void_p * len(inbufs))(*[_addr(b) for b in inbufs])
+    (slot s = slot s OP slot s+m); outbuf may be one of the inbufs exactly; a
+    None slot (not slot 0) is absent: its partner passes through."""
+    _span_check(count, datatype, op, outbuf, *[b for b in inbufs if b is not None])
+    arr = (ctypes.c_void_p * len(inbufs))(*[None if b is None else _addr(b) for b in inbufs])
     return lib().MPIX_Reduce_local_tree_async(arr, len(inbufs), _addr(outbuf), count,
                                               H.as_c_int(datatype), H.as_c_int(op),
                                               _stream_ptr(stream))

@@ -54,7 +54,7 @@ def _inputs(P, n, case, seed):
 @SETTINGS
 @given(P=st.integers(1, 12), case=st.sampled_from(CASES),
        algo=st.sampled_from(['recursive_halving', 'pairwise', 'pairwise_sequential',
-                             'pairwise_pipelined']),
+                             'pairwise_pipelined', 'pull', 'recursive_halving_pull']),
        in_place=st.booleans(), data=st.data(), seed=st.integers(0, 2**31))
 def test_reduce_scatter_random(oracle, P, case, algo, in_place, data, seed):
     from mpich_amd import ccl
@@ -62,7 +62,7 @@ def test_reduce_scatter_random(oracle, P, case, algo, in_place, data, seed):
     counts = data.draw(st.lists(st.integers(0, 90), min_size=P, max_size=P))
     total = sum(counts)
     sends = _inputs(P, total, case, seed)
-    sim = 'recursive_halving' if algo == 'recursive_halving' else 'pairwise'
+    sim = 'recursive_halving' if algo.startswith('recursive_halving') else 'pairwise'
     exp = oracle.rs_schedule(sends, counts, dt, op, sim)
     comms = host_comms(P, oracle)
     bufs = [s.copy() if in_place else np.zeros(max(1, counts[r]) * ext, np.uint8)
@@ -157,7 +157,7 @@ def _dev(a):
 @GPU_SETTINGS
 @given(P=st.integers(2, 8), case=st.sampled_from(CASES),
        algo=st.sampled_from(['recursive_halving', 'pairwise', 'pairwise_sequential',
-                             'pairwise_pipelined']),
+                             'pairwise_pipelined', 'pull', 'recursive_halving_pull']),
        in_place=st.booleans(), data=st.data(), seed=st.integers(0, 2**31))
 def test_reduce_scatter_random_device(oracle, P, case, algo, in_place, data, seed):
     import torch
@@ -165,7 +165,7 @@ def test_reduce_scatter_random_device(oracle, P, case, algo, in_place, data, see
     dt, op, ext = case
     counts = data.draw(st.lists(st.integers(0, 6000), min_size=P, max_size=P))
     sends = _inputs(P, sum(counts), case, seed)
-    sim = 'recursive_halving' if algo == 'recursive_halving' else 'pairwise'
+    sim = 'recursive_halving' if algo.startswith('recursive_halving') else 'pairwise'
     exp = oracle.rs_schedule(sends, counts, dt, op, sim)
     dsend = [_dev(s) for s in sends]
     bufs = [_dev(s) if in_place else torch.zeros(max(1, counts[r]) * ext, dtype=torch.uint8,

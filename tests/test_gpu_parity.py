@@ -579,14 +579,15 @@ def _special_f64(rng, n):
                                            ('MPI_FLOAT', 'MPI_REPLACE'), ('MPI_FLOAT', 'MPI_NO_OP')])
 def test_tree_combine(R, H, oracle, k, dtname, opname):
     """MPIX_Reduce_local_tree_async == the level-by-level fold done with
-    MPI_Reduce_local calls (slot s = slot s OP slot s+m, m = 1, 2, 4, ...):
-    bit-exact, NaN payloads and +-0 included; packet path, unaligned element
-    path and in place (out = slot 0)"""
+    MPI_Reduce_local calls (slot s = slot s OP slot s+m, m = 1, 2, 4, ...;
+    an absent slot's partner passes through): bit-exact, NaN payloads and +-0
+    included; packet path, unaligned element path and in place (out = slot 0)"""
     dt, op = getattr(H, dtname), getattr(H, opname)
     ext = R.datatype_extent(dt)
-    for n, off, in_place in ((100003, 0, False), (4097, 4 if ext % 8 else 8, False),
-                             (65536 + 5, 0, True)):
-        rng = np.random.default_rng(k * 7919 + n + (1 if in_place else 0))
+    # in_place: None, or the slot whose buffer is also the output
+    for n, off, in_place in ((100003, 0, None), (4097, 4 if ext % 8 else 8, None),
+                             (65536 + 5, 0, 0), (65536 + 5, 0, 1)):
+        rng = np.random.default_rng(k * 7919 + n + (0 if in_place is None else 1 + in_place))
         nb = n * ext + 64
 
         def mk():
@@ -604,20 +605,26 @@ def test_tree_combine(R, H, oracle, k, dtname, opname):
                     rng.uniform(-1, 1, nb // 8).view(np.uint8)
             return rng.uniform(-1, 1, nb // 4).astype(np.float32).view(np.uint8)
         ins = [mk() for _ in range(k)]
-        v = [x[off:off + n * ext].copy() for x in ins]
+        # absent slots (None): every odd slot above k/2, as the fold of a
+        # non-power-of-two world leaves them (slot 0 always present)
+        absent = {q for q in range(k) if q % 2 and q > k // 2} if k >= 4 else set()
+        v = [None if q in absent else x[off:off + n * ext].copy() for q, x in enumerate(ins)]
         m = 1
         while m < k:
             for q in range(0, k, 2 * m):
-                oracle.reduce_local(v[q + m], v[q], n, dt, op)
+                if v[q] is not None and v[q + m] is not None:
+                    oracle.reduce_local(v[q + m], v[q], n, dt, op)
+                elif v[q + m] is not None:
+                    v[q] = v[q + m]
             m *= 2
         exp = v[0]
-        dins = [dev(x) for x in ins]
-        if in_place:
-            dout, oo = dins[0], off
+        dins = [None if q in absent else dev(x) for q, x in enumerate(ins)]
+        if in_place is not None:
+            dout, oo = dins[in_place], off
         else:
             dout, oo = dev(np.zeros(nb, np.uint8)), off
-        rc = R.reduce_local_tree_async([d.data_ptr() + off for d in dins], dout.data_ptr() + oo, n,
-                                       dt, op)
+        rc = R.reduce_local_tree_async([None if d is None else d.data_ptr() + off for d in dins],
+                                       dout.data_ptr() + oo, n, dt, op)
         assert rc == 0, rc
         got = host(dout)[oo:oo + n * ext]
         assert got.tobytes() == exp.tobytes(), (n, off, in_place)
