@@ -753,8 +753,13 @@ def rsb_secondary(args, world, rank, dev, out):
         else:   # pairwise family and the pulls: one block per peer link, all links at once
             link_bytes = total * 4 / world
             links = world - 1
+        cc.set_step_timing(True)        # one more call: rank 0's per-step device times
+        once()
+        torch.cuda.synchronize()
+        cc.set_step_timing(False)
+        steps = cc.step_times()
         out[name] = dict(parity_redscatblk3_all_ranks=True, ms=round(t * 1e3, 3),
-                         bit_identical_to=bits,
+                         bit_identical_to=bits, steps_rank0=steps,
                          busbw_GBs=round((world - 1) / world * total * 4 / t / 1e9, 2),
                          per_link_GBs=round(link_bytes / t / 1e9, 2), links_active=links,
                          frac_of_xgmi_link=round(link_bytes / t / 1e9 / XGMI_LINK_GBS, 4))
