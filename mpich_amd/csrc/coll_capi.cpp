@@ -845,6 +845,7 @@ int rs_pairwise(const char *sb, char *rb, const std::vector<size_t> &cnts, MPIX_
     const size_t blk = cnts[rank] * ext, sstride = round256(blk);
     const bool in_place = sb == rb;
     char *acc = in_place ? rb + disps[rank] * ext : rb;
+    TRY(mark(c, "start", s));
     if (!in_place)
         TRY(copy(c, rb, sb + disps[rank] * ext, blk, s));                   // :58-64
     if (!concurrent) {
@@ -864,8 +865,10 @@ int rs_pairwise(const char *sb, char *rb, const std::vector<size_t> &cnts, MPIX_
             ins.push_back(ws + (i - 1) * sstride);
         }
         TRY(exchange(c, ops, s));
+        TRY(mark(c, "exchange", s));
         if (cnts[rank])
             TRY(combine_multi(c, ins, acc, (MPIX_Aint) cnts[rank], dt, op, s));
+        TRY(mark(c, "combine", s));
     }
     if (in_place && rank != 0) {
         // with uneven counts the own block can overlap the front of recvbuf;
@@ -1206,6 +1209,7 @@ int rs_pull(const char *sb, char *rb, const std::vector<size_t> &cnts, MPIX_Data
     const size_t blk = cnts[rank] * ext;
     const bool in_place = sb == rb;
     char *acc = in_place ? rb + disps[rank] * ext : rb;
+    TRY(mark(c, "start", s));
     std::vector<const char *> bases(size, sb);  // where each rank's inputs are read
     if (c->kind == K_LOCAL_DEV) {
         // threads of one process: the user buffers themselves
