@@ -60,5 +60,5 @@ extern "C" const char *mpix_build_info(void)
 {
     return "libmpix_redop gfx950 HIP " MPIX_STR(HIP_VERSION_MAJOR) "." MPIX_STR(HIP_VERSION_MINOR)
         " unroll=" MPIX_STR(MPIX_REDOP_UNROLL) " nt_load=" MPIX_STR(MPIX_REDOP_NT_LOAD)
-        " nt_store=" MPIX_STR(MPIX_REDOP_NT_STORE);
+        " nt_store=" MPIX_STR(MPIX_REDOP_NT_STORE) " grouped_loads=" MPIX_STR(MPIX_REDOP_GROUPED_LOADS);
 }

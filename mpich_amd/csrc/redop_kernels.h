@@ -32,6 +32,9 @@
 #ifndef MPIX_REDOP_NT_STORE
 #define MPIX_REDOP_NT_STORE 1
 #endif
+#ifndef MPIX_REDOP_GROUPED_LOADS
+#define MPIX_REDOP_GROUPED_LOADS 1
+#endif
 
 namespace mpix {
 
@@ -79,7 +82,9 @@ template <class C> __device__ __forceinline__ v4u combine16(v4u a, v4u b, const 
 // AIN: `in` has the same 16-byte phase as `io` (packet loads); otherwise it
 // is only element-aligned and its packets are read with unaligned loads
 // (still one dwordx4 per lane; the lines are shared with the neighbours').
-template <class C, int U, bool NTL, bool NTS, bool AIN = true>
+// GRP: issue all U `inout` packet loads, then all U `in` loads (instead of
+// alternating them per packet)
+template <class C, int U, bool NTL, bool NTS, bool AIN = true, bool GRP = MPIX_REDOP_GROUPED_LOADS>
 __global__ void __launch_bounds__(1024)
 k_contig(const typename C::unit *__restrict__ in, typename C::unit *__restrict__ io,
          uint64_t head, uint64_t npk, uint64_t tail_start, uint32_t ntail, Params prm)
@@ -99,10 +104,19 @@ k_contig(const typename C::unit *__restrict__ in, typename C::unit *__restrict__
     for (uint64_t i = (uint64_t) blockIdx.x * tile + threadIdx.x; i < npk; i += stride) {
         if (i + (U - 1) * nt < npk) {
             v4u a[U], b[U];
+            if constexpr (GRP) {
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                a[u] = ld16<NTL>(vio + i + u * nt);
-                b[u] = ldin(i + u * nt);
+                for (int u = 0; u < U; ++u)
+                    a[u] = ld16<NTL>(vio + i + u * nt);
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    b[u] = ldin(i + u * nt);
+            } else {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    a[u] = ld16<NTL>(vio + i + u * nt);
+                    b[u] = ldin(i + u * nt);
+                }
             }
 #pragma unroll
             for (int u = 0; u < U; ++u)
