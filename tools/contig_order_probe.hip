@@ -21,20 +21,36 @@ using namespace mpix;
 
 using C = FSum<float>;
 
-static void launch(bool grp, const float *in, float *io, uint64_t n, hipStream_t s)
+// variant 0: alternating U=4 (round 1), 1: grouped U=4 (shipped), 2: grouped U=8,
+// 3: grouped U=2, 4: grouped U=4 with 512-thread blocks
+static void launch(int v, const float *in, float *io, uint64_t n, hipStream_t s)
 {
     const uint64_t npk = n / 4;
-    const unsigned grid = (unsigned) (npk / (256 * 4));
     Params prm{};
-    if (grp)
-        hipLaunchKernelGGL((k_contig<C, 4, true, true, true, true>), dim3(grid), dim3(256), 0, s,
-                           in, io, 0, npk, npk * 4, 0u, prm);
-    else
-        hipLaunchKernelGGL((k_contig<C, 4, true, true, true, false>), dim3(grid), dim3(256), 0, s,
-                           in, io, 0, npk, npk * 4, 0u, prm);
+    switch (v) {
+        case 0:
+            hipLaunchKernelGGL((k_contig<C, 4, true, true, true, false>), dim3((unsigned) (npk / 1024)),
+                               dim3(256), 0, s, in, io, 0, npk, npk * 4, 0u, prm);
+            break;
+        case 2:
+            hipLaunchKernelGGL((k_contig<C, 8, true, true, true, true>), dim3((unsigned) (npk / 2048)),
+                               dim3(256), 0, s, in, io, 0, npk, npk * 4, 0u, prm);
+            break;
+        case 3:
+            hipLaunchKernelGGL((k_contig<C, 2, true, true, true, true>), dim3((unsigned) (npk / 512)),
+                               dim3(256), 0, s, in, io, 0, npk, npk * 4, 0u, prm);
+            break;
+        case 4:
+            hipLaunchKernelGGL((k_contig<C, 4, true, true, true, true>), dim3((unsigned) (npk / 2048)),
+                               dim3(512), 0, s, in, io, 0, npk, npk * 4, 0u, prm);
+            break;
+        default:
+            hipLaunchKernelGGL((k_contig<C, 4, true, true, true, true>), dim3((unsigned) (npk / 1024)),
+                               dim3(256), 0, s, in, io, 0, npk, npk * 4, 0u, prm);
+    }
 }
 
-static double timeit(bool grp, const float *in, float *io, uint64_t n, hipStream_t s)
+static double timeit(int grp, const float *in, float *io, uint64_t n, hipStream_t s)
 {
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
@@ -78,8 +94,8 @@ int main()
     CK(hipStreamSynchronize(s));
     // same bits
     CK(hipMemcpyAsync(y2, y, N * 4, hipMemcpyDeviceToDevice, s));
-    launch(false, x, y, N, s);
-    launch(true, x, y2, N, s);
+    launch(0, x, y, N, s);
+    launch(1, x, y2, N, s);
     CK(hipStreamSynchronize(s));
     std::vector<float> h1(1 << 20), h2(1 << 20);
     bool ok = true;
@@ -94,13 +110,17 @@ int main()
                          {"slab+4KiB", slab + N + 1024, slab},
                          {"slab+64KiB", slab + N + 16384, slab}};
     printf("{\"ok\": %s", ok ? "true" : "false");
+    const char *names[5] = {"alternating_u4", "grouped_u4", "grouped_u8", "grouped_u2",
+                            "grouped_u4_b512"};
     for (auto &p : ps) {
-        double sa = 0, sb = 0;
-        for (int r = 0; r < 6; ++r) {
-            sa += timeit(false, p.in, p.io, N, s);
-            sb += timeit(true, p.in, p.io, N, s);
-        }
-        printf(", \"%s\": {\"alternating_ms\": %.4f, \"grouped_ms\": %.4f}", p.name, sa / 6, sb / 6);
+        double t[5] = {0, 0, 0, 0, 0};
+        for (int r = 0; r < 6; ++r)
+            for (int v = 0; v < 5; ++v)
+                t[v] += timeit(v, p.in, p.io, N, s);
+        printf(", \"%s\": {", p.name);
+        for (int v = 0; v < 5; ++v)
+            printf("%s\"%s_ms\": %.4f", v ? ", " : "", names[v], t[v] / 6);
+        printf("}");
     }
     printf("}\n");
     return ok ? 0 : 1;
