@@ -588,7 +588,8 @@ hipError_t launch_tree(const void *const *ins, int k, void *out, uint64_t count,
             hipLaunchKernelGGL((k_contig_tree<C, 2, 4>), dim3(grid_for(256 * 4, npk, 0)),
                                dim3(256), 0, s, mi, k, pres, tout, head, npk, tail_start, ntail,
                                prm);
-        else
+        else            // one 16-slot form for every k (an 8-slot form, more waves in
+                        // flight, measured 4-9 % slower at k = 4 and 8)
             hipLaunchKernelGGL((k_contig_tree<C, kMaxMulti, 1>), dim3(grid_for(256, npk, 0)),
                                dim3(256), 0, s, mi, k, pres, tout, head, npk, tail_start, ntail,
                                prm);
