@@ -4,6 +4,7 @@
 `--mib` MiB each.  Bytes per launch: tree (k + 1) x block, multi (k + 2) x
 block.  Prints one JSON line.  Usage: python tools/tree_probe.py [--mib 256]"""
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -60,7 +61,35 @@ def main():
                              multi_GBs=round(bm / tm / 1e9, 1)))
             del blocks, out, acc
             torch.cuda.empty_cache()
-    line = json.dumps({'tree_probe': rows})
+    # the pull allgather's gather kernel: 7 segments of `mib` MiB in one launch
+    # against 7 back-to-back hipMemcpyAsync (device to device), local HBM
+    L = redop.lib()
+    vp = ctypes.c_void_p
+    L.MPIX_Copy_multi_async.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(vp),
+                                        ctypes.POINTER(ctypes.c_ssize_t), ctypes.c_int, vp]
+    n = a.mib * (1 << 20) // 4
+    with torch.cuda.stream(s):
+        src = [torch.rand(n, device='cuda') for _ in range(7)]
+        dst = [torch.empty(n, device='cuda') for _ in range(7)]
+        torch.cuda.synchronize()
+        srcs = (vp * 7)(*[t.data_ptr() for t in src])
+        dsts = (vp * 7)(*[t.data_ptr() for t in dst])
+        nb = (ctypes.c_ssize_t * 7)(*([n * 4] * 7))
+
+        def multi():
+            assert L.MPIX_Copy_multi_async(srcs, dsts, nb, 7, vp(s.cuda_stream)) == 0
+
+        def memcpys():
+            for x, y in zip(src, dst):
+                y.copy_(x, non_blocking=True)
+        tc, tm = timed(multi, s), timed(memcpys, s)
+        assert all(torch.equal(x, y) for x, y in zip(src, dst))
+        copy_row = dict(segments=7, segment_MiB=a.mib, copy_multi_ms=round(tc * 1e3, 4),
+                        copy_multi_GBs=round(2 * 7 * n * 4 / tc / 1e9, 1),
+                        memcpy_ms=round(tm * 1e3, 4),
+                        memcpy_GBs=round(2 * 7 * n * 4 / tm / 1e9, 1))
+        del src, dst
+    line = json.dumps({'tree_probe': rows, 'copy_multi': copy_row})
     print(line)
     if a.out:
         with open(a.out, 'w') as f:
