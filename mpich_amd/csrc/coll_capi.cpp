@@ -20,10 +20,12 @@
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
 
+#include <fcntl.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include <chrono>
 #include <condition_variable>
@@ -108,6 +110,9 @@ struct MPIX_Comm_s {
     std::vector<char *> win_old;       // outgrown / rejected windows, freed with the comm
     std::vector<void *> peer_map;      // peers' pull windows, mapped and verified
     bool win_broken = false;           // pulls given up on this communicator
+    struct Nonce { int rank, attempt; uint64_t n0, n1; };
+    std::vector<Nonce> nonce_hist;     // every window nonce published (MPIX_COLL_TRACE)
+    std::vector<int> skew_fds;         // MPIX_COLL_WINDOW_FDSKEW probe hook
     struct Shared {                    // MPIX_Comm_alloc_shared windows
         char *base;                    // header + bytes
         size_t bytes;
@@ -993,6 +998,39 @@ struct LocalRec {   // K_LOCAL_DEV: the raw address
     uint64_t raw;
 };
 
+// MPIX_COLL_TRACE: what a mapping that failed verification shows instead --
+// the nonce of an earlier window (whose, from which attempt), of this round's
+// window of another rank, or nothing published
+void trace_wrong_window(MPIX_Comm c, int q, const uint64_t seen[2], const std::vector<char> &all)
+{
+    const char *what = "no published nonce";
+    int who = -1, when = -1;
+    for (int p = 0; p < c->size; ++p) {
+        WinRec r;
+        memcpy(&r, all.data() + kRec * (size_t) p, sizeof r);
+        if (r.nonce[0] == seen[0] && r.nonce[1] == seen[1]) {
+            what = "this round's window of rank";
+            who = p;
+        }
+    }
+    for (const auto &h : c->nonce_hist)
+        if (who < 0 && h.n0 == seen[0] && h.n1 == seen[1]) {
+            what = "an earlier window of rank";
+            who = h.rank;
+            when = h.attempt;
+        }
+    fprintf(stderr, "[mpix_coll rank %d] window of rank %d reads %016llx%016llx: %s %d (attempt %d)\n",
+            c->rank, q, (unsigned long long) seen[0], (unsigned long long) seen[1], what, who, when);
+    for (int p = 0; p < c->size; ++p) {   // the published handles, to compare
+        WinRec r;
+        memcpy(&r, all.data() + kRec * (size_t) p, sizeof r);
+        fprintf(stderr, "[mpix_coll rank %d]   handle of rank %d:", c->rank, p);
+        for (size_t b = 0; b < sizeof r.handle; ++b)
+            fprintf(stderr, "%02x", (unsigned char) r.handle[b]);
+        fprintf(stderr, "\n");
+    }
+}
+
 void close_maps(std::vector<void *> *maps)
 {
     for (void *m : *maps)
@@ -1016,7 +1054,17 @@ int verified_window(MPIX_Comm c, size_t bytes, hipStream_t s, char **w_out,
         void *w = nullptr;
         WinRec me;
         memset(&me, 0, sizeof me);
-        if (hipMalloc(&w, kWinHdr + bytes) == hipSuccess) {
+        // probe hooks (tools/win_grow_probe.py): a rank- and attempt-dependent
+        // allocation size, and rank-dependent numbers of open descriptors
+        size_t pad = 0;
+        const char *ep = getenv("MPIX_COLL_WINDOW_PAD");
+        if (ep && atoi(ep))
+            pad = ((size_t) c->rank + 1 + (size_t) c->size * attempt) << 21;
+        const char *es = getenv("MPIX_COLL_WINDOW_FDSKEW");
+        if (es && c->skew_fds.empty())
+            for (int k = 0; k < (c->rank + 1) * atoi(es); ++k)
+                c->skew_fds.push_back(open("/dev/null", O_RDONLY));
+        if (hipMalloc(&w, kWinHdr + bytes + pad) == hipSuccess) {
             me.nonce[0] = ((uint64_t) rd() << 32) ^ rd() ^ ((uint64_t) c->rank << 48);
             me.nonce[1] = ((uint64_t) rd() << 32) ^ rd() ^ (uint64_t) attempt;
             hipIpcMemHandle_t h;
@@ -1060,7 +1108,14 @@ int verified_window(MPIX_Comm c, size_t bytes, hipStream_t s, char **w_out,
                 seen[0] != r.nonce[0] || seen[1] != r.nonce[1]) {
                 (void) hipGetLastError();
                 good = 0;
+                if (coll_trace())
+                    trace_wrong_window(c, q, seen, all);
             }
+        }
+        for (int q = 0; q < c->size; ++q) {     // every nonce ever published, for the trace
+            WinRec r;
+            memcpy(&r, all.data() + kRec * (size_t) q, sizeof r);
+            c->nonce_hist.push_back({q, attempt, r.nonce[0], r.nonce[1]});
         }
         // agreement: every rank's mappings verified, or nobody uses them
         std::vector<char> votes;
@@ -2333,6 +2388,9 @@ int MPIX_Comm_free(MPIX_Comm comm)
         if (comm->tok)
             (void) hipFree(comm->tok);
         close_maps(&comm->peer_map);
+        for (int fd : comm->skew_fds)
+            if (fd >= 0)
+                close(fd);
         if (comm->win)
             (void) hipFree(comm->win);
         for (char *w : comm->win_old)
