@@ -104,6 +104,7 @@ struct MPIX_Comm_s {
     hipEvent_t stage_ev = nullptr;     // recorded after the copies out of the staging memory
     char *tok = nullptr;               // barrier tokens / published records, (1 + size) slots
     char *win = nullptr;               // pull window (header + data), see ensure_windows
+    hipEvent_t win_ev = nullptr;       // recorded after the last pull that used the window
     size_t win_bytes = 0;
     std::vector<char *> win_old;       // outgrown / rejected windows, freed with the comm
     std::vector<void *> peer_map;      // peers' pull windows, mapped and verified
@@ -372,11 +373,17 @@ int mark(MPIX_Comm c, const char *label, hipStream_t s)
 // one published record per rank (barrier tokens are 1-byte records)
 constexpr size_t kRec = 256;
 
+// token buffer: (1 + size) record slots, then the barrier's own bytes (one to
+// send, one per peer to receive), so a barrier still in flight on one stream
+// never lands in a record slot another stream's allgather is reading
+size_t tok_bytes(MPIX_Comm c) { return kRec * (size_t) (c->size + 1) + round256(1 + (size_t) c->size); }
+char *barrier_tok(MPIX_Comm c) { return c->tok + kRec * (size_t) (c->size + 1); }
+
 int token_buffer(MPIX_Comm c, hipStream_t s)
 {
     if (c->tok)
         return MPIX_REDOP_SUCCESS;
-    const size_t bytes = kRec * (size_t) (c->size + 1);
+    const size_t bytes = tok_bytes(c);
     if (c->host()) {
         c->tok = static_cast<char *>(calloc(1, bytes));
         return c->tok ? MPIX_REDOP_SUCCESS : MPIX_REDOP_ERR_OTHER;
@@ -428,10 +435,11 @@ int barrier(MPIX_Comm c, hipStream_t s)
         return MPIX_REDOP_SUCCESS;
     TRY(token_buffer(c, s));
     std::vector<MPIX_P2p_op> ops;
+    char *t = barrier_tok(c);
     for (int q = 0; q < c->size; ++q)
         if (q != c->rank) {
-            ops.push_back(snd(q, c->tok, 1));
-            ops.push_back(rcv(q, c->tok + kRec * (size_t) (1 + q), 1));
+            ops.push_back(snd(q, t, 1));
+            ops.push_back(rcv(q, t + 1 + q, 1));
         }
     return exchange(c, ops, s);
 }
@@ -1177,11 +1185,17 @@ int ensure_windows(MPIX_Comm c, size_t need, hipStream_t s, bool *ok)
     *ok = false;
     if (c->win_broken)
         return MPIX_REDOP_SUCCESS;
+    // the window is shared by pulls issued on any stream: a new user is
+    // ordered behind the previous one (its closing barrier) on the device
+    if (!c->win_ev)
+        HTRY(hipEventCreateWithFlags(&c->win_ev, hipEventDisableTiming));
     if (c->win && c->win_bytes >= need) {
+        HTRY(hipStreamWaitEvent(s, c->win_ev, 0));
         *ok = true;
         return MPIX_REDOP_SUCCESS;
     }
-    HTRY(hipStreamSynchronize(s));      // nothing in flight reads the old mappings
+    HTRY(hipEventSynchronize(c->win_ev));   // nothing in flight reads the old mappings
+    HTRY(hipStreamSynchronize(s));
     close_maps(&c->peer_map);
     if (c->win) {                       // outgrown: kept allocated, see above
         c->win_old.push_back(c->win);
@@ -1294,6 +1308,7 @@ int rs_pull(const char *sb, char *rb, const std::vector<size_t> &cnts, MPIX_Data
     char *acc = in_place ? rb + disps[rank] * ext : rb;
     TRY(mark(c, "start", s));
     std::vector<const char *> bases(size, sb);  // where each rank's inputs are read
+    bool used_win = false;
     if (c->kind == K_LOCAL_DEV) {
         // threads of one process: the user buffers themselves
         LocalRec me{1, 0, reinterpret_cast<uint64_t>(sb)};
@@ -1321,6 +1336,7 @@ int rs_pull(const char *sb, char *rb, const std::vector<size_t> &cnts, MPIX_Data
             TRY(ensure_windows(c, total * ext, s, &ok));
             if (!ok)
                 return fallback();
+            used_win = true;
             // the blocks the peers read (this rank's own block is read from sb)
             char *wd = c->win + kWinHdr;
             TRY(copy(c, wd, sb, disps[rank] * ext, s));
@@ -1365,6 +1381,8 @@ int rs_pull(const char *sb, char *rb, const std::vector<size_t> &cnts, MPIX_Data
         TRY(combine_multi(c, ins, acc, (MPIX_Aint) cnts[rank], dt, op, s));
     TRY(mark(c, "pull+combine", s));
     TRY(barrier(c, s));                 // peers done reading this rank's buffer / window
+    if (used_win)
+        HTRY(hipEventRecord(c->win_ev, s));
     if (in_place && rank != 0) {
         if (disps[rank] * ext < blk) {
             char *w;
@@ -1600,6 +1618,7 @@ int allreduce_pull(const char *sendbuf, char *rb, size_t count, MPIX_Datatype dt
     // in_base[q]: where rank q's input is read; out_base[q]: where its
     // reduced block is read in the allgather; out: where this rank's goes
     std::vector<const char *> in_base(size, in), out_base(size, rb);
+    bool used_win = false;
     char *out = mine >= 0 ? rb + disps[mine] * ext : nullptr;
     TRY(mark(c, "start", s));
     if (c->kind == K_LOCAL_DEV) {     // threads of one process: the user buffers
@@ -1636,6 +1655,7 @@ int allreduce_pull(const char *sendbuf, char *rb, size_t count, MPIX_Datatype dt
             TRY(ensure_windows(c, nb, s, &ok));
             if (!ok)
                 return fallback();
+            used_win = true;
             char *wd = c->win + kWinHdr;
             if (mine >= 0) {            // every block but this rank's own (only it reads that)
                 TRY(copy(c, wd, in, disps[mine] * ext, s));
@@ -1693,6 +1713,8 @@ int allreduce_pull(const char *sendbuf, char *rb, size_t count, MPIX_Datatype dt
     }
     TRY(mark(c, "allgather pull", s));
     TRY(barrier(c, s));                 // peers done reading this rank's window / buffers
+    if (used_win)
+        HTRY(hipEventRecord(c->win_ev, s));
     return MPIX_REDOP_SUCCESS;
 }
 
@@ -2415,6 +2437,10 @@ int MPIX_Comm_free(MPIX_Comm comm)
             (void) hipHostFree(comm->stage);
         if (comm->tok)
             (void) hipFree(comm->tok);
+        if (comm->win_ev) {
+            (void) hipEventSynchronize(comm->win_ev);
+            (void) hipEventDestroy(comm->win_ev);
+        }
         close_maps(&comm->peer_map);
         if (comm->win)
             (void) hipFree(comm->win);

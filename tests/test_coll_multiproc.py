@@ -399,3 +399,49 @@ def test_rccl_rsb_matches_oracle(oracle, tmp_path):
     cases.append(('ar_mp', 'allreduce_mp', 'float', 25013))
     cases.append(('ar_pull', 'allreduce_pull', 'float', 25013))
     _run(oracle, tmp_path, world, 'nccl', cases)
+
+
+def _streams_worker(rank, world, port, outdir):
+    import torch.distributed as dist
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from mpich_amd import ccl, coll
+    MPI_INT = 0x4c000405
+    c = coll.comm_for(None, True)
+    n = 30011
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    ins, outs = [], []
+    for it in range(6):
+        # block i of rank r holds r + i + 10 * it (redscatblk3.c:43-48)
+        ins.append(torch.cat([torch.full((n,), rank + i + 10 * it, dtype=torch.int32, device='cuda')
+                              for i in range(world)]))
+        outs.append(torch.empty(n, dtype=torch.int32, device='cuda'))
+    torch.cuda.synchronize()
+    for it in range(6):         # async pulls alternating between two streams, no host sync
+        algo = ('pull', 'recursive_halving_pull')[it % 2]
+        st = streams[it % 2]
+        rc = ccl.reduce_scatter_block(ins[it], outs[it], n, MPI_INT, MPI_SUM, c, algo, stream=st,
+                                      blocking=False)
+        assert rc == 0, rc
+    torch.cuda.synchronize()
+    bad = [it for it in range(6)
+           if not bool(torch.all(outs[it] == world * rank + world * (world - 1) // 2 + world * 10 * it))]
+    with open(os.path.join(outdir, 'streams%d.txt' % rank), 'w') as f:
+        f.write(' '.join(map(str, bad)))
+    dist.barrier()
+    coll.free_comms()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world', [2, 3])
+def test_staged_async_pulls_on_two_streams(tmp_path, world):
+    """the pull window is shared by every call on the communicator: async
+    pulls issued back to back on alternating streams (each call ordered
+    behind the previous user of the window) all give the closed form"""
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    mp.spawn(_streams_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    for r in range(world):
+        assert open(tmp_path / ('streams%d.txt' % r)).read() == '', r
