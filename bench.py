@@ -65,6 +65,8 @@ def parse():
     p.add_argument('--rsb-bytes', type=int, default=4 << 30, help='RSB vector bytes per rank')
     p.add_argument('--extras-timeout', type=float, default=300.0,
                    help='watchdog (s) over the N>1 secondary collective figures and teardown')
+    p.add_argument('--value-timeout', type=float, default=600.0,
+                   help='watchdog (s) over the N>1 value leg (bootstrap, parity check, timed steps)')
     p.add_argument('--pmc', default=os.path.join(ROOT, 'profiles', 'r02_pmc_summary.json'),
                    help='PMC traffic summary (from tools/pmc_summary.py) to quote as traffic')
     return p.parse_args()
@@ -868,17 +870,18 @@ class _Emitter:
             print(json.dumps(r, default=str), flush=True)
 
 
-def _watchdog(seconds, emit):
+def _watchdog(seconds, emit, note=True, code=3):
     """a hung secondary collective: rank 0 still prints the line (with the
     headline), then every rank leaves with a NON-zero status so the hang
-    reads as a failure"""
+    reads as a failure (note=False: the line is printed as it stands)"""
     import threading
 
     def fire():
-        emit.emit('secondary collectives exceeded %.0f s; headline kept, rank exits' % seconds)
+        emit.emit('secondary collectives exceeded %.0f s; headline kept, rank exits' % seconds
+                  if note else None)
         sys.stdout.flush()
         sys.stderr.flush()
-        os._exit(3)
+        os._exit(code)
     t = threading.Timer(seconds, fire)
     t.daemon = True
     t.start()
@@ -908,14 +911,24 @@ def main():
     if world == 1:
         single_gpu(args, dev)
         return 0
+    # a hung value leg (communicator bootstrap, a collective that never
+    # completes) still ends the run with rank 0's error line and a non-zero status
+    failed_line = {'metric': METRIC_RSB, 'value': None, 'unit': 'GB/s', 'n_gpus': world}
+    first = _Emitter(rank, dict(failed_line, error='value leg (reduce-scatter over RCCL) did not '
+                                                   'finish within %.0f s' % args.value_timeout))
+    dog0 = _watchdog(args.value_timeout, first, note=False, code=2)
     try:
         result = multi_gpu(args, world, rank, dev)
     except Exception as e:      # the value leg failed: say so at the top level, exit non-zero
-        if rank == 0:
-            print(json.dumps({'metric': METRIC_RSB, 'value': None, 'unit': 'GB/s', 'n_gpus': world,
-                              'error': '%s: %s' % (type(e).__name__, e)}), flush=True)
+        first.result = dict(failed_line, error='%s: %s' % (type(e).__name__, e))
+        first.emit()
         sys.stdout.flush()
         os._exit(1)
+    dog0.cancel()
+    with first.lock:            # the watchdog fired meanwhile: its line stands
+        if first.done:
+            return 2
+        first.done = True
     emit = _Emitter(rank, result)
     dog = _watchdog(args.extras_timeout, emit)
     result['extras_timeout_s'] = args.extras_timeout
