@@ -1148,7 +1148,7 @@ int verified_window(MPIX_Comm c, size_t bytes, hipStream_t s, char **w_out,
                 if (q != c->rank)
                     check(q, all);
         }
-        for (int q = 0; q < c->size; ++q) {     // every nonce ever published, for the trace
+        for (int q = 0; q < c->size && coll_trace(); ++q) {   // every nonce published, for the trace
             WinRec r;
             memcpy(&r, all.data() + kRec * (size_t) q, sizeof r);
             c->nonce_hist.push_back({q, attempt, r.nonce[0], r.nonce[1]});
