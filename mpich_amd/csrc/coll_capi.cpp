@@ -1207,6 +1207,9 @@ int ensure_windows(MPIX_Comm c, size_t need, hipStream_t s, bool *ok)
     TRY(verified_window(c, bytes, s, &w, &c->peer_map));
     if (!w) {
         c->win_broken = true;
+        if (coll_trace())
+            fprintf(stderr, "[mpix_coll rank %d] pull windows given up: the RCCL-transport "
+                            "schedules run instead\n", c->rank);
         return MPIX_REDOP_SUCCESS;
     }
     c->win = w;

@@ -445,3 +445,53 @@ def test_staged_async_pulls_on_two_streams(tmp_path, world):
     mp.spawn(_streams_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
     for r in range(world):
         assert open(tmp_path / ('streams%d.txt' % r)).read() == '', r
+
+
+def _growth_worker(rank, world, port, outdir):
+    import torch.distributed as dist
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    os.environ['MPIX_COLL_TRACE'] = '1'
+    torch.cuda.set_device(0)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    trace = open(os.path.join(outdir, 'gtrace%d.txt' % rank), 'w')
+    os.dup2(trace.fileno(), 2)          # the library's trace lines land in the file
+    from mpich_amd import coll
+    MPI_INT = 0x4c000405
+    bad = []
+    # the bench's order: a small window first, then growth to a large one
+    for it, (algo, n) in enumerate((('recursive_halving_pull', 4099), ('recursive_halving_pull', 1 << 22),
+                                    ('pull', 1 << 22), ('pull', 1 << 23))):
+        blk = torch.cat([torch.full((n,), rank + i + it, dtype=torch.int32, device='cuda')
+                         for i in range(world)])
+        o = torch.empty(n, dtype=torch.int32, device='cuda')
+        torch.cuda.synchronize()
+        coll.reduce_scatter_block(blk, o, n, MPI_INT, MPI_SUM, algorithm=algo)
+        torch.cuda.synchronize()
+        if not bool(torch.all(o == world * rank + world * (world - 1) // 2 + world * it)):
+            bad.append('%s@%d' % (algo, n))
+        del blk, o
+        torch.cuda.empty_cache()
+    with open(os.path.join(outdir, 'growth%d.txt' % rank), 'w') as f:
+        f.write(' '.join(bad))
+    dist.barrier()
+    coll.free_comms()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world', [2, 3])
+def test_staged_pull_windows_grow_and_verify(tmp_path, world):
+    """the pull window starts small and grows twice with the message (to
+    world x 16 MiB, then world x 32 MiB per rank) and every window verifies
+    -- exported one rank at a time, a retry allowed -- so the pulls really
+    run instead of falling back (which would give the same bits, hiding a
+    broken window path)"""
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    mp.spawn(_growth_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    for r in range(world):
+        assert open(tmp_path / ('growth%d.txt' % r)).read() == '', r
+        lines = open(tmp_path / ('gtrace%d.txt' % r)).read().splitlines()
+        assert not any('given up' in ln for ln in lines), lines
+        sizes = [ln for ln in lines if 'pull window' in ln and 'all 1' in ln]
+        assert len(sizes) == 3, lines       # the first window, then two growths
