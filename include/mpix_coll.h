@@ -153,8 +153,10 @@ int MPIX_Comm_free(MPIX_Comm comm);
                                            all P ranks over xGMI (pull windows, as
                                            MPIX_RSB_PULL) and folds them level by level as the
                                            log2(P) halving steps would, writing recvbuf
-                                           directly.  P a power of two <= 16 and a device
-                                           communicator; otherwise RECURSIVE_HALVING */
+                                           directly.  P <= 16 (P not a power of two: the
+                                           reference's pair fold is the tree's first level)
+                                           and a device communicator; otherwise
+                                           RECURSIVE_HALVING */
 #define MPIX_RSB_LAST               MPIX_RSB_RECURSIVE_HALVING_PULL
 size_t MPIX_Reduce_scatter_block_workspace(MPIX_Aint recvcount, MPIX_Datatype datatype,
                                            MPIX_Comm comm, int algorithm);
@@ -236,8 +238,10 @@ int MPIX_Exscan_async(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_
                                                    rank's block of every rank's input
                                                    (MPIX_Reduce_local_tree_async), then ONE copy
                                                    kernel reads every peer's finished block
-                                                   (MPIX_Copy_multi_async); no workspace.  P a power of two <= 16 on a device
-                                                   communicator, else REDUCE_SCATTER_ALLGATHER */
+                                                   (MPIX_Copy_multi_async); no workspace.  P <= 16
+                                                   (P not a power of two: the reference's pair
+                                                   fold first) on a device communicator, else
+                                                   REDUCE_SCATTER_ALLGATHER */
 #define MPIX_ALLREDUCE_LAST                 MPIX_ALLREDUCE_PULL
 size_t MPIX_Allreduce_workspace(MPIX_Aint count, MPIX_Datatype datatype, MPIX_Comm comm);
 int MPIX_Allreduce(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Datatype datatype,
