@@ -76,7 +76,12 @@ template <typename T> struct IBxor {
 
 // Fortran logicals: MPII_FROM_FLOG(x) = (x == .FALSE. ? 0 : 1), compared after
 // the usual promotion; MPII_TO_FLOG(c) = c ? .TRUE. : .FALSE. cast to T.
-template <typename T> struct FlogW { using type = long long; };
+// The logical kinds are signed (int8..int128) and .FALSE. is an int
+// (mpii_fortlogical.h:13), so the comparison is in int up to 4-byte kinds --
+// exactly C's promotion, and one 32-bit compare per element instead of a
+// sign-extended 64-bit one.
+template <typename T> struct FlogW { using type = int; };
+template <> struct FlogW<int64_t> { using type = long long; };
 template <> struct FlogW<__int128> { using type = __int128; };
 template <typename T> MPIX_DEV int flog_from(T x, const Params &p)
 {
