@@ -1,7 +1,9 @@
 # A/B of the synchronous call's completion word at the headline size: the
 # stream write (hipStreamWriteValue32, default MPIX_REDOP_SYNC=flag) against a
 # one-lane signal kernel (MPIX_REDOP_SYNC=kernel), alternating processes; then
-# the GPU parity/boundary suites under the kernel mode.
+# the GPU parity/boundary suites under the kernel mode.  The kernel mode was
+# removed after this A/B (no gain, profiles/r02_sync_kernel_ab.json); rerunning
+# this script needs it back in redop_capi.cpp.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
