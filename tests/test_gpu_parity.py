@@ -438,6 +438,46 @@ def test_fortran_booleans(R, H, oracle):
         oracle.set_fortran_booleans(1, 0)
 
 
+def _flog_operand(rng, n, size, tv, fv):
+    """n logicals of `size` bytes: the kind's own truncations of .TRUE. and
+    .FALSE., 0, 1, -1 and random words; LOGICAL16 words are sign-extended
+    int64 or carry random high halves (the comparison is full width)"""
+    pick = np.array([tv, fv, 0, 1, -1], dtype=np.int64)
+    lo = np.where(rng.random(n) < 0.8, pick[rng.integers(0, 5, n)],
+                  rng.integers(-(1 << 62), 1 << 62, n))
+    if size == 16:
+        hi = np.where(lo < 0, -1, 0)
+        hi = np.where(rng.random(n) < 0.1, rng.integers(-(1 << 62), 1 << 62, n), hi)
+        return np.stack([lo, hi], 1).astype(np.int64).view(np.uint8).reshape(-1)
+    return lo.astype({1: np.int8, 2: np.int16, 4: np.int32, 8: np.int64}[size]).view(np.uint8)
+
+
+@pytest.mark.parametrize('kind,size', [('MPI_LOGICAL1', 1), ('MPI_LOGICAL2', 2), ('MPI_LOGICAL4', 4),
+                                       ('MPI_LOGICAL8', 8), ('MPI_LOGICAL16', 16)])
+@pytest.mark.parametrize('tv,fv', [(1, 0), (-1, 0), (5, -3), (300, 7), (7, 300), (0, 1)])
+def test_fortran_logical_kinds(R, H, oracle, kind, size, tv, fv):
+    """MPII_FROM_FLOG compares each kind after C's promotion against an int
+    .FALSE. (mpii_fortlogical.h:13,29) and MPII_TO_FLOG casts .TRUE./.FALSE.
+    back to the kind: every logical kind, booleans that do and do not fit it"""
+    dt = getattr(H, kind)
+    n = 20011
+    rng = np.random.default_rng(size * 1000 + (tv & 0xff) * 7 + (fv & 0xff))
+    a = _flog_operand(rng, n, size, tv, fv)
+    b = _flog_operand(rng, n, size, tv, fv)
+    try:
+        R.set_fortran_booleans(tv, fv)
+        oracle.set_fortran_booleans(tv, fv)
+        for op in (H.MPI_LAND, H.MPI_LOR, H.MPI_LXOR):
+            da, db = dev(a), dev(b)
+            assert R.MPI_Reduce_local(db, da, n, dt, op) == 0
+            exp = a.copy()
+            assert oracle.reduce_local(b.copy(), exp, n, dt, op) == 0
+            assert np.array_equal(host(da), exp), (kind, tv, fv, op)
+    finally:
+        R.set_fortran_booleans(1, 0)
+        oracle.set_fortran_booleans(1, 0)
+
+
 @pytest.mark.parametrize('blocklen,stride', [(1, 2), (1, 3), (3, 7), (4, 4), (5, 8)])
 def test_vector_target(R, H, oracle, blocklen, stride):
     """config 5 semantics (typerep_op.c:115-150): vector target, packed source;
