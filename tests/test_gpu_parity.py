@@ -291,6 +291,37 @@ def test_ragged_and_misaligned(R, H, oracle, count, offs):
     assert np.array_equal(host(da).view(np.float32), exp)
 
 
+@pytest.mark.parametrize('dtname,opname,kind,size', SWEEP,
+                         ids=['%s-%s' % (s[0], s[1]) for s in SWEEP])
+def test_relative_misalignment(R, H, oracle, dtname, opname, kind, size):
+    """every (op, type) with `in` and `inout` at different 16-byte phases
+    (the packet kernel's unaligned-`in` form) and, for multi-byte units, at
+    byte offsets that are not even element-aligned (the element-wise kernel);
+    ragged counts, inbuf untouched, the sweep's parity rule"""
+    dt, op = getattr(H, dtname), getattr(H, opname)
+    ext = R.datatype_extent(dt)
+    n = (1 << 16) // ext + 5
+    rng = np.random.default_rng((0x5EED0007 * 17 + dt * 5 + op) & 0xffffffff)
+    offs = [(0, ext), (ext, 0), (3 * ext, 16 - ext if ext < 16 else 32)]
+    if ext > 1:
+        offs += [(1, 0), (0, 3)]
+    for oa, ob in offs:
+        a = make_operand(rng, kind, size, n, dtname).view(np.uint8)
+        b = make_operand(rng, kind, size, n, dtname).view(np.uint8)
+        pa = np.zeros(n * ext + 64, np.uint8)
+        pb = np.zeros(n * ext + 64, np.uint8)
+        pa[oa:oa + n * ext] = a
+        pb[ob:ob + n * ext] = b
+        da, db = dev(pa), dev(pb)
+        assert R.MPI_Reduce_local(db.data_ptr() + ob, da.data_ptr() + oa, n, dt, op) == 0
+        exp = a.copy()
+        assert oracle.reduce_local(b.copy(), exp, n, dt, op) == 0
+        got = host(da)
+        assert not got[:oa].any() and not got[oa + n * ext:].any(), (oa, ob)   # no spill-over
+        assert np.array_equal(host(db)[ob:ob + n * ext], b)
+        assert compare(got[oa:oa + n * ext].copy(), exp, kind, size, opname, ext) == 0, (oa, ob)
+
+
 @pytest.mark.parametrize('dtname,ext', [('MPI_CHAR', 1), ('MPI_SHORT', 2), ('MPI_DOUBLE', 8),
                                         ('MPI_C_DOUBLE_COMPLEX', 16)])
 def test_ragged_small_units(R, H, oracle, dtname, ext):
