@@ -1038,3 +1038,18 @@ def test_pageable_workers_concurrent_callers(R, H, oracle):
             assert np.array_equal(a, e)
     finally:
         R.set_pageable(prev['threads'], prev['chunk_bytes'])
+
+
+def test_bf16_sum_specials_on_gpu(R, H, oracle):
+    """bf16 SUM's half-away store (op_fns.c:473-483) on the HIP path: every
+    pair of the special / tie patterns of tests/test_bf16_oracle.py, bit-exact
+    against the oracle except that a NaN only has to be a NaN"""
+    from tests.test_bf16_oracle import BF16_PATTERNS as pats
+    a = np.repeat(pats, len(pats))
+    b = np.tile(pats, len(pats))
+    da, db = dev(a), dev(b)
+    assert R.MPI_Reduce_local(db, da, len(a), H.MPIX_BFLOAT16, H.MPI_SUM) == 0
+    exp = a.copy()
+    assert oracle.reduce_local(b.copy(), exp, len(a), H.MPIX_BFLOAT16, H.MPI_SUM) == 0
+    got = host(da).view(np.uint16)
+    assert compare(got.view(np.uint8), exp.view(np.uint8), 'bf16', 2, 'MPI_SUM', 2) == 0
