@@ -1053,3 +1053,34 @@ def test_bf16_sum_specials_on_gpu(R, H, oracle):
     assert oracle.reduce_local(b.copy(), exp, len(a), H.MPIX_BFLOAT16, H.MPI_SUM) == 0
     got = host(da).view(np.uint16)
     assert compare(got.view(np.uint8), exp.view(np.uint8), 'bf16', 2, 'MPI_SUM', 2) == 0
+
+
+@pytest.mark.parametrize('dtname,npt', [('MPIX_C_FLOAT16', np.float16), ('MPI_FLOAT', np.float32),
+                                        ('MPI_DOUBLE', np.float64)])
+@pytest.mark.parametrize('opname', ['MPI_MAX', 'MPI_MIN'])
+def test_maxmin_select_specials_on_gpu(R, H, oracle, dtname, npt, opname):
+    """MPL_MAX/MPL_MIN are selects, (a>b)?a:b and (a<b)?a:b (mpl_base.h:105-106):
+    with a NaN on either side the result is the in operand bit for bit
+    (payload and sign kept), and on equal values (+0 vs -0) it is the in
+    operand too.  Every pair of the special values, against the oracle and
+    against numpy's select, bit-exact"""
+    fi = np.finfo(npt)
+    nanbits = {np.float16: [0x7e00, 0xfe01, 0x7c01, 0x7fff],
+               np.float32: [0x7fc00000, 0xffc00001, 0x7f800001, 0x7fffffff],
+               np.float64: [0x7ff8000000000000, 0xfff8000000000001, 0x7ff0000000000001,
+                            0x7fffffffffffffff]}[npt]
+    uint = {np.float16: np.uint16, np.float32: np.uint32, np.float64: np.uint64}[npt]
+    vals = np.array([0.0, -0.0, 1.0, -1.0, np.inf, -np.inf, fi.max, -fi.max, fi.tiny, -fi.tiny,
+                     fi.smallest_subnormal, -fi.smallest_subnormal, 0.5, 2.0], npt)
+    vals = np.concatenate([vals, np.array(nanbits, uint).view(npt)])
+    a = np.repeat(vals, len(vals))
+    b = np.tile(vals, len(vals))
+    da, db = dev(a), dev(b)
+    op = getattr(H, opname)
+    assert R.MPI_Reduce_local(db, da, len(a), getattr(H, dtname), op) == 0
+    got = host(da).view(uint)
+    exp = a.copy()
+    assert oracle.reduce_local(b.copy(), exp, len(a), getattr(H, dtname), op) == 0
+    sel = np.where(a > b, a, b) if opname == 'MPI_MAX' else np.where(a < b, a, b)
+    assert np.array_equal(exp.view(uint), sel.view(uint))
+    assert np.array_equal(got, exp.view(uint))
