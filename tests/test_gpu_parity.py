@@ -1084,3 +1084,37 @@ def test_maxmin_select_specials_on_gpu(R, H, oracle, dtname, npt, opname):
     sel = np.where(a > b, a, b) if opname == 'MPI_MAX' else np.where(a < b, a, b)
     assert np.array_equal(exp.view(uint), sel.view(uint))
     assert np.array_equal(got, exp.view(uint))
+
+
+@pytest.mark.parametrize('dtname,npt', [('MPI_C_FLOAT_COMPLEX', np.float32),
+                                        ('MPI_C_DOUBLE_COMPLEX', np.float64),
+                                        ('MPI_COMPLEX', np.float32),
+                                        ('MPI_DOUBLE_COMPLEX', np.float64),
+                                        ('MPI_COMPLEX4', np.float16)])
+@pytest.mark.parametrize('opname', ['MPI_PROD', 'MPI_SUM'])
+def test_complex_specials_on_gpu(R, H, oracle, dtname, npt, opname):
+    """complex SUM / PROD on every pair of 21 special values (zeros of both
+    signs, infinities and NaNs in either component, overflow and subnormal
+    magnitudes): C `_Complex` products with the Annex G recovery of a
+    both-NaN result, struct complex without it (op_fns.c:61-91), SUM per
+    component; against the oracle under the sweep's rule (a NaN component
+    only has to be a NaN)"""
+    inf, nan = np.inf, np.nan
+    big = np.finfo(npt).max / 2
+    sub = np.finfo(npt).smallest_subnormal
+    z = [(0, 0), (-0.0, 0), (0, -0.0), (1, 0), (0, 1), (-1, -1), (inf, 0), (0, inf),
+         (-inf, 1), (1, -inf), (inf, inf), (nan, 0), (0, nan), (nan, nan), (inf, nan),
+         (nan, -inf), (big, big), (big, -big), (sub, sub), (3, -2), (0.5, 0.25)]
+    vals = np.array(z, npt).reshape(-1)
+    n = len(z)
+    a = np.repeat(vals.reshape(n, 2), n, axis=0).reshape(-1)
+    b = np.tile(vals.reshape(n, 2), (n, 1)).reshape(-1)
+    dt, op = getattr(H, dtname), getattr(H, opname)
+    da, db = dev(a), dev(b)
+    with np.errstate(all='ignore'):
+        assert R.MPI_Reduce_local(db, da, n * n, dt, op) == 0
+        exp = a.copy()
+        assert oracle.reduce_local(b.copy(), exp, n * n, dt, op) == 0
+    size = np.dtype(npt).itemsize
+    got = host(da)
+    assert compare(got, exp.view(np.uint8), 'cplx', size, opname, 2 * size) == 0
