@@ -1118,3 +1118,37 @@ def test_complex_specials_on_gpu(R, H, oracle, dtname, npt, opname):
     size = np.dtype(npt).itemsize
     got = host(da)
     assert compare(got, exp.view(np.uint8), 'cplx', size, opname, 2 * size) == 0
+
+
+@pytest.mark.parametrize('dtname', ['MPI_FLOAT_INT', 'MPI_2REAL', 'MPI_DOUBLE_INT',
+                                    'MPI_2DOUBLE_PRECISION', 'MPIR_2FLOAT16'])
+@pytest.mark.parametrize('opname', ['MPI_MAXLOC', 'MPI_MINLOC'])
+def test_loc_specials_on_gpu(R, H, oracle, dtname, opname):
+    """MAXLOC / MINLOC (op_fns.c:299-352) on every pair of special values:
+    a strict winner takes (value, loc), equal values (+0 and -0 included)
+    keep the smaller loc, a NaN on either side leaves inout unchanged;
+    padding bytes are inout's.  Bit-exact against the oracle"""
+    entry = next(s for s in SWEEP if s[0] == dtname and s[1] == opname)
+    vdt, ldt, ext, loff = entry[2][1:]
+    vals = np.array([0.0, -0.0, 1.0, -1.0, np.inf, -np.inf, np.nan, 2.0, 1.0, -np.nan],
+                    np.dtype(vdt))
+    nv = len(vals)
+    rng = np.random.default_rng(0x5EED0011)
+
+    def pack(v, locs):
+        buf = rng.integers(0, 256, len(v) * ext, dtype=np.uint8).reshape(len(v), ext)
+        buf[:, :np.dtype(vdt).itemsize] = v.view(np.uint8).reshape(len(v), -1)
+        buf[:, loff:loff + np.dtype(ldt).itemsize] = \
+            locs.astype(ldt).view(np.uint8).reshape(len(v), -1)
+        return buf.reshape(-1)
+
+    la = rng.integers(0, 4, nv * nv)
+    lb = rng.integers(0, 4, nv * nv)
+    a = pack(np.repeat(vals, nv), la)
+    b = pack(np.tile(vals, nv), lb)
+    dt, op = getattr(H, dtname), getattr(H, opname)
+    da, db = dev(a), dev(b)
+    assert R.MPI_Reduce_local(db, da, nv * nv, dt, op) == 0
+    exp = a.copy()
+    assert oracle.reduce_local(b.copy(), exp, nv * nv, dt, op) == 0
+    assert np.array_equal(host(da), exp)
