@@ -222,37 +222,85 @@ def allreduce_scalar(x, op, dev):
     return t.item()
 
 
+def host_topology():
+    """this process's CPUs grouped into physical cores (first SMT sibling of
+    each core kept), the sockets they sit on, and the cgroup CPU quota"""
+    aff = sorted(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') else \
+        list(range(os.cpu_count()))
+    cores, sockets = {}, set()
+    for c in aff:
+        base = '/sys/devices/system/cpu/cpu%d/topology/' % c
+        try:
+            pkg = int(open(base + 'physical_package_id').read())
+            core = int(open(base + 'core_id').read())
+        except (OSError, ValueError):
+            pkg, core = 0, c
+        sockets.add(pkg)
+        cores.setdefault((pkg, core), c)
+    # one thread per physical core, sockets interleaved so a prefix of the
+    # list spreads over both sockets' memory controllers
+    by_sock = {}
+    for (pkg, _), c in sorted(cores.items()):
+        by_sock.setdefault(pkg, []).append(c)
+    phys = []
+    for i in range(max(len(v) for v in by_sock.values())):
+        for pkg in sorted(by_sock):
+            if i < len(by_sock[pkg]):
+                phys.append(by_sock[pkg][i])
+    quota = None
+    try:
+        q, period = open('/sys/fs/cgroup/cpu.max').read().split()
+        quota = None if q == 'max' else round(int(q) / int(period), 2)
+    except (OSError, ValueError):
+        pass
+    model = ''
+    try:
+        for line in open('/proc/cpuinfo'):
+            if line.startswith('model name'):
+                model = line.split(':', 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return dict(affinity=aff, physical=phys, sockets=len(sockets), cgroup_cpu_quota=quota,
+                model=model)
+
+
 def cpu_baseline(seconds, count, crossover_rows):
     """The oracle (clean-room C restatement of MPICH's op_fns.c loop) on a
     bounded sample of the SAME workload: MPI_Reduce_local(MPI_SUM, MPI_FLOAT)
-    on `count`-element (1 GiB) host operands, repeated for ~seconds/2 on one
-    core (MPICH's path is one thread per rank) and ~seconds/2 on all cores
-    of this process's share.  BASELINE config 1 (16 MiB, cache-resident on
-    this host) is reported beside it, and one core's time per call at each
+    on `count`-element (1 GiB) host operands.  `value` is one core (MPICH's
+    path is one thread per rank); `allcores` runs one pinned thread per
+    physical core of this process's CPUs, every thread first-touching its own
+    slice (NUMA-local), and is read against a host triad (a += 0.5 b, the
+    combine's own traffic) on the same threads and layout.  BASELINE config 1
+    (16 MiB) is reported beside it, and one core's time per call at each
     host-crossover size (timed in C, like the GPU side) fills crossover_rows."""
     from oracle import oracle as orc
     orc.build()
-    ncores = len(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') else os.cpu_count()
-    threads_all = max(1, min(16, ncores))
+    topo = host_topology()
+    phys = topo['physical']
+    alg = 3 * count * 4
 
-    def leg(n, nth, budget):
-        rng = np.random.default_rng(0x5EED0001)
-        a = rng.uniform(-1, 1, n).astype(np.float32)
-        b = rng.uniform(-1, 1, n).astype(np.float32)
-        t_list = []
-        t_end = time.perf_counter() + budget
-        while time.perf_counter() < t_end or len(t_list) < 3:
-            t0 = orc.wtime()
-            orc.reduce_local(b, a, n, H.MPI_FLOAT, H.MPI_SUM, nthreads=nth)
-            t_list.append(orc.wtime() - t0)
-        t_list.sort()
-        med = t_list[len(t_list) // 2]
-        return dict(gibs=round(3 * n * 4 / GIB / med, 3), best=round(3 * n * 4 / GIB / t_list[0], 3),
-                    reps=len(t_list), threads=nth)
+    def reduce_leg(cpus, budget, n=count):
+        best, med, passes = orc.bench_reduce(n, H.MPI_FLOAT, H.MPI_SUM, cpus, budget)
+        return dict(gibs=round(3 * n * 4 / GIB / med, 3), best=round(3 * n * 4 / GIB / best, 3),
+                    reps=passes, threads=len(cpus))
 
-    one = leg(count, 1, seconds * 0.4)
-    allc = leg(count, threads_all, seconds * 0.3)
-    c1 = leg(4194304, 1, seconds * 0.15)
+    def triad_leg(cpus, budget):
+        best, med, passes = orc.bench_triad(count, cpus, budget)
+        return dict(gibs=round(alg / GIB / med, 3), best=round(alg / GIB / best, 3), reps=passes,
+                    threads=len(cpus))
+
+    one = reduce_leg(phys[:1], seconds * 0.25)
+    allc = reduce_leg(phys, seconds * 0.15)
+    tri_all = triad_leg(phys, seconds * 0.15)
+    tri_one = triad_leg(phys[:1], seconds * 0.1)
+    c1 = reduce_leg(phys[:1], seconds * 0.1, n=4194304)
+    scaling = []
+    for k in (8, 16, 32, 64):
+        if k < len(phys):
+            scaling.append(dict(threads=k, reduce_gibs=reduce_leg(phys[:k], seconds * 0.03)['gibs'],
+                                triad_gibs=triad_leg(phys[:k], seconds * 0.03)['gibs']))
     if crossover_rows:
         B = bench_lib()
         fn = ctypes.cast(orc.lib().oracle_reduce_local, ctypes.c_void_p).value
@@ -263,26 +311,28 @@ def cpu_baseline(seconds, count, crossover_rows):
             b = rng.uniform(-1, 1, n).astype(np.float32)
             r['cpu_1core_us'] = round(c_call_median_us(B, fn, a.ctypes.data, b.ctypes.data, n,
                                                        _reps_for(r['bytes'])), 2)
-    model = ''
-    try:
-        for line in open('/proc/cpuinfo'):
-            if line.startswith('model name'):
-                model = line.split(':', 1)[1].strip()
-                break
-    except OSError:
-        pass
     return dict(
         value=one['gibs'], unit='GiB/s', cores=1, kind='port',
         sample='same workload (MPI_Reduce_local MPI_SUM MPI_FLOAT, %d elements = %d MiB per '
-               'operand, host-resident) through oracle/redop_oracle.c, 1 thread, %d calls, median'
-               % (count, count * 4 >> 20, one['reps']),
+               'operand, host-resident) through oracle/redop_oracle.c, 1 pinned thread, %d calls, '
+               'median' % (count, count * 4 >> 20, one['reps']),
         best=one['best'],
-        allcores=dict(value=allc['gibs'], threads=threads_all, reps=allc['reps'],
-                      note='disjoint slices, one thread per core of this process share'),
+        frac_of_host_triad_1core=round(one['gibs'] / tri_one['gibs'], 4),
+        allcores=dict(value=allc['gibs'], threads=allc['threads'], reps=allc['reps'],
+                      host_triad_gibs=tri_all['gibs'],
+                      frac_of_host_triad=round(allc['gibs'] / tri_all['gibs'], 4),
+                      note='one pinned thread per physical core of this process (%d sockets), '
+                           'each first-touching its own slice of both operands (NUMA-local); '
+                           'host triad = a += 0.5 b on the same threads and layout (12 B per '
+                           'element, the combine\'s own traffic)' % topo['sockets']),
+        host_triad_1core_gibs=tri_one['gibs'],
+        thread_scaling=scaling,
         config1_16MiB_1core=dict(value=c1['gibs'], reps=c1['reps'],
                                  note='BASELINE config 1; 48 MiB per call is cache-resident on '
                                       'this host'),
-        host_cpu=model, nproc=os.cpu_count(), affinity_cpus=ncores)
+        host_cpu=topo['model'], nproc=os.cpu_count(), affinity_cpus=len(topo['affinity']),
+        physical_cores=len(phys), sockets=topo['sockets'],
+        cgroup_cpu_quota=topo['cgroup_cpu_quota'])
 
 
 def load_pmc(path, count):
@@ -396,7 +446,7 @@ def single_gpu(args, dev):
             B, inb, inout, n, stream,
             (64 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20, 64 << 20) if args.sweep
             else (64 << 10, 1 << 20, 16 << 20))
-        end_to_end(result, n)
+        end_to_end(result, n, dev)
         crossover = host_crossover_gpu(B)
         result['configs_3_and_5'] = other_configs(inb, inout, n, stream)
     if args.sweep:
@@ -471,14 +521,69 @@ def other_configs(inb, inout, n, stream):
                                                    4)))
 
 
-def end_to_end(result, n):
+def pcie_rates(hin, hio, dev, reps=3):
+    """measured PCIe rates between this GPU and page-locked host memory
+    (hipMemcpyAsync through torch copies, 1 GiB each): H2D alone, D2H alone,
+    and the zero-copy call's own pattern -- `in` and `inout` in (2 x H2D)
+    while the result goes out (1 x D2H) at the same time, on two streams.
+    That pattern's time is the PCIe floor of a host-resident call."""
+    n = hin.numel()
+    d0 = torch.empty(n, dtype=torch.float32, device=dev)
+    d1 = torch.empty(n, dtype=torch.float32, device=dev)
+    s_in, s_out = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    torch.cuda.synchronize()
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        best = None
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            t = time.perf_counter() - t0
+            best = t if best is None else min(best, t)
+        return best
+
+    def h2d():
+        with torch.cuda.stream(s_in):
+            d0.copy_(hin, non_blocking=True)
+
+    def d2h():
+        with torch.cuda.stream(s_out):
+            hio.copy_(d1, non_blocking=True)
+
+    def pattern():
+        with torch.cuda.stream(s_in):
+            d0.copy_(hin, non_blocking=True)
+            d0.copy_(hin, non_blocking=True)
+        with torch.cuda.stream(s_out):
+            hio.copy_(d1, non_blocking=True)
+    nb = 4 * n
+    t_h2d, t_d2h = timed(h2d), timed(d2h)
+    d1.copy_(hio)           # the operands keep their values for the timed calls
+    torch.cuda.synchronize()
+    t_pat = timed(pattern)
+    with torch.no_grad():
+        hio.copy_(d1)
+    del d0, d1
+    return dict(h2d_GBs=round(nb / t_h2d / 1e9, 2), d2h_GBs=round(nb / t_d2h / 1e9, 2),
+                pattern_2h2d_1d2h_ms=round(t_pat * 1e3, 2),
+                pattern_GiBs=round(3 * nb / t_pat / GIB, 2),
+                note='page-locked host <-> HBM, 1 GiB per copy, best of %d; pattern = the '
+                     'host-resident call\'s 2 GiB in + 1 GiB out at once' % reps), t_pat
+
+
+def end_to_end(result, n, dev=None):
     """host-resident end to end (never `value`): pinned operands read and
     written by the kernel over PCIe; pageable operands through the host
-    workers and through hipMemcpyAsync staging"""
+    workers and through hipMemcpyAsync staging; each against the measured
+    PCIe floor of the same traffic"""
     hin = torch.empty(n, dtype=torch.float32).pin_memory()
     hio = torch.empty(n, dtype=torch.float32).pin_memory()
     hin.uniform_(-1, 1)
     hio.uniform_(-1, 1)
+    pcie, t_floor = pcie_rates(hin, hio, dev if dev is not None else torch.device('cuda', 0))
     redop.check(redop.MPI_Reduce_local(hin, hio, n, H.MPI_FLOAT, H.MPI_SUM))
     reps = 3
     t0 = time.perf_counter()
@@ -487,8 +592,11 @@ def end_to_end(result, n):
     te = (time.perf_counter() - t0) / reps
     result['end_to_end_host'] = dict(gibs=round(3 * n * 4 / GIB / te, 2),
                                      ms_per_call=round(te * 1e3, 2),
+                                     frac_of_pcie=round(t_floor / te, 4), pcie=pcie,
                                      note='pinned host buffers: the kernel reads and writes '
-                                          'them over PCIe (zero-copy); never `value`')
+                                          'them over PCIe (zero-copy); never `value`; '
+                                          'frac_of_pcie = measured PCIe floor of the same '
+                                          'traffic / call time')
     del hin, hio
     pin_ = np.random.default_rng(0x5EED0007).random(n, dtype=np.float32)
     pio_ = np.random.default_rng(0x5EED0008).random(n, dtype=np.float32)
@@ -502,7 +610,8 @@ def end_to_end(result, n):
             for _ in range(reps):
                 redop.check(redop.MPI_Reduce_local(pin_, pio_, n, H.MPI_FLOAT, H.MPI_SUM))
             tp = (time.perf_counter() - t0) / reps
-            pg[label] = dict(gibs=round(3 * n * 4 / GIB / tp, 2), ms_per_call=round(tp * 1e3, 2))
+            pg[label] = dict(gibs=round(3 * n * 4 / GIB / tp, 2), ms_per_call=round(tp * 1e3, 2),
+                             frac_of_pcie=round(t_floor / tp, 4))
     finally:
         redop.check(redop.set_pageable(prev['threads'], prev['chunk_bytes']))
     pg['workers_x_chunk'] = '%d x %d MiB' % (prev['threads'] or 8, prev['chunk_bytes'] >> 20)
@@ -548,6 +657,22 @@ def size_sweep(inb, inout, n, stream, nbytes_alg):
 
 
 # ------------------------------------------------------------------ N > 1
+def schedule_ran(cc, requested, kind='rs'):
+    """which schedule the last collective on communicator `cc` actually ran
+    (MPIX_Comm_get_state): a requested pull whose windows failed verification
+    on some rank, or a shape a variant does not cover, runs the schedule with
+    the same bits instead -- its time must never be reported under the
+    requested name.  Returns the fields a leg carries; 'error' is set when
+    the requested schedule did not run (the leg is then not timed)."""
+    st = cc.state()
+    ran = st['last_rs'] if kind == 'rs' else st['last_allreduce']
+    out = dict(schedule_requested=requested, schedule_ran=ran,
+               window_retries=st['window_retries'], pulls_enabled=st['pulls_enabled'])
+    if ran != requested:
+        out['error'] = 'fell back to %s' % ran
+    return out
+
+
 def rh_expected_block(sends, rank, recvcount):
     """rank's block of MPI_Reduce_scatter_block by recursive halving, as the
     reference schedule associates it (…recursive_halving.c:110-229): the
@@ -605,6 +730,9 @@ def multi_gpu(args, world, rank, dev):
     dr = torch.empty(rc_small, dtype=torch.float32, device=dev)
     redop.check(ccl.reduce_scatter_block(ds, dr, rc_small, H.MPI_FLOAT, H.MPI_SUM, cc,
                                          'recursive_halving'), 'MPIX_Reduce_scatter_block')
+    sched = schedule_ran(cc, 'recursive_halving')
+    if 'error' in sched:
+        raise RuntimeError('value leg: recursive halving requested, ' + sched['error'])
     got = dr.cpu().numpy()
     ok = got.tobytes() == rh_expected_block(sends, rank, rc_small).tobytes()
     ok_all = allreduce_scalar(1.0 if ok else 0.0, dist.ReduceOp.MIN, dev) == 1.0
@@ -659,6 +787,7 @@ def multi_gpu(args, world, rank, dev):
                 'parallelism': 'rsb%d (one rank per GPU, libmpix_coll over RCCL)' % world},
         parity=dict(checked=True, recvcount=rc_small, bit_exact_all_ranks=True,
                     against='numpy restatement of the recursive-halving association'),
+        schedule_ran=sched['schedule_ran'],
         roofline={'bound': 'hbm', 'unit': 'GB/s',
                   'achieved': round(comb_gbs, 1) if comb_gbs else None, 'peak': HBM_PEAK_GBS,
                   'frac': round(comb_gbs / HBM_PEAK_GBS, 4) if comb_gbs else None,
@@ -718,6 +847,10 @@ def rsb_secondary(args, world, rank, dev, out):
         torch.cuda.synchronize()        # inputs ready before the communicator's stream reads them
         redop.check(ccl.reduce_scatter_block(blk, o, rc_small, H.MPI_INT, H.MPI_SUM, cc, algo),
                     'MPIX_Reduce_scatter_block')
+        sched = schedule_ran(cc, algo)
+        if 'error' in sched:        # every rank agrees on a fallback: nobody times this leg
+            out[name] = sched
+            continue
         ok = allreduce_scalar(1 if bool(torch.all(o == world * rank + world * (world - 1) // 2))
                               else 0, dist.ReduceOp.MIN, dev)
         if not ok:
@@ -726,7 +859,11 @@ def rsb_secondary(args, world, rank, dev, out):
         def once():
             redop.check(ccl.reduce_scatter_block(src, recv, recvcount, H.MPI_FLOAT, H.MPI_SUM, cc,
                                                  algo), 'MPIX_Reduce_scatter_block')
-        once()
+        once()                          # at the timed size: the pull windows grow here
+        sched = schedule_ran(cc, algo)
+        if 'error' in sched:
+            out[name] = sched
+            continue
         bits = None
         if name == 'pairwise':
             refs['pairwise'] = recv.clone()
@@ -760,7 +897,8 @@ def rsb_secondary(args, world, rank, dev, out):
         torch.cuda.synchronize()
         cc.set_step_timing(False)
         steps = cc.step_times()
-        out[name] = dict(parity_redscatblk3_all_ranks=True, ms=round(t * 1e3, 3),
+        sched = schedule_ran(cc, algo)      # the timed calls ran it too
+        out[name] = dict(sched, parity_redscatblk3_all_ranks=True, ms=round(t * 1e3, 3),
                          bit_identical_to=bits, steps_rank0=steps,
                          busbw_GBs=round((world - 1) / world * total * 4 / t / 1e9, 2),
                          per_link_GBs=round(link_bytes / t / 1e9, 2), links_active=links,
@@ -795,6 +933,8 @@ def allreduce_secondary(args, world, rank, dev, res):
     torch.cuda.synchronize()
     res.update(parity_allred_sum_test_1_all_ranks=True, bytes_per_rank=n * 4, P=world)
     sh_in = sh_out = None
+    asked = {'c_reduce_scatter_allgather': 'reduce_scatter_allgather',
+             'c_rsag_multipath': 'rsag_multipath', 'c_pull': 'pull', 'c_pull_shared': 'pull'}
     for name, fn in (('c_reduce_scatter_allgather',
                       lambda: redop.check(ccl.allreduce(send, recv, n, H.MPI_FLOAT, H.MPI_SUM, cc,
                                                         'reduce_scatter_allgather', workspace=ws),
@@ -818,6 +958,10 @@ def allreduce_secondary(args, world, rank, dev, res):
             sh_in.copy_(send)
             torch.cuda.synchronize()
         fn()
+        sched = schedule_ran(cc, asked[name], 'ar') if name in asked else {}
+        if 'error' in sched:
+            res[name] = sched
+            continue
         if name == 'c_reduce_scatter_allgather':
             ref = recv.clone()
         elif name in ('c_rsag_multipath', 'c_pull', 'c_pull_shared'):  # same association
@@ -835,7 +979,9 @@ def allreduce_secondary(args, world, rank, dev, res):
         torch.cuda.synchronize()
         dist.barrier()
         t = allreduce_scalar((time.perf_counter() - t0) / reps, dist.ReduceOp.MAX, dev)
-        res[name] = dict(ms=round(t * 1e3, 3),
+        if name in asked:
+            sched = schedule_ran(cc, asked[name], 'ar')
+        res[name] = dict(sched, ms=round(t * 1e3, 3),
                          busbw_GBs=round(2 * (world - 1) / world * n * 4 / t / 1e9, 2))
     if sh_in is not None:
         cc.free_shared(sh_in.data_ptr())

@@ -280,6 +280,19 @@ int MPIX_Comm_free_shared(MPIX_Comm comm, void *ptr);
  * and the label of the step that ended at each (`labels` may be NULL; each
  * label at most 32 bytes with its NUL) and clears the record.  Device
  * communicators only. */
+/* Which schedule actually ran -- an explicitly requested algorithm may not be
+ * able to run (a pull whose windows failed verification on some rank, a
+ * device pair without peer access, MULTIPATH on a shape it does not cover), in
+ * which case the schedule with the same bits runs instead; this is how a
+ * caller tells.  pulls_enabled: 1 while the pull schedules can run on this
+ * communicator; last_rs_algorithm / last_allreduce_algorithm: the MPIX_RSB_* /
+ * MPIX_ALLREDUCE_* value of the schedule the last reduce-scatter / allreduce
+ * ran (AUTO resolved; -1 before the first); window_retries: pull-window
+ * verification attempts that failed so far; fallbacks: calls whose requested
+ * schedule did not run.  Any pointer may be NULL.  Local, not collective. */
+int MPIX_Comm_get_state(MPIX_Comm comm, int *pulls_enabled, int *last_rs_algorithm,
+                        int *last_allreduce_algorithm, int *window_retries, int *fallbacks);
+
 int MPIX_Comm_set_step_timing(MPIX_Comm comm, int enable);
 int MPIX_Comm_step_times(MPIX_Comm comm, double *ms, char (*labels)[32], int max, int *n);
 

@@ -261,6 +261,19 @@ int MPIX_Ipc_export(const void *devptr, void *handle_out, MPIX_Aint *offset_out)
 int MPIX_Ipc_open(const void *handle, void **base_out);
 int MPIX_Ipc_close(void *base);
 
+/* ---- operands on two devices ----
+ * 1 if kernels on `device` can dereference memory of `peer_device` (same
+ * device, or peer access enabled -- by this call at the pair's first use,
+ * once per process), else 0.  Replaces the all-pairs loop of the reference's
+ * HIP init hook (yaksa/src/backend/hip/hooks/yaksuri_hip_init_hooks.c:164-181:
+ * hipDeviceCanAccessPeer, hipDeviceEnablePeerAccess, "already enabled"
+ * tolerated).  Every entry point settles its pairs itself: MPIX_Reduce_local
+ * runs on inout's device and, without peer access, copies `in` over with
+ * hipMemcpyPeerAsync; the stream-ordered entry points return MPI_ERR_BUFFER
+ * for an operand the stream's device cannot reach.  Env MPIX_REDOP_PEER=stage
+ * treats every pair of distinct devices as unreachable. */
+int MPIX_Redop_peer_access(int device, int peer_device);
+
 /* 1 if (op, datatype) goes to the GPU path, else 0 -- the contract of
  * MPIR_Typerep_reduce_is_supported (typerep_yaksa_pack.c:227-271), which
  * reduce_local.c:68 (count 0) and maint/gen_coll.py:546-547 (count of the
@@ -270,6 +283,11 @@ int MPIX_Ipc_close(void *base);
  * -1 = no limit, as MPIR_CVAR_YAKSA_REDUCTION_THRESHOLD), or when no kernel
  * covers the pair.  When 0, a caller keeps its own CPU op table. */
 int MPIX_Redop_is_supported(MPIX_Op op, MPIX_Aint count, MPIX_Datatype datatype);
+
+/* 1 if a GPU kernel covers (op, datatype), whatever the knobs above say (the
+ * collectives of libmpix_coll decline a pair only when this is 0, so
+ * MPIX_REDOP_ENABLE=0 never turns them off). */
+int MPIX_Redop_has_gpu_path(MPIX_Op op, MPIX_Datatype datatype);
 
 /* The same predicate with the operands in view, for reduce_local.c's branch:
  * additionally 0 when BOTH buffers are host-resident and one operand holds

@@ -71,6 +71,7 @@ def lib():
             'MPIX_Comm_alloc_shared': ([vp, sz, ctypes.POINTER(vp)], i32),
             'MPIX_Comm_free_shared': ([vp, vp], i32),
             'MPIX_Comm_set_step_timing': ([vp, i32], i32),
+            'MPIX_Comm_get_state': ([vp] + [ctypes.POINTER(i32)] * 5, i32),
             'MPIX_Comm_step_times': ([vp, ctypes.POINTER(ctypes.c_double), vp, i32,
                                       ctypes.POINTER(i32)], i32),
             'MPIX_Comm_rank': ([vp, ctypes.POINTER(i32)], i32),
@@ -192,6 +193,20 @@ class Comm:
         raw = labels.raw
         return [dict(phase=raw[32 * k:32 * (k + 1)].split(b'\0', 1)[0].decode(),
                      ms=round(ms[k], 4)) for k in range(n.value)]
+
+    def state(self):
+        """MPIX_Comm_get_state: which schedule the last collectives actually
+        ran (names from RSB_ALGORITHMS / AR_ALGORITHMS, None before the
+        first), whether the pulls can run, failed window verifications and
+        calls whose requested schedule did not run"""
+        v = [ctypes.c_int() for _ in range(5)]
+        redop.check(lib().MPIX_Comm_get_state(self.h, *[ctypes.byref(x) for x in v]),
+                    'MPIX_Comm_get_state')
+        rs_names = {n: k for k, n in RSB_ALGORITHMS.items()}
+        ar_names = {n: k for k, n in AR_ALGORITHMS.items()}
+        return dict(pulls_enabled=bool(v[0].value), last_rs=rs_names.get(v[1].value),
+                    last_allreduce=ar_names.get(v[2].value), window_retries=v[3].value,
+                    fallbacks=v[4].value)
 
     def free(self):
         if self.h:

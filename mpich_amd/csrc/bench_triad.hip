@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <time.h>
 #include <vector>
 
 typedef float f4 __attribute__((ext_vector_type(4)));
@@ -93,6 +94,32 @@ extern "C" int mpix_bench_call_loop(void *fn, const void *in, void *io, int64_t 
     }
     auto b = std::chrono::steady_clock::now();
     *total_s = std::chrono::duration<double>(b - a).count();
+    return 0;
+}
+
+// The same loop with every call's host entry and return stamped (CLOCK_MONOTONIC
+// and CLOCK_BOOTTIME ns, t[4*i + 0..3] = mono in, mono out, boot in, boot out),
+// to line the calls up with a rocprofv3 kernel trace (tools/sync_gap.py)
+extern "C" int mpix_bench_call_loop_ts(void *fn, const void *in, void *io, int64_t count, int dt,
+                                       int op, int reps, uint64_t *t)
+{
+    if (!fn || reps < 0 || !t)
+        return 12;
+    sync_reduce_fn f = (sync_reduce_fn) fn;
+    auto ns = [](clockid_t c) {
+        struct timespec ts;
+        clock_gettime(c, &ts);
+        return (uint64_t) ts.tv_sec * 1000000000ull + (uint64_t) ts.tv_nsec;
+    };
+    for (int i = 0; i < reps; ++i) {
+        t[4 * i + 0] = ns(CLOCK_MONOTONIC);
+        t[4 * i + 2] = ns(CLOCK_BOOTTIME);
+        int rc = f(in, io, count, dt, op);
+        t[4 * i + 1] = ns(CLOCK_MONOTONIC);
+        t[4 * i + 3] = ns(CLOCK_BOOTTIME);
+        if (rc)
+            return rc;
+    }
     return 0;
 }
 

@@ -24,6 +24,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include <chrono>
 #include <condition_variable>
@@ -63,6 +64,7 @@ struct Local {
     int size = 0;
     bool host = false;
     std::vector<int> devices;
+    bool peer_ok = true;    // every rank's device can read every other's (pulls allowed)
     std::mutex m;
     std::condition_variable cv;
     std::map<std::tuple<int, int, uint64_t>, Slot> slots;
@@ -109,6 +111,12 @@ struct MPIX_Comm_s {
     std::vector<char *> win_old;       // outgrown / rejected windows, freed with the comm
     std::vector<void *> peer_map;      // peers' pull windows, mapped and verified
     bool win_broken = false;           // pulls given up on this communicator
+    // what actually ran (MPIX_Comm_get_state): the schedule of the last
+    // reduce-scatter / allreduce after AUTO and any fallback, the calls whose
+    // requested schedule did not run, window verification attempts that failed
+    int last_rs = -1, last_ar = -1;
+    int fallbacks = 0, win_retries = 0;
+    int same_node = -1;                // every rank on this host (IPC possible): -1 not yet asked
     struct Nonce { int rank, attempt; uint64_t n0, n1; };
     std::vector<Nonce> nonce_hist;     // every window nonce published (MPIX_COLL_TRACE)
     struct Shared {                    // MPIX_Comm_alloc_shared windows
@@ -120,11 +128,27 @@ struct MPIX_Comm_s {
     bool timing = false;               // MPIX_Comm_set_step_timing
     std::vector<std::pair<std::string, hipEvent_t>> marks;
     bool host() const { return kind == K_LOCAL_HOST || (kind == K_CUSTOM && device < 0); }
+    // threads driving several devices pull from each other's buffers only with
+    // peer access between every pair of them (else the pull schedules run
+    // their transport form, same bits); processes decide by their windows
+    bool pulls_possible() const { return !(kind == K_LOCAL_DEV && local && !local->peer_ok); }
 };
 
 namespace {
 
 int hip_fail(hipError_t e) { return e == hipSuccess ? MPIX_REDOP_SUCCESS : MPIX_REDOP_ERR_OTHER; }
+
+// A requested schedule that could not run: record what runs instead, so the
+// caller can tell (MPIX_Comm_get_state) -- never one schedule's time under
+// another's name.  Printed under MPIX_COLL_TRACE.
+void ran_instead(MPIX_Comm c, int *last, int alg)
+{
+    ++c->fallbacks;
+    *last = alg;
+    if (getenv("MPIX_COLL_TRACE"))
+        fprintf(stderr, "[mpix_coll rank %d] requested schedule did not run: schedule %d instead\n",
+                c->rank, alg);
+}
 
 #define TRY(x) do { int rc_ = (x); if (rc_ != MPIX_REDOP_SUCCESS) return rc_; } while (0)
 #define HTRY(x) do { if ((x) != hipSuccess) return MPIX_REDOP_ERR_OTHER; } while (0)
@@ -595,8 +619,12 @@ int check_args(MPIX_Comm c, const void *recvbuf, MPIX_Aint count, MPIX_Datatype 
     // at its first combine, mid-schedule, with peers still posted to this
     // rank: decline it here, before any exchange, so every rank returns the
     // same error (the reference computes these on the CPU, which the caller
-    // keeps for them).  A custom combine takes whatever it is given.
-    if (!c->combine && !MPIX_Redop_is_supported(op, 0, dt))
+    // keeps for them).  A custom combine takes whatever it is given.  The
+    // test is the knob-independent one: MPIX_REDOP_ENABLE / _THRESHOLD steer
+    // MPIX_Redop_is_supported's callers (reduce_local.c's branch), not the
+    // collectives, as MPIR_CVAR_ENABLE_YAKSA_REDUCTION only moves reductions
+    // back to the CPU
+    if (!c->combine && !MPIX_Redop_has_gpu_path(op, dt))
         return MPIX_REDOP_ERR_TYPE;
     if (!recvbuf && count)
         return MPIX_REDOP_ERR_BUFFER;
@@ -682,12 +710,19 @@ int rs_recursive_halving(const char *sb, char *rb, const std::vector<size_t> &cn
                              rcv(dst, tmp_recvbuf + newdisps[recv_idx] * ext, recv_cnt * ext)}, s));
             TRY(mark(c, "exchange", s));
             char *out = tmp_results + newdisps[recv_idx] * ext;
-            if (direct && mask == 1 && recv_idx == newrank) {
-                out = rb;           // the last step's half is this rank's block
+            const char *own = cur + newdisps[recv_idx] * ext;
+            const size_t nbytes = recv_cnt * ext;
+            // the last step's half is this rank's block: written straight into
+            // recvbuf, unless that would overwrite the half being read -- with
+            // MPI_IN_PLACE at P = 2 the first step is the last and reads
+            // recvbuf itself ([disps[1], +c1) against [0, c1) at rank 1)
+            if (direct && mask == 1 && recv_idx == newrank &&
+                (own == rb || own + nbytes <= rb || rb + nbytes <= own)) {
+                out = rb;
                 in_rb = true;
             }
-            TRY(combine_to(c, cur + newdisps[recv_idx] * ext, tmp_recvbuf + newdisps[recv_idx] * ext,
-                           out, (MPIX_Aint) recv_cnt, dt, op, s, ext));
+            TRY(combine_to(c, own, tmp_recvbuf + newdisps[recv_idx] * ext, out,
+                           (MPIX_Aint) recv_cnt, dt, op, s, ext));
             TRY(mark(c, "combine", s));
             send_idx = recv_idx;
             last_idx = recv_idx + mask;
@@ -1055,6 +1090,32 @@ int verified_window(MPIX_Comm c, size_t bytes, hipStream_t s, char **w_out,
                     std::vector<void *> *maps)
 {
     *w_out = nullptr;
+    // IPC handles open only on the exporter's node: a communicator spanning
+    // nodes would allocate three message-size windows per attempt before
+    // giving up.  One record exchange, once per communicator, settles it
+    // first: the kernel's boot id and the host name must match on every rank.
+    if (c->same_node < 0) {
+        char me[kRec];
+        memset(me, 0, sizeof me);
+        if (FILE *f = fopen("/proc/sys/kernel/random/boot_id", "r")) {
+            if (!fgets(me, 64, f))
+                me[0] = 0;
+            fclose(f);
+        }
+        (void) gethostname(me + 64, 128);
+        if (const char *id = getenv("MPIX_COLL_NODE_ID"))    // test hook: pretend another node
+            snprintf(me + 192, 64, "%s", id);
+        std::vector<char> all;
+        TRY(allgather_records(c, me, sizeof me, &all, s));
+        c->same_node = 1;
+        for (int q = 0; q < c->size; ++q)
+            if (memcmp(all.data() + kRec * (size_t) q, me, sizeof me) != 0)
+                c->same_node = 0;
+        if (!c->same_node && coll_trace())
+            fprintf(stderr, "[mpix_coll rank %d] peers on other nodes: no pull windows\n", c->rank);
+    }
+    if (!c->same_node)
+        return MPIX_REDOP_SUCCESS;
     std::random_device rd;
     for (int attempt = 0; attempt < 3; ++attempt) {
         void *w = nullptr;
@@ -1170,6 +1231,7 @@ int verified_window(MPIX_Comm c, size_t bytes, hipStream_t s, char **w_out,
             return MPIX_REDOP_SUCCESS;
         }
         close_maps(maps);
+        ++c->win_retries;
         if (w)
             c->win_old.push_back(static_cast<char *>(w));     // never reused, see above
     }
@@ -1297,6 +1359,7 @@ int rs_pull(const char *sb, char *rb, const std::vector<size_t> &cnts, MPIX_Data
         total += n;
     auto fallback = [&]() -> int {     // same bits: one-group pairwise / recursive halving
         const int alg = tree ? MPIX_RSB_RECURSIVE_HALVING : MPIX_RSB_PAIRWISE;
+        ran_instead(c, &c->last_rs, alg);
         char *w;
         TRY(workspace(c, nullptr, 0, rs_workspace(total, cnts[rank], ext, size, alg), s, &w));
         return release_scratch(c, w,
@@ -1304,7 +1367,7 @@ int rs_pull(const char *sb, char *rb, const std::vector<size_t> &cnts, MPIX_Data
                                     : rs_pairwise(sb, rb, cnts, dt, op, c, w, s, ext, true),
                                s);
     };
-    if (c->host() || c->combine || size > 16)
+    if (c->host() || c->combine || size > 16 || !c->pulls_possible())
         return fallback();
     const size_t blk = cnts[rank] * ext;
     const bool in_place = sb == rb;
@@ -1596,6 +1659,7 @@ int allreduce_pull(const char *sendbuf, char *rb, size_t count, MPIX_Datatype dt
     const int rank = c->rank, size = c->size;
     const size_t nb = count * ext;
     auto fallback = [&]() -> int {
+        ran_instead(c, &c->last_ar, MPIX_ALLREDUCE_REDUCE_SCATTER_ALLGATHER);
         if (sendbuf)
             TRY(copy(c, rb, sendbuf, nb, s));
         char *tmp;
@@ -1603,7 +1667,7 @@ int allreduce_pull(const char *sendbuf, char *rb, size_t count, MPIX_Datatype dt
         return release_scratch(c, tmp, allreduce_rsag(rb, count, dt, op, c, tmp, s, ext, true,
                                                       false), s);
     };
-    if (c->host() || c->combine || size > 16)
+    if (c->host() || c->combine || size > 16 || !c->pulls_possible())
         return fallback();
     const char *in = sendbuf ? sendbuf : rb;
     // the reference's layout (:85-127): P - pof2 even/odd pairs fold first (the
@@ -2079,10 +2143,11 @@ int rs_entry(const void *sendbuf, void *recvbuf, const std::vector<size_t> &cnts
     char *rb = static_cast<char *>(recvbuf);
     const char *sb = sendbuf ? static_cast<const char *>(sendbuf) : rb;
     int algo = rs_choose(algorithm, total * ext);
+    c->last_rs = algo;
     if (algo == MPIX_RSB_RECURSIVE_HALVING_MULTIPATH && !multipath_shape(cnts, c->size))
-        algo = MPIX_RSB_RECURSIVE_HALVING;
+        ran_instead(c, &c->last_rs, algo = MPIX_RSB_RECURSIVE_HALVING);
     if (algo == MPIX_RSB_RECURSIVE_HALVING_PULL && c->size > 16)
-        algo = MPIX_RSB_RECURSIVE_HALVING;
+        ran_instead(c, &c->last_rs, algo = MPIX_RSB_RECURSIVE_HALVING);
     if (c->size == 1)
         return finish(c, sendbuf ? copy(c, rb, sb, cnts[0] * ext, s) : MPIX_REDOP_SUCCESS, s,
                       blocking);
@@ -2154,6 +2219,10 @@ int allreduce_entry(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Da
         return MPIX_REDOP_ERR_COUNT;    // :127
     if (algorithm != MPIX_ALLREDUCE_RECURSIVE_DOUBLING && splits_message_forbidden(op))
         return MPIX_REDOP_ERR_OP;       // MPIR_Allreduce_equal uses recursive doubling only
+    c->last_ar = algorithm;
+    if (algorithm == MPIX_ALLREDUCE_RSAG_MULTIPATH && c->size > 1 &&
+        !(c->size >= 4 && !(c->size & (c->size - 1)) && (size_t) count % (size_t) pof2 == 0))
+        ran_instead(c, &c->last_ar, MPIX_ALLREDUCE_REDUCE_SCATTER_ALLGATHER);
     if (algorithm == MPIX_ALLREDUCE_PULL && c->size > 1)
         return finish(c, allreduce_pull(static_cast<const char *>(sendbuf), rb, (size_t) count, dt,
                                         op, c, ws, ws_bytes, s, ext),
@@ -2243,8 +2312,18 @@ int MPIX_Comm_create_local(int size, const int *devices, MPIX_Comm *comms)
     auto L = std::make_shared<Local>();
     L->size = size;
     L->host = devices == nullptr;
-    if (devices)
+    if (devices) {
         L->devices.assign(devices, devices + size);
+        // ranks on distinct devices read each other's buffers in the pull
+        // schedules: peer access for every ordered pair, as the reference's
+        // HIP init hook enables it (yaksuri_hip_init_hooks.c:164-181).
+        // Without it the pulls run their transport form (same bits) and the
+        // exchanges are runtime-staged device-to-device copies.
+        for (int a = 0; a < size; ++a)
+            for (int b = 0; b < size; ++b)
+                if (devices[a] != devices[b] && !MPIX_Redop_peer_access(devices[a], devices[b]))
+                    L->peer_ok = false;
+    }
     for (int r = 0; r < size; ++r) {
         MPIX_Comm c = new_comm(r, size, L->host ? K_LOCAL_HOST : K_LOCAL_DEV);
         c->local = L;
@@ -2354,6 +2433,25 @@ int MPIX_Comm_free_shared(MPIX_Comm comm, void *ptr)
         return MPIX_REDOP_SUCCESS;
     }
     return MPIX_REDOP_ERR_BUFFER;
+}
+
+int MPIX_Comm_get_state(MPIX_Comm comm, int *pulls_enabled, int *last_rs_algorithm,
+                        int *last_allreduce_algorithm, int *window_retries, int *fallbacks)
+{
+    if (!comm)
+        return MPIX_REDOP_ERR_ARG;
+    if (pulls_enabled)
+        *pulls_enabled = !comm->host() && !comm->combine && comm->size <= 16 &&
+                         !comm->win_broken && comm->pulls_possible();
+    if (last_rs_algorithm)
+        *last_rs_algorithm = comm->last_rs;
+    if (last_allreduce_algorithm)
+        *last_allreduce_algorithm = comm->last_ar;
+    if (window_retries)
+        *window_retries = comm->win_retries;
+    if (fallbacks)
+        *fallbacks = comm->fallbacks;
+    return MPIX_REDOP_SUCCESS;
 }
 
 int MPIX_Comm_set_step_timing(MPIX_Comm comm, int enable)

@@ -532,16 +532,6 @@ Where classify(const void *p, int *dev, const void **devptr)
     return Where::Pageable;
 }
 
-// The stream-ordered entry points take device-accessible pointers only: a
-// pageable host pointer handed to a kernel would fault the GPU, so it is
-// refused with MPI_ERR_BUFFER; pinned host memory is translated to its
-// device mapping.
-bool device_accessible(const void *p, const void **devptr)
-{
-    int dev = 0;
-    return classify(p, &dev, devptr) != Where::Pageable;
-}
-
 bool overlaps(const void *a, const void *b, uint64_t bytes)
 {
     uintptr_t x = (uintptr_t) a, y = (uintptr_t) b;
@@ -637,9 +627,13 @@ int run_sync(DevState *d, const void *in, void *io, uint64_t count, uint32_t it,
 
 // Host-resident operand(s): stream them through device scratch in chunks,
 // alternating two streams so chunk k+1's copies overlap chunk k's kernel.
+// in_peer >= 0: `in` is device memory of that device, which `dev` cannot reach
+// (no peer access): it is streamed the same way with hipMemcpyPeerAsync.
 int staged(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext, uint32_t op,
-           bool in_host, bool io_host, int dev)
+           bool in_host, bool io_host, int dev, int in_peer = -1)
 {
+    if (in_peer >= 0)
+        in_host = true;
     DevState *d = dev_state(dev);
     if (!d)
         return MPIX_REDOP_ERR_OTHER;
@@ -669,7 +663,10 @@ int staged(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext, 
         char *dst_io = (char *) io + off * ext;
         const void *kin = src_in;
         void *kio = dst_io;
-        if (in_host) {
+        if (in_peer >= 0) {
+            rc = hip_err(hipMemcpyPeerAsync(slot, dev, src_in, in_peer, n * ext, s));
+            kin = slot;
+        } else if (in_host) {
             rc = hip_err(hipMemcpyAsync(slot, src_in, n * ext, hipMemcpyHostToDevice, s));
             kin = slot;
         }
@@ -693,7 +690,8 @@ int staged(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext, 
 // is_equal header back (k_equal writes nothing else).  When the scratch
 // cannot be had nothing has been touched and MPI_ERR_TYPE sends the caller to
 // its own op table.
-int equal_whole(const void *in, void *io, uint64_t n, bool in_host, bool io_host, int dev)
+int equal_whole(const void *in, void *io, uint64_t n, bool in_host, bool io_host, int dev,
+                int in_peer = -1)
 {
     DevState *d = dev_state(dev);
     if (!d)
@@ -717,7 +715,10 @@ int equal_whole(const void *in, void *io, uint64_t n, bool in_host, bool io_host
     const void *kin = in;
     void *kio = io;
     int rc = MPIX_REDOP_SUCCESS;
-    if (in_host) {
+    if (in_peer >= 0) {
+        rc = hip_err(hipMemcpyPeerAsync(d->scratch, dev, in, in_peer, n, s));
+        kin = d->scratch;
+    } else if (in_host) {
         rc = hip_err(hipMemcpyAsync(d->scratch, in, n, hipMemcpyHostToDevice, s));
         kin = d->scratch;
     }
@@ -886,6 +887,78 @@ struct DeviceGuard {
     }
 };
 
+// ------------------------------------------- peer access between devices
+// A kernel on device `dev` may dereference another device's hipMalloc memory
+// only once peer access dev -> owner is enabled.  The reference's HIP backend
+// enables it for every device pair at init (yaksuri_hip_init_hooks.c:164-181:
+// hipDeviceCanAccessPeer, then hipDeviceEnablePeerAccess, "already enabled"
+// tolerated); here each pair is settled at its first use, once per process.
+// State per ordered pair: 0 unknown, 1 direct access, 2 impossible (callers
+// then copy with hipMemcpyPeerAsync or decline).  MPIX_REDOP_PEER=stage treats
+// every pair as impossible (the staging path, testable on any 2-GPU box).
+std::atomic<int8_t> g_peer[kMaxDev][kMaxDev];
+std::mutex g_peer_mu;
+
+bool peer_access(int dev, int owner)
+{
+    if (dev == owner)
+        return true;
+    if (dev < 0 || owner < 0 || dev >= kMaxDev || owner >= kMaxDev)
+        return false;
+    int8_t st = g_peer[dev][owner].load(std::memory_order_acquire);
+    if (st)
+        return st == 1;
+    std::lock_guard<std::mutex> l(g_peer_mu);
+    st = g_peer[dev][owner].load(std::memory_order_acquire);
+    if (st)
+        return st == 1;
+    const char *force = getenv("MPIX_REDOP_PEER");
+    int can = 0;
+    bool ok = !(force && strcmp(force, "stage") == 0) &&
+              hipDeviceCanAccessPeer(&can, dev, owner) == hipSuccess && can;
+    if (ok) {
+        DeviceGuard g(dev);
+        hipError_t e = hipDeviceEnablePeerAccess(owner, 0);
+        ok = e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled;
+    }
+    (void) hipGetLastError();       // "already enabled" is sticky otherwise
+    g_peer[dev][owner].store(ok ? 1 : 2, std::memory_order_release);
+    return ok;
+}
+
+// The device a stream's kernels run on (the null stream: the current one).
+int stream_device(hipStream_t s)
+{
+    int dev = 0;
+    if (s) {
+        hipDevice_t d;
+        if (hipStreamGetDevice(s, &d) == hipSuccess)
+            return (int) d;
+        (void) hipGetLastError();
+    }
+    (void) hipGetDevice(&dev);
+    return dev;
+}
+
+// The stream-ordered entry points take pointers a kernel on `s` can
+// dereference: a pageable host pointer would fault the GPU and is refused with
+// MPI_ERR_BUFFER; pinned host memory is translated to its device mapping; and
+// another device's memory is reachable only with peer access (enabled here at
+// first use), else refused too.  `launch` caches the stream's device (-2 = not
+// looked up yet).
+bool reachable(const void *p, hipStream_t s, int *launch, const void **devptr)
+{
+    int owner = -1;
+    const Where w = classify(p, &owner, devptr);
+    if (w == Where::Pageable)
+        return false;
+    if (w != Where::Device)
+        return true;
+    if (*launch == -2)
+        *launch = stream_device(s);
+    return peer_access(*launch, owner);
+}
+
 // ------------------------------------------- derived targets as runs
 // One uop call of typerep_op_fallback: `n` elements at extent stride from
 // byte offset `off` of inout (may be negative: lb < 0), combined with the
@@ -916,7 +989,8 @@ int enqueue_runs(const void *inbuf, void *inoutbuf, const std::vector<Run> &runs
         return MPIX_REDOP_ERR_BUFFER;
     {
         const void *pin, *pio;
-        if (!device_accessible(inbuf, &pin) || !device_accessible(inoutbuf, &pio))
+        int launch = -2;
+        if (!reachable(inbuf, s, &launch, &pin) || !reachable(inoutbuf, s, &launch, &pio))
             return MPIX_REDOP_ERR_BUFFER;
         inbuf = pin;
         inoutbuf = (void *) pio;
@@ -1118,7 +1192,9 @@ int MPIX_Reduce_local_async(const void *inbuf, void *inoutbuf, MPIX_Aint count,
     if (rc != MPIX_REDOP_SUCCESS || count == 0)
         return set_err(rc);
     const void *pin, *pio;
-    if (!device_accessible(inbuf, &pin) || !device_accessible(inoutbuf, &pio))
+    int launch = -2;
+    if (!reachable(inbuf, (hipStream_t) stream, &launch, &pin) ||
+        !reachable(inoutbuf, (hipStream_t) stream, &launch, &pio))
         return set_err(MPIX_REDOP_ERR_BUFFER);
     return set_err(enqueue(pin, (void *) pio, (uint64_t) count, it, ext, (uint32_t) op,
                            (hipStream_t) stream));
@@ -1147,6 +1223,14 @@ int MPIX_Reduce_local(const void *inbuf, void *inoutbuf, MPIX_Aint count, MPIX_D
     bool io_stage = wio == Where::Pageable || (wio == Where::Pinned && !zc);
     int dev = wio == Where::Device ? dio : (win == Where::Device ? din : cur);
     DeviceGuard guard(dev);
+    if (win == Where::Device && wio == Where::Device && din != dio && !peer_access(dio, din))
+        // operands on two devices without peer access: the kernel runs where
+        // inout lives and `in` is copied over in chunks (hipMemcpyPeerAsync);
+        // MPIX_EQUAL's one header covers the whole message: copied whole
+        return set_err(opi == 15
+                           ? equal_whole(pin, (void *) pio, (uint64_t) count, false, false, dev, din)
+                           : staged(pin, (void *) pio, (uint64_t) count, it, ext, (uint32_t) op,
+                                    false, false, dev, din));
     bool pageable = win == Where::Pageable || wio == Where::Pageable;
     if (pageable && (uint64_t) count * ext <= g_bounce_bytes) {
         // only pageable operands bounce; pinned ones are used through their mapping
@@ -1207,7 +1291,9 @@ int MPIX_Reduce_local_vector_async(const void *inbuf, void *inoutbuf, MPIX_Aint 
         return set_err(MPIX_REDOP_ERR_BUFFER);
     {
         const void *pin, *pio;
-        if (!device_accessible(inbuf, &pin) || !device_accessible(inoutbuf, &pio))
+        int launch = -2;
+        if (!reachable(inbuf, (hipStream_t) stream, &launch, &pin) ||
+            !reachable(inoutbuf, (hipStream_t) stream, &launch, &pio))
             return set_err(MPIX_REDOP_ERR_BUFFER);
         inbuf = pin;
         inoutbuf = (void *) pio;
@@ -1346,10 +1432,11 @@ int MPIX_Reduce_local_multi_async(const void *const *inbufs, int ninputs, void *
         return set_err(MPIX_REDOP_SUCCESS);
     const void *dins[mpix::kMaxMultiInputs];
     const void *pio;
-    if (!device_accessible(inoutbuf, &pio))
+    int launch = -2;
+    if (!reachable(inoutbuf, (hipStream_t) stream, &launch, &pio))
         return set_err(MPIX_REDOP_ERR_BUFFER);
     for (int q = 0; q < ninputs; ++q)
-        if (!device_accessible(inbufs[q], &dins[q]))
+        if (!reachable(inbufs[q], (hipStream_t) stream, &launch, &dins[q]))
             return set_err(MPIX_REDOP_ERR_BUFFER);
     inbufs = dins;
     inoutbuf = (void *) pio;
@@ -1399,12 +1486,13 @@ int MPIX_Reduce_local_tree_async(const void *const *inbufs, int ninputs, void *o
         return set_err(MPIX_REDOP_ERR_OP);      // EQUAL is never split or folded
     const void *dins[mpix::kMaxMultiInputs];
     const void *pout;
-    if (!device_accessible(outbuf, &pout))
+    int launch = -2;
+    if (!reachable(outbuf, (hipStream_t) stream, &launch, &pout))
         return set_err(MPIX_REDOP_ERR_BUFFER);
     int last = 0;
     for (int q = 0; q < ninputs; ++q) {
         dins[q] = nullptr;
-        if (inbufs[q] && !device_accessible(inbufs[q], &dins[q]))
+        if (inbufs[q] && !reachable(inbufs[q], (hipStream_t) stream, &launch, &dins[q]))
             return set_err(MPIX_REDOP_ERR_BUFFER);
         if (inbufs[q])
             last = q;
@@ -1431,7 +1519,7 @@ int MPIX_Copy_multi_async(const void *const *srcs, void *const *dsts, const MPIX
     const void *ds[mpix::kMaxMultiInputs];
     void *dd[mpix::kMaxMultiInputs];
     uint64_t nb[mpix::kMaxMultiInputs];
-    int m = 0;
+    int m = 0, launch = -2;
     for (int q = 0; q < n; ++q) {
         if (bytes[q] < 0)
             return set_err(MPIX_REDOP_ERR_COUNT);
@@ -1440,7 +1528,8 @@ int MPIX_Copy_multi_async(const void *const *srcs, void *const *dsts, const MPIX
         if (!srcs[q] || !dsts[q] || overlaps(srcs[q], dsts[q], (uint64_t) bytes[q]))
             return set_err(MPIX_REDOP_ERR_BUFFER);
         const void *pd;
-        if (!device_accessible(srcs[q], &ds[m]) || !device_accessible(dsts[q], &pd))
+        if (!reachable(srcs[q], (hipStream_t) stream, &launch, &ds[m]) ||
+            !reachable(dsts[q], (hipStream_t) stream, &launch, &pd))
             return set_err(MPIX_REDOP_ERR_BUFFER);
         dd[m] = (void *) pd;
         nb[m++] = (uint64_t) bytes[q];
@@ -1483,6 +1572,11 @@ int MPIX_Ipc_close(void *base)
     return set_err(hip_err(hipIpcCloseMemHandle(base)));
 }
 
+int MPIX_Redop_peer_access(int device, int peer_device)
+{
+    return peer_access(device, peer_device) ? 1 : 0;
+}
+
 // the (op, type) half of the predicate: a kernel exists (knob-independent)
 static int has_gpu_path(uint32_t op, uint32_t it)
 {
@@ -1494,6 +1588,11 @@ static int has_gpu_path(uint32_t op, uint32_t it)
     if (opi == 15)
         return (it & 0xffffff00u) == U8;
     return gpu_entry(opi, it) ? 1 : 0;
+}
+
+int MPIX_Redop_has_gpu_path(MPIX_Op op, MPIX_Datatype datatype)
+{
+    return has_gpu_path((uint32_t) op, to_internal((uint32_t) datatype));
 }
 
 // MPIR_Typerep_reduce_is_supported (typerep_yaksa_pack.c:227-271): the enable

@@ -61,6 +61,8 @@ def lib():
             'MPIX_Ipc_export': ([vp, vp, ctypes.POINTER(aint)], i32),
             'MPIX_Ipc_open': ([vp, ctypes.POINTER(vp)], i32),
             'MPIX_Ipc_close': ([vp], i32),
+            'MPIX_Redop_peer_access': ([i32, i32], i32),
+            'MPIX_Redop_has_gpu_path': ([i32, i32], i32),
             'MPIX_Redop_op_dt_check': ([i32, i32], i32),
             'MPIX_Redop_internal_op_dt_check': ([i32, i32], i32),
             'MPIX_Datatype_internal': ([i32], i32),
@@ -298,6 +300,17 @@ def ipc_open(handle):
 
 def ipc_close(base):
     return lib().MPIX_Ipc_close(base)
+
+
+def peer_access(device, peer_device):
+    """True if kernels on `device` can read `peer_device`'s memory (peer access
+    enabled at the pair's first use, yaksuri_hip_init_hooks.c:164-181)"""
+    return bool(lib().MPIX_Redop_peer_access(device, peer_device))
+
+
+def has_gpu_path(op, datatype):
+    """a kernel covers (op, datatype), whatever the support knobs say"""
+    return bool(lib().MPIX_Redop_has_gpu_path(H.as_c_int(op), H.as_c_int(datatype)))
 
 
 def check(rc, what='MPI_Reduce_local'):

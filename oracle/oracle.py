@@ -19,8 +19,9 @@ _lib = None
 
 def build(force=False):
     """Compile the oracle with gcc (oracle/Makefile)."""
+    srcs = [os.path.join(HERE, f) for f in ('redop_oracle.c', 'host_bench.c')]
     if force or not os.path.exists(LIB_PATH) or \
-            os.path.getmtime(LIB_PATH) < os.path.getmtime(os.path.join(HERE, 'redop_oracle.c')):
+            os.path.getmtime(LIB_PATH) < max(os.path.getmtime(f) for f in srcs):
         subprocess.check_call(['make', '-s', '-C', HERE])
     return LIB_PATH
 
@@ -60,6 +61,9 @@ def lib():
         L.oracle_allreduce_ring.argtypes = L.oracle_rsb_recursive_halving.argtypes
         L.oracle_scan.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(vp), il, i32, i32, i32, i32]
         L.oracle_wtime.restype = ctypes.c_double
+        dp, ip = ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32)
+        L.oracle_bench_reduce.argtypes = [il, i32, i32, i32, ip, ctypes.c_double, dp, dp, ip]
+        L.oracle_bench_triad.argtypes = [il, i32, ip, ctypes.c_double, dp, dp, ip]
         _lib = L
     return _lib
 
@@ -215,3 +219,26 @@ def combine_fn_address():
     """address of oracle_combine (MPIX_Combine_fn signature), for installing
     the oracle as the combine of a host-memory libmpix_coll communicator"""
     return ctypes.cast(lib().oracle_combine, ctypes.c_void_p).value
+
+
+def _bench(fn, *args):
+    best, med, passes = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
+    rc = fn(*args, ctypes.byref(best), ctypes.byref(med), ctypes.byref(passes))
+    if rc:
+        raise RuntimeError('host bench failed (%d)' % rc)
+    return best.value, med.value, passes.value
+
+
+def bench_reduce(count, datatype, op, cpus, seconds):
+    """MPI_Reduce_local(datatype, op) on `count` elements split over one
+    pinned thread per entry of `cpus` (each first-touches its own slice);
+    (best, median) seconds per pass and the number of passes"""
+    arr = (ctypes.c_int * len(cpus))(*cpus)
+    return _bench(lib().oracle_bench_reduce, count, _i32(datatype), _i32(op), len(cpus), arr,
+                  float(seconds))
+
+
+def bench_triad(count, cpus, seconds):
+    """host STREAM triad on `count` fp32 (12 bytes each) over pinned threads"""
+    arr = (ctypes.c_int * len(cpus))(*cpus)
+    return _bench(lib().oracle_bench_triad, count, len(cpus), arr, float(seconds))

@@ -62,3 +62,80 @@ def test_emitter_prints_once_and_only_on_rank0():
         """)
     assert p.returncode == 0
     assert p.stdout.strip().splitlines() == ['{"v": 1}']
+
+
+def _threads(comms, fn):
+    import threading
+    out = [None] * len(comms)
+    ts = [threading.Thread(target=lambda r=r: out.__setitem__(r, fn(r, comms[r])))
+          for r in range(len(comms))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(60)
+    assert not any(t.is_alive() for t in ts), 'a rank hung'
+    return out
+
+
+def test_schedule_ran_reports_fallback(oracle, monkeypatch):
+    """a requested schedule that cannot run is reported as
+    'fell back to ...' by the bench helper and never timed under its name.
+    On host communicators the pulls cannot run (no device memory to map), so
+    'pull' runs one-group pairwise and 'recursive_halving_pull' recursive
+    halving -- with MPIX_COLL_WINDOW_FAULT set as in the GPU fault test."""
+    import bench
+    from mpich_amd import ccl
+    monkeypatch.setenv('MPIX_COLL_WINDOW_FAULT', '1')
+    P, n = 4, 1003
+    comms = ccl.comm_create_local(P)
+    for c in comms:
+        c.set_combine(oracle.combine_fn_address())
+    sends = [np.random.default_rng(r).uniform(-1, 1, P * n).astype(np.float32) for r in range(P)]
+    recvs = [np.zeros(n, np.float32) for _ in range(P)]
+    MPI_FLOAT, MPI_SUM = 0x4c00040a, 0x58000003
+    try:
+        for algo, ran in (('pull', 'pairwise'), ('recursive_halving_pull', 'recursive_halving'),
+                          ('recursive_halving_multipath', 'recursive_halving'),  # P=4 ok on host
+                          ('pairwise', 'pairwise')):
+            rcs = _threads(comms, lambda r, c: ccl.reduce_scatter_block(
+                sends[r], recvs[r], n, MPI_FLOAT, MPI_SUM, c, algo))
+            assert rcs == [0] * P
+            for c in comms:
+                got = bench.schedule_ran(c, algo)
+                if algo == 'recursive_halving_multipath':
+                    assert got['schedule_ran'] == algo and 'error' not in got, got
+                else:
+                    assert got['schedule_ran'] == ran, got
+                    assert ('error' in got) == (ran != algo), got
+                    if ran != algo:
+                        assert got['error'] == 'fell back to ' + ran
+                assert got['pulls_enabled'] is False
+        st = comms[0].state()
+        assert st['fallbacks'] == 2 and st['window_retries'] == 0, st
+        # allreduce: pull -> reduce_scatter_allgather; multipath on P=3-like
+        # shapes (count % P) -> reduce_scatter_allgather
+        outs = [np.zeros(P * n, np.float32) for _ in range(P)]
+        for algo, count in (('pull', P * n), ('rsag_multipath', P * n - 1),
+                            ('rsag_multipath', P * n)):
+            rcs = _threads(comms, lambda r, c: ccl.allreduce(sends[r][:count], outs[r][:count],
+                                                              count, MPI_FLOAT, MPI_SUM, c, algo))
+            assert rcs == [0] * P
+            got = bench.schedule_ran(comms[1], algo, 'ar')
+            fell = algo == 'pull' or count % P
+            assert got['schedule_ran'] == ('reduce_scatter_allgather' if fell else algo), got
+            assert ('error' in got) == bool(fell)
+    finally:
+        for c in comms:
+            c.free()
+
+
+def test_state_before_first_collective():
+    from mpich_amd import ccl
+    comms = ccl.comm_create_local(2)
+    try:
+        st = comms[0].state()
+        assert st == dict(pulls_enabled=False, last_rs=None, last_allreduce=None,
+                          window_retries=0, fallbacks=0), st
+    finally:
+        for c in comms:
+            c.free()

@@ -802,14 +802,16 @@ def test_reduce_scatter_device_pipelined(oracle, P):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('counts', [[1, 4000, 3, 9000], [1, 4000], [4000, 1], [5, 5]])
 @pytest.mark.parametrize('algo', ['recursive_halving', 'pairwise', 'pairwise_sequential'])
-def test_reduce_scatter_device_in_place_overlap(oracle, algo):
+def test_reduce_scatter_device_in_place_overlap(oracle, algo, counts):
     """MPI_IN_PLACE with uneven counts where a rank's own block overlaps the
     front of recvbuf (counts [1, 4000, 3, 9000]: rank 1's block at offset 1
-    is moved to offset 0), device buffers"""
+    is moved to offset 0), device buffers.  P = 2 recursive halving: the
+    first step is also the last and reads recvbuf's second block while the
+    result goes to its front -- [1, 4000] overlaps."""
     import torch
     from mpich_amd import ccl
-    counts = [1, 4000, 3, 9000]
     P = len(counts)
     sends = float_sends(P, sum(counts), 0x5EED0900)
     bufs = [torch.from_numpy(s.copy()).cuda() for s in sends]
@@ -1088,3 +1090,99 @@ def test_scan_device_matches_oracle(oracle, exclusive):
                          exclusive)
     for r in range(P):
         assert douts[r].cpu().numpy().view(np.uint8).tobytes() == exp[r].tobytes(), r
+
+
+@pytest.mark.gpu
+def test_collectives_ignore_support_knob(oracle):
+    """MPIX_REDOP_ENABLE=0 (set_support(enable=False)) only answers
+    MPIX_Redop_is_supported's callers; the collectives keep their kernels
+    (the reference's MPIR_CVAR_ENABLE_YAKSA_REDUCTION only moves
+    reductions back to the CPU)"""
+    import torch
+    from mpich_amd import ccl, redop
+    P, n = 3, 10007
+    sends = float_sends(P, P * n, 0x5EED0A00)
+    dsend = [torch.from_numpy(s).cuda() for s in sends]
+    drecv = [torch.zeros(n, dtype=torch.float32, device='cuda') for _ in range(P)]
+    torch.cuda.synchronize()
+    before = redop.get_support()
+    redop.check(redop.set_support(enable=False))
+    comms = _dev_comms(P)
+    try:
+        assert not redop.is_supported(MPI_SUM, MPI_FLOAT)
+        assert redop.has_gpu_path(MPI_SUM, MPI_FLOAT)
+        rcs = run_ranks(comms, lambda r, c: ccl.reduce_scatter_block(
+            dsend[r], drecv[r], n, MPI_FLOAT, MPI_SUM, c, 'recursive_halving'))
+        assert rcs == [0] * P
+    finally:
+        free_all(comms)
+        redop.check(redop.set_support(before['enable'], before['threshold_bytes'],
+                                      before['host_floor_bytes'], before['pinned_floor_bytes']))
+    exp = oracle.rsb_recursive_halving([s.view(np.uint8) for s in sends], n, MPI_FLOAT, MPI_SUM)
+    for r in range(P):
+        assert drecv[r].cpu().numpy().tobytes() == exp[r].tobytes(), r
+
+
+@pytest.mark.gpu
+def test_state_on_device_local_communicator(oracle):
+    """MPIX_Comm_get_state on the device transport: the pulls run as asked
+    (no fallback) and AUTO resolves to the generic.json choice"""
+    import torch
+    from mpich_amd import ccl
+    P, n = 4, 4099
+    dsend = [torch.from_numpy(s).cuda() for s in float_sends(P, P * n, 7)]
+    drecv = [torch.zeros(n, dtype=torch.float32, device='cuda') for _ in range(P)]
+    torch.cuda.synchronize()
+    comms = _dev_comms(P)
+    try:
+        for algo, ran in (('recursive_halving_pull', 'recursive_halving_pull'), ('pull', 'pull'),
+                          ('auto', 'recursive_halving'), ('pairwise', 'pairwise')):
+            rcs = run_ranks(comms, lambda r, c: ccl.reduce_scatter_block(
+                dsend[r], drecv[r], n, MPI_FLOAT, MPI_SUM, c, algo))
+            assert rcs == [0] * P
+            for c in comms:
+                st = c.state()
+                assert st['last_rs'] == ran and st['pulls_enabled'] and st['fallbacks'] == 0, st
+    finally:
+        free_all(comms)
+
+
+def _ndev():
+    import torch
+    return torch.cuda.device_count() if torch.cuda.is_available() else 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('algo', ['pull', 'recursive_halving_pull', 'recursive_halving'])
+def test_local_communicator_on_distinct_devices(oracle, algo):
+    """MPIX_Comm_create_local(P, [0..P-1]): peer access is enabled for every
+    device pair at creation (yaksuri_hip_init_hooks.c:164-181), so the pulls
+    read the other GPUs' buffers directly; bit-identical to the oracle.
+    Skipped below 2 devices (the test box has one)."""
+    import torch
+    from mpich_amd import ccl, redop
+    P = min(_ndev(), 8)
+    if P < 2:
+        pytest.skip('needs >= 2 GPUs for ranks on distinct devices (this box has %d)' % P)
+    n = 40961
+    sends = float_sends(P, P * n, 0x5EED0B00)
+    dsend = [torch.from_numpy(s).to('cuda:%d' % r) for r, s in enumerate(sends)]
+    drecv = [torch.zeros(n, dtype=torch.float32, device='cuda:%d' % r) for r in range(P)]
+    for r in range(P):
+        torch.cuda.synchronize(r)
+    comms = ccl.comm_create_local(P, list(range(P)))
+    try:
+        rcs = run_ranks(comms, lambda r, c: ccl.reduce_scatter_block(
+            dsend[r], drecv[r], n, MPI_FLOAT, MPI_SUM, c, algo))
+        assert rcs == [0] * P
+        peers = all(redop.peer_access(a, b) for a in range(P) for b in range(P))
+        st = comms[0].state()
+        assert st['pulls_enabled'] == peers, st
+        if peers:
+            assert st['last_rs'] == algo, st
+    finally:
+        free_all(comms)
+    sim = oracle.rsb_pairwise if algo == 'pull' else oracle.rsb_recursive_halving
+    exp = sim([s.view(np.uint8) for s in sends], n, MPI_FLOAT, MPI_SUM)
+    for r in range(P):
+        assert drecv[r].cpu().numpy().tobytes() == exp[r].tobytes(), r
