@@ -281,26 +281,31 @@ def cpu_baseline(seconds, count, crossover_rows):
     phys = topo['physical']
     alg = 3 * count * 4
 
-    def reduce_leg(cpus, budget, n=count):
-        best, med, passes = orc.bench_reduce(n, H.MPI_FLOAT, H.MPI_SUM, cpus, budget)
-        return dict(gibs=round(3 * n * 4 / GIB / med, 3), best=round(3 * n * 4 / GIB / best, 3),
+    def leg(kind, cpus, budget, n=count):
+        if kind == 'reduce':
+            best, med, passes, span = orc.bench_reduce(n, H.MPI_FLOAT, H.MPI_SUM, cpus, budget)
+        else:
+            best, med, passes, span = orc.bench_triad(n, cpus, budget)
+        nb = 3 * n * 4
+        return dict(gibs=round(nb / GIB / med, 3), best=round(nb / GIB / best, 3),
+                    sustained=round(passes * nb / GIB / span, 3) if span > 0 else None,
                     reps=passes, threads=len(cpus))
 
-    def triad_leg(cpus, budget):
-        best, med, passes = orc.bench_triad(count, cpus, budget)
-        return dict(gibs=round(alg / GIB / med, 3), best=round(alg / GIB / best, 3), reps=passes,
-                    threads=len(cpus))
-
-    one = reduce_leg(phys[:1], seconds * 0.25)
-    allc = reduce_leg(phys, seconds * 0.15)
-    tri_all = triad_leg(phys, seconds * 0.15)
-    tri_one = triad_leg(phys[:1], seconds * 0.1)
-    c1 = reduce_leg(phys[:1], seconds * 0.1, n=4194304)
-    scaling = []
-    for k in (8, 16, 32, 64):
-        if k < len(phys):
-            scaling.append(dict(threads=k, reduce_gibs=reduce_leg(phys[:k], seconds * 0.03)['gibs'],
-                                triad_gibs=triad_leg(phys[:k], seconds * 0.03)['gibs']))
+    quota = topo['cgroup_cpu_quota']
+    nq = max(1, min(len(phys), int(quota))) if quota else len(phys)
+    one = leg('reduce', phys[:1], seconds * 0.25)
+    allc = leg('reduce', phys, seconds * 0.15)
+    tri_all = leg('triad', phys, seconds * 0.1)
+    tri_one = leg('triad', phys[:1], seconds * 0.1)
+    c1 = leg('reduce', phys[:1], seconds * 0.1, n=4194304)
+    quota_leg = None
+    if nq < len(phys):
+        q = leg('reduce', phys[:nq], seconds * 0.1)
+        tq = leg('triad', phys[:nq], seconds * 0.1)
+        quota_leg = dict(threads=nq, value=q['gibs'], sustained=q['sustained'],
+                         host_triad_gibs=tq['gibs'], frac_of_host_triad=round(q['gibs'] / tq['gibs'], 4),
+                         note='as many pinned threads as the cgroup quota grants CPUs, spread '
+                              'over both sockets: what this process can sustain')
     if crossover_rows:
         B = bench_lib()
         fn = ctypes.cast(orc.lib().oracle_reduce_local, ctypes.c_void_p).value
@@ -317,22 +322,25 @@ def cpu_baseline(seconds, count, crossover_rows):
                'operand, host-resident) through oracle/redop_oracle.c, 1 pinned thread, %d calls, '
                'median' % (count, count * 4 >> 20, one['reps']),
         best=one['best'],
+        host_triad_1core_gibs=tri_one['gibs'],
         frac_of_host_triad_1core=round(one['gibs'] / tri_one['gibs'], 4),
         allcores=dict(value=allc['gibs'], threads=allc['threads'], reps=allc['reps'],
-                      host_triad_gibs=tri_all['gibs'],
+                      sustained=allc['sustained'], host_triad_gibs=tri_all['gibs'],
                       frac_of_host_triad=round(allc['gibs'] / tri_all['gibs'], 4),
                       note='one pinned thread per physical core of this process (%d sockets), '
                            'each first-touching its own slice of both operands (NUMA-local); '
-                           'host triad = a += 0.5 b on the same threads and layout (12 B per '
-                           'element, the combine\'s own traffic)' % topo['sockets']),
-        host_triad_1core_gibs=tri_one['gibs'],
-        thread_scaling=scaling,
+                           'value = median pass; host triad = a += 0.5 b on the same threads '
+                           'and layout (12 B per element, the combine\'s own traffic); with a '
+                           'cgroup quota below the thread count the passes run in the quota\'s '
+                           'run windows and `sustained` (all passes / their wall span) is the '
+                           'throttled rate' % topo['sockets']),
+        quota_threads=quota_leg,
         config1_16MiB_1core=dict(value=c1['gibs'], reps=c1['reps'],
                                  note='BASELINE config 1; 48 MiB per call is cache-resident on '
                                       'this host'),
         host_cpu=topo['model'], nproc=os.cpu_count(), affinity_cpus=len(topo['affinity']),
         physical_cores=len(phys), sockets=topo['sockets'],
-        cgroup_cpu_quota=topo['cgroup_cpu_quota'])
+        cgroup_cpu_quota=quota)
 
 
 def load_pmc(path, count):
@@ -561,6 +569,9 @@ def pcie_rates(hin, hio, dev, reps=3):
             hio.copy_(d1, non_blocking=True)
     nb = 4 * n
     t_h2d, t_d2h = timed(h2d), timed(d2h)
+    # the call's floor: its 2 GiB in at the H2D rate and its 1 GiB out at the
+    # D2H rate, the two directions concurrent (full duplex)
+    t_floor = max(2 * t_h2d, t_d2h)
     d1.copy_(hio)           # the operands keep their values for the timed calls
     torch.cuda.synchronize()
     t_pat = timed(pattern)
@@ -568,10 +579,12 @@ def pcie_rates(hin, hio, dev, reps=3):
         hio.copy_(d1)
     del d0, d1
     return dict(h2d_GBs=round(nb / t_h2d / 1e9, 2), d2h_GBs=round(nb / t_d2h / 1e9, 2),
-                pattern_2h2d_1d2h_ms=round(t_pat * 1e3, 2),
-                pattern_GiBs=round(3 * nb / t_pat / GIB, 2),
-                note='page-locked host <-> HBM, 1 GiB per copy, best of %d; pattern = the '
-                     'host-resident call\'s 2 GiB in + 1 GiB out at once' % reps), t_pat
+                floor_ms=round(t_floor * 1e3, 2),
+                sdma_pattern_2h2d_1d2h_ms=round(t_pat * 1e3, 2),
+                note='page-locked host <-> HBM copies (SDMA), 1 GiB each, best of %d; floor = '
+                     'max(2 GiB at the H2D rate, 1 GiB at the D2H rate), the call\'s own '
+                     'traffic with both directions at once; the SDMA engines themselves reach '
+                     'only sdma_pattern when both directions run together' % reps), t_floor
 
 
 def end_to_end(result, n, dev=None):

@@ -62,8 +62,8 @@ def lib():
         L.oracle_scan.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(vp), il, i32, i32, i32, i32]
         L.oracle_wtime.restype = ctypes.c_double
         dp, ip = ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32)
-        L.oracle_bench_reduce.argtypes = [il, i32, i32, i32, ip, ctypes.c_double, dp, dp, ip]
-        L.oracle_bench_triad.argtypes = [il, i32, ip, ctypes.c_double, dp, dp, ip]
+        L.oracle_bench_reduce.argtypes = [il, i32, i32, i32, ip, ctypes.c_double, dp, dp, ip, dp]
+        L.oracle_bench_triad.argtypes = [il, i32, ip, ctypes.c_double, dp, dp, ip, dp]
         _lib = L
     return _lib
 
@@ -222,17 +222,19 @@ def combine_fn_address():
 
 
 def _bench(fn, *args):
-    best, med, passes = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
-    rc = fn(*args, ctypes.byref(best), ctypes.byref(med), ctypes.byref(passes))
+    best, med, passes, span = ctypes.c_double(), ctypes.c_double(), ctypes.c_int(), \
+        ctypes.c_double()
+    rc = fn(*args, ctypes.byref(best), ctypes.byref(med), ctypes.byref(passes), ctypes.byref(span))
     if rc:
         raise RuntimeError('host bench failed (%d)' % rc)
-    return best.value, med.value, passes.value
+    return best.value, med.value, passes.value, span.value
 
 
 def bench_reduce(count, datatype, op, cpus, seconds):
     """MPI_Reduce_local(datatype, op) on `count` elements split over one
     pinned thread per entry of `cpus` (each first-touches its own slice);
-    (best, median) seconds per pass and the number of passes"""
+    (best, median) seconds per pass, the number of passes and the wall span
+    of all passes (passes / span = sustained rate)"""
     arr = (ctypes.c_int * len(cpus))(*cpus)
     return _bench(lib().oracle_bench_reduce, count, _i32(datatype), _i32(op), len(cpus), arr,
                   float(seconds))

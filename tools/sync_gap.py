@@ -9,15 +9,9 @@ run:    sync_gap.py run OUT.json [reps]
         CLOCK_MONOTONIC and CLOCK_BOOTTIME.  Run it under
         rocprofv3 --kernel-trace --output-format csv.
 report: sync_gap.py report OUT.json KERNEL_TRACE.csv
-        lines the calls up with the trace (the clock whose offset puts each
-        kernel inside its call) and splits each call into
-          launch   host entry -> kernel start
-          kernel   the k_contig dispatch
-          to_blit  kernel end -> the stream's completion write
-                   (__amd_rocclr_streamOpsWrite) starts
-          blit     that write's own duration
-          wake     write end -> host return (spin sees the word)
-          between  host return -> next call's entry (the loop itself)
+        splits the time between consecutive kernels on the GPU's own clock
+        (kernel, end -> completion write, the write, write -> next kernel)
+        and reads the host's per-call time beside it
 """
 import ctypes
 import csv
@@ -57,46 +51,47 @@ def run(out, reps):
 
 
 def report(host_json, trace_csv, out=None):
+    """the split of one call, from the GPU's own timestamps (exact, one clock)
+    plus the host's per-call time (another clock: only differences of it are
+    used, never compared with the GPU's)"""
     h = json.load(open(host_json))
     calls = h['calls']
-    rows = list(csv.DictReader(open(trace_csv)))
     ev = []
-    for r in rows:
-        name = r.get('Kernel_Name') or r.get('KernelName') or ''
-        s, e = int(r['Start_Timestamp']), int(r['End_Timestamp'])
-        ev.append((s, e, name))
+    for r in csv.DictReader(open(trace_csv)):
+        ev.append((int(r['Start_Timestamp']), int(r['End_Timestamp']), r['Kernel_Name']))
     ev.sort()
-    ks = [x for x in ev if 'k_contig' in x[2]]
-    blits = [x for x in ev if 'streamOpsWrite' in x[2]]
-    # the recorded pass = the last len(calls) big kernels
-    big = [x for x in ks if x[1] - x[0] > 100000][-len(calls):]
-    best = None
-    for clk in ('mono', 'boot'):
-        inside = sum(c[clk + '_in'] <= k[0] and k[1] <= c[clk + '_out'] for c, k in zip(calls, big))
-        if best is None or inside > best[1]:
-            best = (clk, inside)
-    clk = best[0]
-    parts = {k: [] for k in ('launch', 'kernel', 'to_blit', 'blit', 'wake', 'call', 'between')}
-    for i, (c, k) in enumerate(zip(calls, big)):
-        bl = next((b for b in blits if b[0] >= k[1]), None)
-        parts['launch'].append((k[0] - c[clk + '_in']) / 1e3)
+    # the recorded pass: the last len(calls) big kernels, each followed by its
+    # stream completion write (__amd_rocclr_streamOpsWrite)
+    big = [i for i, x in enumerate(ev) if 'k_contig' in x[2] and x[1] - x[0] > 100000]
+    big = big[-len(calls):]
+    parts = {k: [] for k in ('kernel', 'end_to_signal', 'signal', 'signal_to_next_kernel',
+                             'gpu_period', 'host_call', 'host_period')}
+    for j, i in enumerate(big):
+        k = ev[i]
         parts['kernel'].append((k[1] - k[0]) / 1e3)
-        if bl and bl[1] <= c[clk + '_out'] + 1000:
-            parts['to_blit'].append((bl[0] - k[1]) / 1e3)
-            parts['blit'].append((bl[1] - bl[0]) / 1e3)
-            parts['wake'].append((c[clk + '_out'] - bl[1]) / 1e3)
-        else:
-            parts['wake'].append((c[clk + '_out'] - k[1]) / 1e3)
-        parts['call'].append((c[clk + '_out'] - c[clk + '_in']) / 1e3)
-        if i + 1 < len(calls):
-            parts['between'].append((calls[i + 1][clk + '_in'] - c[clk + '_out']) / 1e3)
-    summ = {k: dict(median_us=round(statistics.median(v), 2), mean_us=round(statistics.mean(v), 2),
-                    n=len(v)) for k, v in parts.items() if v}
-    res = dict(clock=clk, kernels_inside_calls=best[1], calls=len(calls), split=summ,
-               overhead_us_median=round(summ['call']['median_us'] - summ['kernel']['median_us'], 2),
-               note='per synchronous 1 GiB fp32 SUM call; launch = host entry to kernel start, '
-                    'to_blit + blit = the stream completion write after the kernel, wake = its '
-                    'end to the host seeing the word and returning')
+        sig = ev[i + 1] if i + 1 < len(ev) and 'streamOpsWrite' in ev[i + 1][2] else None
+        if sig:
+            parts['end_to_signal'].append((sig[0] - k[1]) / 1e3)
+            parts['signal'].append((sig[1] - sig[0]) / 1e3)
+        if j + 1 < len(big):
+            nxt = ev[big[j + 1]]
+            parts['gpu_period'].append((nxt[0] - k[0]) / 1e3)
+            if sig:
+                parts['signal_to_next_kernel'].append((nxt[0] - sig[1]) / 1e3)
+    for j, c in enumerate(calls):
+        parts['host_call'].append((c['mono_out'] - c['mono_in']) / 1e3)
+        if j + 1 < len(calls):
+            parts['host_period'].append((calls[j + 1]['mono_in'] - c['mono_in']) / 1e3)
+    med = {k: round(statistics.median(v), 2) for k, v in parts.items() if v}
+    res = dict(calls=len(calls), median_us=med,
+               overhead_us=round(med['host_call'] - med['kernel'], 2),
+               gpu_idle_between_kernels_us=round(med['gpu_period'] - med['kernel'], 2),
+               note='one synchronous 1 GiB fp32 SUM MPIX_Reduce_local per call, called back to '
+                    'back from C. GPU clock: kernel, end_to_signal (kernel end -> the stream\'s '
+                    'completion write starts: end-of-kernel release + dispatch), signal (that '
+                    'write, a blit kernel), signal_to_next_kernel (host sees the word, returns, '
+                    'enters the next call, launches; the kernel starts). host_call - kernel = '
+                    'the per-call overhead against the kernel alone.')
     if out:
         json.dump(res, open(out, 'w'), indent=1)
     print(json.dumps(res))
