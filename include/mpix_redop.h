@@ -374,7 +374,11 @@ int MPIX_Redop_get_launch(int *block_threads, int *unroll, int *max_grid);
  * threads 0..16, chunk 64 KiB..256 MiB.  The slots are one set per device
  * for the whole process (threads x 2 x chunk of page-locked memory, 256 MiB
  * at the defaults, freed by MPIX_Redop_finalize); a call that finds the set
- * in use by another thread stages its operands instead. */
+ * in use by another thread stages its operands instead.  Each worker copies
+ * its next chunk while the kernel of its current one runs (two buffers per
+ * worker; env MPIX_REDOP_PAGEABLE_DB=0 for one), and env
+ * MPIX_REDOP_PAGEABLE_AFFINITY=gpu pins the workers to the CPUs of the GPU's
+ * NUMA node (or to an explicit cpulist such as "64-127"; default none). */
 int MPIX_Redop_set_pageable(int threads, MPIX_Aint chunk_bytes);
 int MPIX_Redop_get_pageable(int *threads, MPIX_Aint *chunk_bytes);
 

@@ -10,6 +10,9 @@
 // for it (exactly how reduce_local.c:66-76 falls back when yaksa declines).
 #include <hip/hip_runtime_api.h>
 
+#include <ctype.h>
+#include <pthread.h>
+#include <sched.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -17,6 +20,7 @@
 
 #include <atomic>
 #include <chrono>
+#include <string>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -259,6 +263,13 @@ size_t g_bounce_bytes = (size_t) 1 << 20;
 // and staging is faster (profiles/r01_pageable_sweep.txt)
 std::atomic<int> g_pipe_threads{8};
 std::atomic<size_t> g_pipe_chunk{(size_t) 16 << 20};
+// Each worker keeps two slots and copies chunk k + W into one while the kernel
+// of chunk k reads the other (MPIX_REDOP_PAGEABLE_DB=0: one slot, copy and
+// kernel in turn), and the workers can be pinned to the CPUs of the GPU's own
+// NUMA node (MPIX_REDOP_PAGEABLE_AFFINITY=gpu, or an explicit cpulist such as
+// "64-127"; "none" leaves them where the scheduler puts them)
+std::atomic<bool> g_pipe_db{true};
+std::string g_pipe_affinity = "none";
 // Support-predicate knobs, the pattern of MPIR_CVAR_ENABLE_YAKSA_REDUCTION and
 // MPIR_CVAR_YAKSA_REDUCTION_THRESHOLD (typerep_yaksa_pack.c:44-64,229-240):
 // MPIX_REDOP_ENABLE=0 makes every predicate answer 0 (the caller keeps its CPU
@@ -308,6 +319,10 @@ void read_env()
         if (t >= 0 && t <= 16)
             g_pipe_threads = t;
     }
+    if (const char *s = getenv("MPIX_REDOP_PAGEABLE_DB"))
+        g_pipe_db = atoi(s) != 0;
+    if (const char *s = getenv("MPIX_REDOP_PAGEABLE_AFFINITY"))
+        g_pipe_affinity = s;
     if (const char *s = getenv("MPIX_REDOP_PAGEABLE_CHUNK")) {
         long long c = atoll(s);
         if (c >= 65536 && c <= (256ll << 20))
@@ -363,13 +378,17 @@ struct DevState {
 // busy stages its operands instead (same kernel, same bits).
 struct PipeSlot {
     hipStream_t s = nullptr;
-    char *host = nullptr;   // in half + inout half, half bytes each
+    char *host = nullptr;   // nbuf buffers of (in half + inout half), half bytes each
     char *dev = nullptr;    // its device mapping
+    hipEvent_t ev[2] = {nullptr, nullptr};   // kernel of the chunk in buffer 0 / 1 done
 };
 struct PipeSet {
     std::mutex mu;
     PipeSlot slot[16];
     size_t half = 0;        // slot half size; slots [0, threads) hold host != nullptr
+    int nbuf = 0;           // buffers per worker (2: double-buffered)
+    bool cpus_known = false;
+    std::vector<int> cpus;  // worker CPUs (empty: no pinning)
 };
 PipeSet *g_pipes = new PipeSet[64];     // per device; never destroyed (finalize frees the memory)
 // Per-thread device state (streams, flag word, scratch).  A thread that exits
@@ -784,6 +803,72 @@ int bounced(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext,
 // bounce.  Each element is combined exactly once, by the same kernel, so the
 // bits equal every other path's.  Returns -1 when the slots cannot be had
 // (caller stages).
+// CPUs of the GPU's NUMA node (sysfs local_cpulist of its PCI function),
+// intersected with this process's affinity; or an explicit "a-b,c" list
+std::vector<int> parse_cpulist(const char *txt)
+{
+    std::vector<int> out;
+    for (const char *p = txt; *p;) {
+        char *e;
+        long a = strtol(p, &e, 10);
+        if (e == p)
+            break;
+        long b = a;
+        p = e;
+        if (*p == '-') {
+            b = strtol(p + 1, &e, 10);
+            p = e;
+        }
+        for (long c = a; c <= b && c < 4096; ++c)
+            out.push_back((int) c);
+        while (*p == ',' || *p == ' ' || *p == '\n')
+            ++p;
+    }
+    return out;
+}
+
+std::vector<int> worker_cpus(int dev)
+{
+    std::vector<int> want;
+    const std::string mode = g_pipe_affinity;
+    if (mode == "gpu") {
+        char bus[64] = {0};
+        if (hipDeviceGetPCIBusId(bus, sizeof bus, dev) == hipSuccess) {
+            for (char *q = bus; *q; ++q)
+                *q = (char) tolower(*q);
+            std::string path = std::string("/sys/bus/pci/devices/") + bus + "/local_cpulist";
+            if (FILE *f = fopen(path.c_str(), "r")) {
+                char line[4096] = {0};
+                if (fgets(line, sizeof line, f))
+                    want = parse_cpulist(line);
+                fclose(f);
+            }
+        }
+        (void) hipGetLastError();
+    } else if (mode != "none" && !mode.empty()) {
+        want = parse_cpulist(mode.c_str());
+    }
+    cpu_set_t mine;
+    std::vector<int> out;
+    if (want.empty() || sched_getaffinity(0, sizeof mine, &mine) != 0)
+        return out;
+    for (int c : want)
+        if (c < CPU_SETSIZE && CPU_ISSET(c, &mine))
+            out.push_back(c);
+    return out;
+}
+
+// Large pageable operand(s): W host workers take chunks k = w, w + W, ...; per
+// chunk a worker memcpys the pageable operand(s) into a pinned buffer of its
+// own, runs one zero-copy kernel over the buffer's device mapping on its own
+// stream (a pinned or device operand is used in place) and memcpys the result
+// back once that kernel is done.  Double-buffered (default), a worker copies
+// chunk k + W into its second buffer while chunk k's kernel runs.  The
+// workers' host copies overlap each other's PCIe transfers, where
+// hipMemcpyAsync from pageable memory serialises through the runtime's own
+// bounce.  Each element is combined exactly once, by the same kernel, so the
+// bits equal every other path's.  Returns -1 when the buffers cannot be had
+// (caller stages).
 int pipelined(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext, uint32_t op,
               bool in_pg, bool io_pg, int dev, int nthreads)
 {
@@ -794,11 +879,12 @@ int pipelined(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ex
     if (!busy.owns_lock())
         return -1;      // another thread is using the set: stage instead
     const size_t half = (g_pipe_chunk.load() + 255) & ~(size_t) 255;
-    bool ready = P.half >= half;
+    const int nbuf = g_pipe_db.load() ? 2 : 1;
+    bool ready = P.half >= half && P.nbuf >= nbuf;
     for (int w = 0; ready && w < nthreads; ++w)
         ready = P.slot[w].host != nullptr;
     if (!ready) {
-        // (re)allocate every worker's slot at the current chunk size
+        // (re)allocate every worker's buffers at the current chunk size
         for (PipeSlot &sl : P.slot) {
             if (sl.s)
                 (void) hipStreamSynchronize(sl.s);
@@ -807,12 +893,16 @@ int pipelined(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ex
             sl.host = sl.dev = nullptr;
         }
         P.half = 0;
+        P.nbuf = 0;
         for (int w = 0; w < nthreads; ++w) {
             PipeSlot &sl = P.slot[w];
             if (!sl.s && hipStreamCreateWithFlags(&sl.s, hipStreamNonBlocking) != hipSuccess)
                 return -1;
+            for (hipEvent_t &e : sl.ev)
+                if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+                    return -1;
             void *h = nullptr, *hd = nullptr;
-            if (hipHostMalloc(&h, 2 * half, hipHostMallocDefault) != hipSuccess)
+            if (hipHostMalloc(&h, 2 * half * (size_t) nbuf, hipHostMallocDefault) != hipSuccess)
                 return -1;
             if (hipHostGetDevicePointer(&hd, h, 0) != hipSuccess) {
                 (void) hipHostFree(h);
@@ -822,6 +912,11 @@ int pipelined(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ex
             sl.dev = (char *) hd;
         }
         P.half = half;
+        P.nbuf = nbuf;
+    }
+    if (!P.cpus_known) {
+        P.cpus = worker_cpus(dev);
+        P.cpus_known = true;
     }
     uint64_t chunk = half / ext;
     if (chunk == 0)
@@ -829,43 +924,76 @@ int pipelined(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ex
     const uint64_t nchunks = (count + chunk - 1) / chunk;
     const int W = (int) std::min<uint64_t>((uint64_t) nthreads, nchunks);
     std::atomic<int> err{MPIX_REDOP_SUCCESS};
+    auto fail = [&](int rc) {
+        int z = MPIX_REDOP_SUCCESS;
+        err.compare_exchange_strong(z, rc);
+    };
     auto work = [&](int w) {
         PipeSlot &sl = P.slot[w];
         if (hipSetDevice(dev) != hipSuccess) {
-            int z = MPIX_REDOP_SUCCESS;
-            err.compare_exchange_strong(z, MPIX_REDOP_ERR_OTHER);
+            fail(MPIX_REDOP_ERR_OTHER);
             return;
         }
-        for (uint64_t k = (uint64_t) w; k < nchunks && err.load() == MPIX_REDOP_SUCCESS;
-             k += (uint64_t) W) {
-            const uint64_t off = k * chunk;
-            const uint64_t n = std::min(chunk, count - off);
+        char *hbuf[2] = {sl.host, sl.host + 2 * half};
+        char *dbuf[2] = {sl.dev, sl.dev + 2 * half};
+        // buffer b: copy chunk k's pageable operand(s) in, enqueue its kernel
+        auto start = [&](uint64_t k, int b) -> int {
+            const uint64_t off = k * chunk, n = std::min(chunk, count - off);
             const size_t bytes = (size_t) (n * ext);
-            const char *src_in = (const char *) in + off * ext;
-            char *dst_io = (char *) io + off * ext;
             if (in_pg)
-                memcpy(sl.host, src_in, bytes);
+                memcpy(hbuf[b], (const char *) in + off * ext, bytes);
             if (io_pg)
-                memcpy(sl.host + half, dst_io, bytes);
-            const void *kin = in_pg ? (const void *) sl.dev : (const void *) src_in;
-            void *kio = io_pg ? (void *) (sl.dev + half) : (void *) dst_io;
+                memcpy(hbuf[b] + half, (char *) io + off * ext, bytes);
+            const void *kin = in_pg ? (const void *) dbuf[b] : (const char *) in + off * ext;
+            void *kio = io_pg ? (void *) (dbuf[b] + half) : (char *) io + off * ext;
             int rc = enqueue(kin, kio, n, it, ext, op, sl.s);
-            if (rc == MPIX_REDOP_SUCCESS)
-                rc = hip_err(hipStreamSynchronize(sl.s));
-            if (rc != MPIX_REDOP_SUCCESS) {
-                int z = MPIX_REDOP_SUCCESS;
-                err.compare_exchange_strong(z, rc);
-                return;
+            return rc ? rc : hip_err(hipEventRecord(sl.ev[b], sl.s));
+        };
+        // chunk k's kernel done: its result back to the pageable inout
+        auto finish = [&](uint64_t k, int b) -> int {
+            int rc = hip_err(hipEventSynchronize(sl.ev[b]));
+            if (rc == MPIX_REDOP_SUCCESS && io_pg) {
+                const uint64_t off = k * chunk, n = std::min(chunk, count - off);
+                memcpy((char *) io + off * ext, hbuf[b] + half, (size_t) (n * ext));
             }
-            if (io_pg)
-                memcpy(dst_io, sl.host + half, bytes);
+            return rc;
+        };
+        uint64_t k = (uint64_t) w;
+        int b = 0, rc = k < nchunks ? start(k, b) : MPIX_REDOP_SUCCESS;
+        for (; k < nchunks && rc == MPIX_REDOP_SUCCESS && err.load() == MPIX_REDOP_SUCCESS;
+             k += (uint64_t) W) {
+            const uint64_t kn = k + (uint64_t) W;
+            if (nbuf == 2) {
+                if (kn < nchunks)
+                    rc = start(kn, b ^ 1);          // overlaps chunk k's kernel
+                int rc2 = finish(k, b);
+                rc = rc ? rc : rc2;
+                b ^= 1;
+            } else {
+                rc = finish(k, b);
+                if (rc == MPIX_REDOP_SUCCESS && kn < nchunks)
+                    rc = start(kn, b);
+            }
         }
+        // no kernel of this worker is left reading its buffers when the call
+        // returns, also when another worker's failure ended the loop early
+        (void) hipStreamSynchronize(sl.s);
+        if (rc != MPIX_REDOP_SUCCESS)
+            fail(rc);
     };
     std::vector<std::thread> pool;
     pool.reserve(W > 0 ? W - 1 : 0);
     for (int w = 1; w < W; ++w)
-        pool.emplace_back(work, w);
-    work(0);
+        pool.emplace_back([&, w]() {
+            if (!P.cpus.empty()) {
+                cpu_set_t set;
+                CPU_ZERO(&set);
+                CPU_SET(P.cpus[(size_t) w % P.cpus.size()], &set);
+                (void) pthread_setaffinity_np(pthread_self(), sizeof set, &set);
+            }
+            work(w);
+        });
+    work(0);        // the caller is worker 0 (its affinity is its own)
     for (std::thread &t : pool)
         t.join();
     return err.load();
@@ -1174,11 +1302,15 @@ int MPIX_Redop_finalize(void)
                 (void) hipStreamSynchronize(sl.s);
                 (void) hipStreamDestroy(sl.s);
             }
+            for (hipEvent_t e : sl.ev)
+                if (e)
+                    (void) hipEventDestroy(e);
             if (sl.host)
                 (void) hipHostFree(sl.host);
             sl = PipeSlot();
         }
         P.half = 0;
+        P.nbuf = 0;
     }
     return MPIX_REDOP_SUCCESS;
 }

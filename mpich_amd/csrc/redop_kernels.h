@@ -65,8 +65,24 @@ __device__ __forceinline__ v4u ld16u(const char *p)
     return v;
 }
 
+// 1-byte combiners may provide apply4(dword, dword): four elements at once
+template <class C, class = void> struct HasApply4 {
+    static constexpr bool value = false;
+};
+template <class C>
+struct HasApply4<C, decltype((void) C::apply4(0u, 0u))> {
+    static constexpr bool value = sizeof(typename C::unit) == 1;
+};
+
 template <class C> __device__ __forceinline__ v4u combine16(v4u a, v4u b, const Params &prm)
 {
+    if constexpr (HasApply4<C>::value) {
+        v4u r;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            r[e] = C::apply4(a[e], b[e]);
+        return r;
+    }
     using T = typename C::unit;
     constexpr int E = 16 / sizeof(T);
     struct alignas(16) Pk { T u[E]; };

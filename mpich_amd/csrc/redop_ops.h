@@ -49,17 +49,27 @@ template <typename T> struct IProd {
     using W = typename Wide<T>::type;
     static MPIX_DEV T apply(T a, T b, const Params &) { return (T) ((W) a * (W) b); }
 };
+// 1-byte logicals, four lanes per dword (SWAR, combine16 uses apply4 when a
+// combiner has it): nz(x) sets bit 7 of every non-zero byte -- the low seven
+// bits plus 0x7f carry into bit 7 exactly when one of them is set, or bit 7
+// itself is -- so each op is 4-10 VALU per 4 elements instead of ~5 per byte.
+// Byte for byte the same 0/1 results as apply().
+MPIX_DEV uint32_t nz_bytes(uint32_t x) { return (((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u; }
+
 template <typename T> struct ILand {
     using unit = T;
     static MPIX_DEV T apply(T a, T b, const Params &) { return (T) ((a != 0) & (b != 0)); }
+    static MPIX_DEV uint32_t apply4(uint32_t a, uint32_t b) { return (nz_bytes(a) & nz_bytes(b)) >> 7; }
 };
 template <typename T> struct ILor {
     using unit = T;
     static MPIX_DEV T apply(T a, T b, const Params &) { return (T) ((a != 0) | (b != 0)); }
+    static MPIX_DEV uint32_t apply4(uint32_t a, uint32_t b) { return nz_bytes(a | b) >> 7; }
 };
 template <typename T> struct ILxor {
     using unit = T;
     static MPIX_DEV T apply(T a, T b, const Params &) { return (T) ((a != 0) ^ (b != 0)); }
+    static MPIX_DEV uint32_t apply4(uint32_t a, uint32_t b) { return (nz_bytes(a) ^ nz_bytes(b)) >> 7; }
 };
 template <typename T> struct IBand {
     using unit = T;
@@ -234,15 +244,25 @@ template <typename R> struct CProdAnnexG {
 // struct complex (MPIR_OP_TYPE_GROUP(COMPLEX), op_fns.c:74-85) on fp16 parts:
 // re = c.re*b.re - c.im*b.im; im = c.im*b.re + c.re*b.im, each fp16 op
 // rounded (native _Float16, no excess precision on gfx950).
+// The four products and the two sums as packed fp16 pairs (v_pk_mul_f16 /
+// v_pk_add_f16 with operand selects): (p1, p3) = (re, im) * y.re, (p2, p4) =
+// (im, re) * y.im, z = (p1 - p2, p3 + p4) -- each lane the same single
+// correctly rounded fp16 op as the scalar form, 3 VALU per element instead of 7.
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
 struct CProdHalf {
     using unit = Cplx<_Float16>;
     static MPIX_DEV unit apply(unit x, unit y, const Params &)
     {
-        _Float16 p1 = x.re * y.re, p2 = x.im * y.im, p3 = x.im * y.re, p4 = x.re * y.im;
-        unit z;
-        z.re = p1 - p2;
-        z.im = p3 + p4;
-        return z;
+        const h2v xv = {x.re, x.im}, xs = {x.im, x.re};
+        const h2v yr = {y.re, y.re}, yi = {y.im, y.im};
+        const h2v a = xv * yr;          // (p1, p3)
+        const h2v b = xs * yi;          // (p2, p4)
+        const h2v sg = {(_Float16) -1, (_Float16) 1};
+        const h2v z = a + b * sg;       // (p1 - p2, p3 + p4): * -1 is exact
+        unit r;
+        r.re = z.x;
+        r.im = z.y;
+        return r;
     }
 };
 

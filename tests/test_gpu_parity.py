@@ -978,6 +978,40 @@ def test_pageable_worker_pipeline(R, H, oracle, threads, chunk, place):
         R.set_pageable(prev['threads'], prev['chunk_bytes'])
 
 
+_PAGEABLE_MODE = r'''
+import sys, numpy as np, torch
+sys.path.insert(0, %r)
+from mpich_amd import redop as R, handles as H
+from oracle import oracle as orc
+orc.build()
+rng = np.random.default_rng(7)
+n = (1 << 22) + 13
+a = rng.uniform(-1, 1, n).astype(np.float32); b = rng.uniform(-1, 1, n).astype(np.float32)
+e = a.copy(); orc.reduce_local(b, e, n, H.MPI_FLOAT, H.MPI_SUM)
+assert R.set_pageable(5, 256 << 10) == 0          # 64+ chunks, ragged last one
+for rep in range(2):
+    x = a.copy()
+    assert R.MPI_Reduce_local(b, x, n, H.MPI_FLOAT, H.MPI_SUM) == 0
+    assert np.array_equal(x, e), rep
+print('mode ok')
+'''
+
+
+@pytest.mark.parametrize('db,aff', [('0', 'none'), ('1', 'gpu'), ('1', '0-3,5'), ('0', 'gpu')])
+def test_pageable_worker_modes(db, aff):
+    """the workers' modes from the environment: one buffer (copy and kernel in
+    turn) or two (the next chunk copied during the kernel), pinned to the
+    GPU's NUMA node or an explicit cpulist; same bits as the oracle"""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, '-c', _PAGEABLE_MODE % root], capture_output=True,
+                       text=True, timeout=300,
+                       env=dict(os.environ, MPIX_REDOP_PAGEABLE_DB=db,
+                                MPIX_REDOP_PAGEABLE_AFFINITY=aff))
+    assert p.returncode == 0 and 'mode ok' in p.stdout, p.stdout + p.stderr
+
+
 def test_pageable_knob_errors(R):
     prev = R.get_pageable()
     assert R.set_pageable(-1, 1 << 20) == 12

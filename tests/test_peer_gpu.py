@@ -135,9 +135,8 @@ def test_cross_device_without_peer_access_stages():
 def test_nan_payloads_recorded():
     """FP SUM/PROD NaN payloads are "parity unpinned" --
     no reference test fixes them.  Records (prints) whether gfx950's results
-    carry the payload x86's loop returns (the oracle built here); asserts only
-    that a NaN operand gives a NaN.  profiles/r03_nan_payloads.json holds a
-    run's full table."""
+    carry the payload x86's loop returns (the oracle built here).
+    profiles/r03_nan_payloads.json holds a run's full table."""
     import json
     import torch
     if not torch.cuda.is_available():
@@ -149,6 +148,13 @@ def test_nan_payloads_recorded():
     summary = json.loads(p.stdout.strip().splitlines()[-1])
     print('NaN payloads vs x86:', summary)
     for k, v in summary.items():
-        if k.endswith('PROD') or k.endswith('SUM'):
-            # inf * 0 and the like make new NaNs; every NaN operand must stay NaN
-            assert v['all_gpu_results_nan'], k
+        # every NaN operand must give a NaN
+        assert v['all_gpu_results_nan'], k
+        # measured in round 3 (profiles/r03_nan_payloads.json): for fp32 and
+        # fp64 gfx950's v_add / v_mul keep the inout operand's payload,
+        # quieted, exactly as the oracle's gcc-built x86 loop does on all 55
+        # NaN pairs -- kept as a regression guard; fp16 differs where both
+        # operands are NaN (which one x86 keeps is gcc's operand order for a
+        # commutative add, not a language rule), so it is only recorded
+        if k.startswith('float32') or k.startswith('float64'):
+            assert v['identical_to_x86'] == v['nan_pairs'], (k, v)
