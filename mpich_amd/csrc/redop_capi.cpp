@@ -803,6 +803,17 @@ int bounced(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext,
 // bounce.  Each element is combined exactly once, by the same kernel, so the
 // bits equal every other path's.  Returns -1 when the slots cannot be had
 // (caller stages).
+struct PipeTrace {
+    int64_t *ns;        // 5 per chunk, or nullptr
+    std::chrono::steady_clock::time_point t0;
+};
+inline void pipe_mark(PipeTrace *t, int, uint64_t k, int what)
+{
+    if (t->ns)
+        t->ns[k * 5 + (uint64_t) what] = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                             std::chrono::steady_clock::now() - t->t0).count();
+}
+
 // CPUs of the GPU's NUMA node (sysfs local_cpulist of its PCI function),
 // intersected with this process's affinity; or an explicit "a-b,c" list
 std::vector<int> parse_cpulist(const char *txt)
@@ -924,6 +935,13 @@ int pipelined(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ex
     const uint64_t nchunks = (count + chunk - 1) / chunk;
     const int W = (int) std::min<uint64_t>((uint64_t) nthreads, nchunks);
     std::atomic<int> err{MPIX_REDOP_SUCCESS};
+    // MPIX_REDOP_PIPE_TRACE=1: per chunk the host times (ns from the call's
+    // start) of copy-in start / end, wait start / end, copy-out end, printed
+    // as one JSON line to stderr (tools/pageable_probe.py reads them)
+    static const bool trace_on = getenv("MPIX_REDOP_PIPE_TRACE") != nullptr;
+    std::vector<int64_t> trace_buf(trace_on ? nchunks * 5 : 0, -1);
+    PipeTrace trv{trace_on ? trace_buf.data() : nullptr, std::chrono::steady_clock::now()};
+    PipeTrace *tr = &trv;
     auto fail = [&](int rc) {
         int z = MPIX_REDOP_SUCCESS;
         err.compare_exchange_strong(z, rc);
@@ -940,10 +958,12 @@ int pipelined(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ex
         auto start = [&](uint64_t k, int b) -> int {
             const uint64_t off = k * chunk, n = std::min(chunk, count - off);
             const size_t bytes = (size_t) (n * ext);
+            pipe_mark(tr, w, k, 0);
             if (in_pg)
                 memcpy(hbuf[b], (const char *) in + off * ext, bytes);
             if (io_pg)
                 memcpy(hbuf[b] + half, (char *) io + off * ext, bytes);
+            pipe_mark(tr, w, k, 1);
             const void *kin = in_pg ? (const void *) dbuf[b] : (const char *) in + off * ext;
             void *kio = io_pg ? (void *) (dbuf[b] + half) : (char *) io + off * ext;
             int rc = enqueue(kin, kio, n, it, ext, op, sl.s);
@@ -951,11 +971,14 @@ int pipelined(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ex
         };
         // chunk k's kernel done: its result back to the pageable inout
         auto finish = [&](uint64_t k, int b) -> int {
+            pipe_mark(tr, w, k, 2);
             int rc = hip_err(hipEventSynchronize(sl.ev[b]));
+            pipe_mark(tr, w, k, 3);
             if (rc == MPIX_REDOP_SUCCESS && io_pg) {
                 const uint64_t off = k * chunk, n = std::min(chunk, count - off);
                 memcpy((char *) io + off * ext, hbuf[b] + half, (size_t) (n * ext));
             }
+            pipe_mark(tr, w, k, 4);
             return rc;
         };
         uint64_t k = (uint64_t) w;
@@ -996,6 +1019,13 @@ int pipelined(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ex
     work(0);        // the caller is worker 0 (its affinity is its own)
     for (std::thread &t : pool)
         t.join();
+    if (trace_on) {
+        fprintf(stderr, "{\"pipe_trace\": {\"W\": %d, \"chunk\": %zu, \"nbuf\": %d, \"ns\": [", W,
+                half, nbuf);
+        for (uint64_t i = 0; i < nchunks * 5; ++i)
+            fprintf(stderr, "%s%lld", i ? "," : "", (long long) trace_buf[i]);
+        fprintf(stderr, "]}}\n");
+    }
     return err.load();
 }
 

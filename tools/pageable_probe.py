@@ -29,6 +29,30 @@ sys.path.insert(0, ROOT)
 CONFIGS = [(8, 16, 0, 'none'), (8, 16, 1, 'none'), (8, 8, 1, 'none'), (8, 16, 1, 'gpu'),
            (8, 8, 1, 'gpu'), (12, 8, 1, 'gpu'), (15, 8, 1, 'gpu'), (15, 16, 1, 'gpu'),
            (12, 16, 0, 'gpu')]
+if os.environ.get('PAGEABLE_CONFIGS'):      # "W:chunkMiB:db:aff,..."
+    CONFIGS = [tuple(int(x) if i < 3 else x for i, x in enumerate(c.split(':')))
+               for c in os.environ['PAGEABLE_CONFIGS'].split(',')]
+
+
+def trace_summary(stderr):
+    """the library's MPIX_REDOP_PIPE_TRACE line of the last call: per chunk
+    copy-in, wait for the kernel, copy-out (ms summed over chunks) and the
+    call's span"""
+    line = [ln for ln in stderr.splitlines() if ln.startswith('{"pipe_trace"')]
+    if not line:
+        return None
+    t = json.loads(line[-1])['pipe_trace']
+    ns = t['ns']
+    k = len(ns) // 5
+    cin = sum(ns[5 * i + 1] - ns[5 * i] for i in range(k)) / 1e6
+    wait = sum(ns[5 * i + 3] - ns[5 * i + 2] for i in range(k)) / 1e6
+    cout = sum(ns[5 * i + 4] - ns[5 * i + 3] for i in range(k)) / 1e6
+    span = max(ns) / 1e6
+    first_wait = min(ns[5 * i + 2] for i in range(k)) / 1e6
+    return dict(chunks=k, W=t['W'], nbuf=t['nbuf'], span_ms=round(span, 2),
+                copy_in_ms_sum=round(cin, 2), wait_ms_sum=round(wait, 2),
+                copy_out_ms_sum=round(cout, 2), first_wait_at_ms=round(first_wait, 2),
+                worker_busy_frac=round((cin + cout) / (t['W'] * span), 3))
 
 
 def memcpy_rate(src, dst, threads, chunk=16 << 20):
@@ -107,11 +131,15 @@ def sweep(path):
         for W, ck, db, aff in CONFIGS:
             env = dict(os.environ, MPIX_REDOP_PAGEABLE_THREADS=str(W),
                        MPIX_REDOP_PAGEABLE_CHUNK=str(ck << 20), MPIX_REDOP_PAGEABLE_DB=str(db),
-                       MPIX_REDOP_PAGEABLE_AFFINITY=aff)
+                       MPIX_REDOP_PAGEABLE_AFFINITY=aff, MPIX_REDOP_PIPE_TRACE='1')
             p = subprocess.run([sys.executable, __file__, 'one'], env=env, capture_output=True,
                                text=True, timeout=300)
-            line = p.stdout.strip().splitlines()[-1] if p.returncode == 0 and p.stdout.strip() \
-                else json.dumps(dict(W=W, chunk_MiB=ck, db=db, aff=aff, error=p.stderr[-500:]))
+            if p.returncode == 0 and p.stdout.strip():
+                d = json.loads(p.stdout.strip().splitlines()[-1])
+                d['trace_last_call'] = trace_summary(p.stderr)
+                line = json.dumps(d)
+            else:
+                line = json.dumps(dict(W=W, chunk_MiB=ck, db=db, aff=aff, error=p.stderr[-500:]))
             f.write(line + '\n')
             f.flush()
             print(line, flush=True)
