@@ -1057,32 +1057,50 @@ struct DeviceGuard {
 std::atomic<int8_t> g_peer[kMaxDev][kMaxDev];
 std::mutex g_peer_mu;
 
-bool peer_access(int dev, int owner)
+enum PeerState : int8_t { kPeerUnknown = 0, kPeerDirect = 1, kPeerNone = 2, kPeerUnsure = 3 };
+
+// kPeerDirect: kernels on `dev` may read `owner`'s memory; kPeerNone: the
+// runtime says they may not (or MPIX_REDOP_PEER=stage); kPeerUnsure: the pair
+// cannot even be asked (an owner index this process does not see, e.g. memory
+// mapped from another process's GPU under a restricted HIP_VISIBLE_DEVICES) --
+// used as it is, as the IPC mapping that produced it allows
+PeerState peer_state(int dev, int owner)
 {
     if (dev == owner)
-        return true;
-    if (dev < 0 || owner < 0 || dev >= kMaxDev || owner >= kMaxDev)
-        return false;
+        return kPeerDirect;
+    int ndev = 0;
+    if (dev < 0 || owner < 0 || dev >= kMaxDev || owner >= kMaxDev ||
+        hipGetDeviceCount(&ndev) != hipSuccess || dev >= ndev || owner >= ndev) {
+        (void) hipGetLastError();
+        return kPeerUnsure;
+    }
     int8_t st = g_peer[dev][owner].load(std::memory_order_acquire);
     if (st)
-        return st == 1;
+        return (PeerState) st;
     std::lock_guard<std::mutex> l(g_peer_mu);
     st = g_peer[dev][owner].load(std::memory_order_acquire);
     if (st)
-        return st == 1;
+        return (PeerState) st;
     const char *force = getenv("MPIX_REDOP_PEER");
+    PeerState r;
     int can = 0;
-    bool ok = !(force && strcmp(force, "stage") == 0) &&
-              hipDeviceCanAccessPeer(&can, dev, owner) == hipSuccess && can;
-    if (ok) {
+    if (force && strcmp(force, "stage") == 0) {
+        r = kPeerNone;
+    } else if (hipDeviceCanAccessPeer(&can, dev, owner) != hipSuccess) {
+        r = kPeerUnsure;
+    } else if (!can) {
+        r = kPeerNone;
+    } else {
         DeviceGuard g(dev);
         hipError_t e = hipDeviceEnablePeerAccess(owner, 0);
-        ok = e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled;
+        r = (e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled) ? kPeerDirect : kPeerNone;
     }
     (void) hipGetLastError();       // "already enabled" is sticky otherwise
-    g_peer[dev][owner].store(ok ? 1 : 2, std::memory_order_release);
-    return ok;
+    g_peer[dev][owner].store((int8_t) r, std::memory_order_release);
+    return r;
 }
+
+bool peer_access(int dev, int owner) { return peer_state(dev, owner) == kPeerDirect; }
 
 // The device a stream's kernels run on (the null stream: the current one).
 int stream_device(hipStream_t s)
@@ -1114,7 +1132,7 @@ bool reachable(const void *p, hipStream_t s, int *launch, const void **devptr)
         return true;
     if (*launch == -2)
         *launch = stream_device(s);
-    return peer_access(*launch, owner);
+    return peer_state(*launch, owner) != kPeerNone;
 }
 
 // ------------------------------------------- derived targets as runs
@@ -1385,7 +1403,8 @@ int MPIX_Reduce_local(const void *inbuf, void *inoutbuf, MPIX_Aint count, MPIX_D
     bool io_stage = wio == Where::Pageable || (wio == Where::Pinned && !zc);
     int dev = wio == Where::Device ? dio : (win == Where::Device ? din : cur);
     DeviceGuard guard(dev);
-    if (win == Where::Device && wio == Where::Device && din != dio && !peer_access(dio, din))
+    if (win == Where::Device && wio == Where::Device && din != dio &&
+        peer_state(dio, din) == kPeerNone)
         // operands on two devices without peer access: the kernel runs where
         // inout lives and `in` is copied over in chunks (hipMemcpyPeerAsync);
         // MPIX_EQUAL's one header covers the whole message: copied whole
