@@ -9,6 +9,7 @@
 // MPIX_Redop_is_supported() says so, so the caller keeps its own op table
 // for it (exactly how reduce_local.c:66-76 falls back when yaksa declines).
 #include <hip/hip_runtime_api.h>
+#include <immintrin.h>
 
 #include <ctype.h>
 #include <pthread.h>
@@ -803,6 +804,50 @@ int bounced(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext,
 // bounce.  Each element is combined exactly once, by the same kernel, so the
 // bits equal every other path's.  Returns -1 when the slots cannot be had
 // (caller stages).
+// Copy into a pinned buffer the GPU is about to read over PCIe.  With plain
+// stores the lines sit dirty in the CPU caches and every PCIe read of them is
+// a snoop hit; non-temporal stores send them to DRAM (glibc's memcpy switches
+// to those only above its own, L3-sized threshold, above our chunk size).
+// MPIX_REDOP_PAGEABLE_NT=0 uses memcpy.
+std::atomic<int> g_pipe_nt{-1};     // -1: not decided yet
+__attribute__((target("avx2"))) static void copy_nt_avx2(char *dst, const char *src, size_t n)
+{
+    size_t head = (32 - ((uintptr_t) dst & 31)) & 31;
+    if (head > n)
+        head = n;
+    memcpy(dst, src, head);
+    dst += head;
+    src += head;
+    n -= head;
+    size_t i = 0;
+    for (; i + 128 <= n; i += 128) {
+        __m256i a = _mm256_loadu_si256((const __m256i *) (src + i));
+        __m256i b = _mm256_loadu_si256((const __m256i *) (src + i + 32));
+        __m256i c = _mm256_loadu_si256((const __m256i *) (src + i + 64));
+        __m256i d = _mm256_loadu_si256((const __m256i *) (src + i + 96));
+        _mm256_stream_si256((__m256i *) (dst + i), a);
+        _mm256_stream_si256((__m256i *) (dst + i + 32), b);
+        _mm256_stream_si256((__m256i *) (dst + i + 64), c);
+        _mm256_stream_si256((__m256i *) (dst + i + 96), d);
+    }
+    _mm_sfence();
+    memcpy(dst + i, src + i, n - i);
+}
+
+void copy_to_pinned(char *dst, const char *src, size_t n)
+{
+    int nt = g_pipe_nt.load(std::memory_order_relaxed);
+    if (nt < 0) {
+        const char *e = getenv("MPIX_REDOP_PAGEABLE_NT");
+        nt = (e ? atoi(e) != 0 : true) && __builtin_cpu_supports("avx2");
+        g_pipe_nt.store(nt);
+    }
+    if (nt)
+        copy_nt_avx2(dst, src, n);
+    else
+        memcpy(dst, src, n);
+}
+
 struct PipeTrace {
     int64_t *ns;        // 5 per chunk, or nullptr
     std::chrono::steady_clock::time_point t0;
@@ -960,9 +1005,9 @@ int pipelined(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ex
             const size_t bytes = (size_t) (n * ext);
             pipe_mark(tr, w, k, 0);
             if (in_pg)
-                memcpy(hbuf[b], (const char *) in + off * ext, bytes);
+                copy_to_pinned(hbuf[b], (const char *) in + off * ext, bytes);
             if (io_pg)
-                memcpy(hbuf[b] + half, (char *) io + off * ext, bytes);
+                copy_to_pinned(hbuf[b] + half, (char *) io + off * ext, bytes);
             pipe_mark(tr, w, k, 1);
             const void *kin = in_pg ? (const void *) dbuf[b] : (const char *) in + off * ext;
             void *kio = io_pg ? (void *) (dbuf[b] + half) : (char *) io + off * ext;

@@ -8,6 +8,7 @@ at first use):
   chunk  MPIX_REDOP_PAGEABLE_CHUNK     bytes per chunk
   db     MPIX_REDOP_PAGEABLE_DB        1: copy the next chunk during the kernel
   aff    MPIX_REDOP_PAGEABLE_AFFINITY  none | gpu (CPUs of the GPU's NUMA node)
+  nt     MPIX_REDOP_PAGEABLE_NT        1: non-temporal stores into the pinned buffers
 
 Beside each: the host memcpy rate of one thread and of W threads (numpy
 copyto on disjoint 16 MiB slices, pageable -> page-locked), and the PCIe
@@ -29,8 +30,8 @@ sys.path.insert(0, ROOT)
 CONFIGS = [(8, 16, 0, 'none'), (8, 16, 1, 'none'), (8, 8, 1, 'none'), (8, 16, 1, 'gpu'),
            (8, 8, 1, 'gpu'), (12, 8, 1, 'gpu'), (15, 8, 1, 'gpu'), (15, 16, 1, 'gpu'),
            (12, 16, 0, 'gpu')]
-if os.environ.get('PAGEABLE_CONFIGS'):      # "W:chunkMiB:db:aff,..."
-    CONFIGS = [tuple(int(x) if i < 3 else x for i, x in enumerate(c.split(':')))
+if os.environ.get('PAGEABLE_CONFIGS'):      # "W:chunkMiB:db:aff[:nt],..."
+    CONFIGS = [tuple(int(x) if i in (0, 1, 2, 4) else x for i, x in enumerate(c.split(':')))
                for c in os.environ['PAGEABLE_CONFIGS'].split(',')]
 
 
@@ -103,6 +104,7 @@ def one():
     W = pg['threads']
     out = dict(W=W, chunk_MiB=pg['chunk_bytes'] >> 20, db=os.environ.get('MPIX_REDOP_PAGEABLE_DB', '1'),
                aff=os.environ.get('MPIX_REDOP_PAGEABLE_AFFINITY', 'none'),
+               nt=os.environ.get('MPIX_REDOP_PAGEABLE_NT', '1'),
                ms=round(ts[len(ts) // 2] * 1e3, 2), best_ms=round(ts[0] * 1e3, 2),
                GiBs=round(3 * n * 4 / ts[len(ts) // 2] / (1 << 30), 2), checked=ok,
                memcpy_1thread_GBs=memcpy_rate(b, pinned, 1),
@@ -128,10 +130,13 @@ def one():
 
 def sweep(path):
     with open(path, 'w') as f:
-        for W, ck, db, aff in CONFIGS:
+        for cfg in CONFIGS:
+            W, ck, db, aff = cfg[:4]
+            nt = cfg[4] if len(cfg) > 4 else 1
             env = dict(os.environ, MPIX_REDOP_PAGEABLE_THREADS=str(W),
                        MPIX_REDOP_PAGEABLE_CHUNK=str(ck << 20), MPIX_REDOP_PAGEABLE_DB=str(db),
-                       MPIX_REDOP_PAGEABLE_AFFINITY=aff, MPIX_REDOP_PIPE_TRACE='1')
+                       MPIX_REDOP_PAGEABLE_AFFINITY=aff, MPIX_REDOP_PAGEABLE_NT=str(nt),
+                       MPIX_REDOP_PIPE_TRACE='1')
             p = subprocess.run([sys.executable, __file__, 'one'], env=env, capture_output=True,
                                text=True, timeout=300)
             if p.returncode == 0 and p.stdout.strip():
