@@ -269,7 +269,17 @@ int MPIX_Comm_barrier(MPIX_Comm comm);
  * place, without first copying its input into the pull window.  Collective;
  * MPI_ERR_OTHER on every rank if no verified mapping could be made.
  * MPIX_Comm_free_shared is collective too; the memory itself is released by
- * MPIX_Comm_free. */
+ * MPIX_Comm_free.
+ *
+ * Device memory a communicator keeps until MPIX_Comm_free (so that a freed
+ * allocation's identity never comes back while a peer may still hold a
+ * mapping of it -- DESIGN.md, "Why windows"): shared allocations after
+ * MPIX_Comm_free_shared; pull windows that failed verification (at most 3
+ * per growth, each header + message size); outgrown pull windows (growth
+ * doubles, so at most the final window's size again).  A communicator whose
+ * ranks are not all on one node (host name and boot id exchanged once,
+ * before the first window) allocates no window at all and runs the pulls'
+ * transport forms. */
 int MPIX_Comm_alloc_shared(MPIX_Comm comm, size_t bytes, void **ptr);
 int MPIX_Comm_free_shared(MPIX_Comm comm, void *ptr);
 
