@@ -271,6 +271,14 @@ std::atomic<size_t> g_pipe_chunk{(size_t) 16 << 20};
 // "64-127"; "none" leaves them where the scheduler puts them)
 std::atomic<bool> g_pipe_db{true};
 std::string g_pipe_affinity = "none";
+// MPIX_REDOP_PAGEABLE_MODE=wave: all workers copy the same chunk in together
+// (each a slice), ONE zero-copy kernel per chunk runs while they copy the next
+// one in and the one before out -- three pinned chunk buffers in rotation.
+// Per-chunk zero-copy kernels pay a fixed ramp of ~0.16 ms each
+// (profiles/r03_pinned_chunks.json), so this form can use large chunks without
+// a long pipeline fill.  "worker" (default until measured otherwise): each
+// worker its own chunks, as above.
+std::atomic<int> g_pipe_wave{0};
 // Support-predicate knobs, the pattern of MPIR_CVAR_ENABLE_YAKSA_REDUCTION and
 // MPIR_CVAR_YAKSA_REDUCTION_THRESHOLD (typerep_yaksa_pack.c:44-64,229-240):
 // MPIX_REDOP_ENABLE=0 makes every predicate answer 0 (the caller keeps its CPU
@@ -322,6 +330,8 @@ void read_env()
     }
     if (const char *s = getenv("MPIX_REDOP_PAGEABLE_DB"))
         g_pipe_db = atoi(s) != 0;
+    if (const char *s = getenv("MPIX_REDOP_PAGEABLE_MODE"))
+        g_pipe_wave = strcmp(s, "wave") == 0;
     if (const char *s = getenv("MPIX_REDOP_PAGEABLE_AFFINITY"))
         g_pipe_affinity = s;
     if (const char *s = getenv("MPIX_REDOP_PAGEABLE_CHUNK")) {
@@ -386,6 +396,11 @@ struct PipeSlot {
 struct PipeSet {
     std::mutex mu;
     PipeSlot slot[16];
+    // wave mode: 3 chunk buffers (in half + inout half each), one stream
+    char *ring = nullptr, *ring_dev = nullptr;
+    size_t ring_half = 0;
+    hipStream_t ring_s = nullptr;
+    hipEvent_t ring_ev[3] = {nullptr, nullptr, nullptr};
     size_t half = 0;        // slot half size; slots [0, threads) hold host != nullptr
     int nbuf = 0;           // buffers per worker (2: double-buffered)
     bool cpus_known = false;
@@ -1074,6 +1089,155 @@ int pipelined(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ex
     return err.load();
 }
 
+// Spin barrier for the wave workers (sense reversal; yields while waiting).
+struct SpinBarrier {
+    std::atomic<int> left;
+    std::atomic<int> gen{0};
+    const int n;
+    explicit SpinBarrier(int n_) : left(n_), n(n_) {}
+    void wait()
+    {
+        const int g = gen.load(std::memory_order_acquire);
+        if (left.fetch_sub(1, std::memory_order_acq_rel) == 1) {
+            left.store(n, std::memory_order_relaxed);
+            gen.fetch_add(1, std::memory_order_release);
+            return;
+        }
+        while (gen.load(std::memory_order_acquire) == g)
+            std::this_thread::yield();
+    }
+};
+
+// Wave mode (see g_pipe_wave).  Step s: the caller launches the kernel of
+// chunk s - 1 (its copy-in finished in step s - 1); every worker copies its
+// slice of chunk s in and, once chunk s - 2's kernel is done, its slice of
+// chunk s - 2 out; then all meet.  Buffer s % 3 held chunk s - 3, whose
+// copy-out ended in step s - 1.  Same kernel per element, same bits.
+// Returns -1 when the buffers cannot be had (caller stages).
+int waved(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext, uint32_t op,
+          bool in_pg, bool io_pg, int dev, int nthreads)
+{
+    if (dev < 0 || dev >= kMaxDev)
+        return -1;
+    PipeSet &P = g_pipes[dev];
+    std::unique_lock<std::mutex> busy(P.mu, std::try_to_lock);
+    if (!busy.owns_lock())
+        return -1;
+    const size_t half = (g_pipe_chunk.load() + 255) & ~(size_t) 255;
+    if (P.ring_half < half) {
+        if (P.ring_s)
+            (void) hipStreamSynchronize(P.ring_s);
+        if (P.ring)
+            (void) hipHostFree(P.ring);
+        P.ring = P.ring_dev = nullptr;
+        P.ring_half = 0;
+        if (!P.ring_s && hipStreamCreateWithFlags(&P.ring_s, hipStreamNonBlocking) != hipSuccess)
+            return -1;
+        for (hipEvent_t &e : P.ring_ev)
+            if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+                return -1;
+        void *h = nullptr, *hd = nullptr;
+        if (hipHostMalloc(&h, 3 * 2 * half, hipHostMallocDefault) != hipSuccess)
+            return -1;
+        if (hipHostGetDevicePointer(&hd, h, 0) != hipSuccess) {
+            (void) hipHostFree(h);
+            return -1;
+        }
+        P.ring = (char *) h;
+        P.ring_dev = (char *) hd;
+        P.ring_half = half;
+    }
+    if (!P.cpus_known) {
+        P.cpus = worker_cpus(dev);
+        P.cpus_known = true;
+    }
+    const uint64_t chunk = half / ext;
+    if (chunk == 0)
+        return -1;
+    const int64_t n = (int64_t) ((count + chunk - 1) / chunk);
+    const int W = nthreads < 1 ? 1 : nthreads;
+    SpinBarrier bar(W);
+    std::atomic<int> err{MPIX_REDOP_SUCCESS};
+    auto fail = [&](int rc) {
+        int z = MPIX_REDOP_SUCCESS;
+        err.compare_exchange_strong(z, rc);
+    };
+    auto span = [&](int64_t k, uint64_t *off, uint64_t *cnt) {
+        *off = (uint64_t) k * chunk;
+        *cnt = std::min<uint64_t>(chunk, count - *off);
+    };
+    // worker w's slice of a chunk of `bytes`: 4 KiB-aligned parts
+    auto slice = [&](int w, size_t bytes, size_t *lo, size_t *len) {
+        size_t per = ((bytes + (size_t) W - 1) / (size_t) W + 4095) & ~(size_t) 4095;
+        *lo = std::min(bytes, per * (size_t) w);
+        *len = std::min(bytes - *lo, per);
+    };
+    auto work = [&](int w) {
+        if (hipSetDevice(dev) != hipSuccess) {
+            fail(MPIX_REDOP_ERR_OTHER);
+        }
+        for (int64_t st = 0; st <= n + 1; ++st) {
+            if (w == 0 && st >= 1 && st - 1 < n && err.load() == MPIX_REDOP_SUCCESS) {
+                uint64_t off, cnt;
+                span(st - 1, &off, &cnt);
+                const int b = (int) ((st - 1) % 3);
+                char *d = P.ring_dev + (size_t) b * 2 * half;
+                const void *kin = in_pg ? (const void *) d : (const char *) in + off * ext;
+                void *kio = io_pg ? (void *) (d + half) : (char *) io + off * ext;
+                int rc = enqueue(kin, kio, cnt, it, ext, op, P.ring_s);
+                if (rc == MPIX_REDOP_SUCCESS)
+                    rc = hip_err(hipEventRecord(P.ring_ev[b], P.ring_s));
+                if (rc)
+                    fail(rc);
+            }
+            if (st < n && err.load() == MPIX_REDOP_SUCCESS) {       // copy chunk st in
+                uint64_t off, cnt;
+                span(st, &off, &cnt);
+                char *h = P.ring + (size_t) (st % 3) * 2 * half;
+                size_t lo, len;
+                slice(w, (size_t) (cnt * ext), &lo, &len);
+                if (len && in_pg)
+                    copy_to_pinned(h + lo, (const char *) in + off * ext + lo, len);
+                if (len && io_pg)
+                    copy_to_pinned(h + half + lo, (const char *) io + off * ext + lo, len);
+            }
+            if (st >= 2 && st - 2 < n && err.load() == MPIX_REDOP_SUCCESS) {   // chunk st-2 out
+                const int b = (int) ((st - 2) % 3);
+                int rc = hip_err(hipEventSynchronize(P.ring_ev[b]));
+                if (rc)
+                    fail(rc);
+                else if (io_pg) {
+                    uint64_t off, cnt;
+                    span(st - 2, &off, &cnt);
+                    size_t lo, len;
+                    slice(w, (size_t) (cnt * ext), &lo, &len);
+                    if (len)
+                        memcpy((char *) io + off * ext + lo, P.ring + (size_t) b * 2 * half + half + lo,
+                               len);
+                }
+            }
+            bar.wait();
+        }
+    };
+    std::vector<std::thread> pool;
+    pool.reserve((size_t) W - 1);
+    for (int w = 1; w < W; ++w)
+        pool.emplace_back([&, w]() {
+            if (!P.cpus.empty()) {
+                cpu_set_t set;
+                CPU_ZERO(&set);
+                CPU_SET(P.cpus[(size_t) w % P.cpus.size()], &set);
+                (void) pthread_setaffinity_np(pthread_self(), sizeof set, &set);
+            }
+            work(w);
+        });
+    work(0);
+    for (std::thread &t : pool)
+        t.join();
+    (void) hipStreamSynchronize(P.ring_s);      // nothing left reading the buffers
+    return err.load();
+}
+
 struct DeviceGuard {
     int prev = -1;
     explicit DeviceGuard(int dev)
@@ -1387,7 +1551,7 @@ int MPIX_Redop_finalize(void)
     for (int i = 0; i < kMaxDev; ++i) {     // the process-wide pageable worker slots
         PipeSet &P = g_pipes[i];
         std::lock_guard<std::mutex> l(P.mu);
-        if (!P.slot[0].s && !P.slot[0].host)
+        if (!P.slot[0].s && !P.slot[0].host && !P.ring && !P.ring_s)
             continue;
         DeviceGuard g(i);
         for (PipeSlot &sl : P.slot) {
@@ -1404,6 +1568,20 @@ int MPIX_Redop_finalize(void)
         }
         P.half = 0;
         P.nbuf = 0;
+        if (P.ring_s) {
+            (void) hipStreamSynchronize(P.ring_s);
+            (void) hipStreamDestroy(P.ring_s);
+        }
+        for (hipEvent_t &e : P.ring_ev)
+            if (e) {
+                (void) hipEventDestroy(e);
+                e = nullptr;
+            }
+        if (P.ring)
+            (void) hipHostFree(P.ring);
+        P.ring = P.ring_dev = nullptr;
+        P.ring_half = 0;
+        P.ring_s = nullptr;
     }
     return MPIX_REDOP_SUCCESS;
 }
@@ -1473,14 +1651,16 @@ int MPIX_Reduce_local(const void *inbuf, void *inoutbuf, MPIX_Aint count, MPIX_D
         return set_err(equal_whole(in_stage ? inbuf : pin, io_stage ? inoutbuf : (void *) pio,
                                    (uint64_t) count, in_stage, io_stage, dev));
     const int pipe_threads = g_pipe_threads.load();
+    const bool wave = g_pipe_wave.load() != 0;
     if (pageable && zc && pipe_threads > 0 &&
-        (uint64_t) count * ext >= 2 * (uint64_t) pipe_threads * g_pipe_chunk.load()) {
+        (uint64_t) count * ext >= (wave ? 4 : 2 * (uint64_t) pipe_threads) * g_pipe_chunk.load()) {
         // pageable operands through the workers' pinned slots; a pinned
         // operand is used through its device mapping
-        rc = pipelined(win == Where::Pageable ? inbuf : pin,
-                       wio == Where::Pageable ? inoutbuf : (void *) pio, (uint64_t) count, it, ext,
-                       (uint32_t) op, win == Where::Pageable, wio == Where::Pageable, dev,
-                       pipe_threads);
+        rc = (wave ? waved : pipelined)(win == Where::Pageable ? inbuf : pin,
+                                        wio == Where::Pageable ? inoutbuf : (void *) pio,
+                                        (uint64_t) count, it, ext, (uint32_t) op,
+                                        win == Where::Pageable, wio == Where::Pageable, dev,
+                                        pipe_threads);
         if (rc >= 0)
             return set_err(rc);
     }

@@ -9,6 +9,7 @@ at first use):
   db     MPIX_REDOP_PAGEABLE_DB        1: copy the next chunk during the kernel
   aff    MPIX_REDOP_PAGEABLE_AFFINITY  none | gpu (CPUs of the GPU's NUMA node)
   nt     MPIX_REDOP_PAGEABLE_NT        1: non-temporal stores into the pinned buffers
+  mode   MPIX_REDOP_PAGEABLE_MODE      worker (own chunks) | wave (all on one chunk)
 
 Beside each: the host memcpy rate of one thread and of W threads (numpy
 copyto on disjoint 16 MiB slices, pageable -> page-locked), and the PCIe
@@ -30,7 +31,7 @@ sys.path.insert(0, ROOT)
 CONFIGS = [(8, 16, 0, 'none'), (8, 16, 1, 'none'), (8, 8, 1, 'none'), (8, 16, 1, 'gpu'),
            (8, 8, 1, 'gpu'), (12, 8, 1, 'gpu'), (15, 8, 1, 'gpu'), (15, 16, 1, 'gpu'),
            (12, 16, 0, 'gpu')]
-if os.environ.get('PAGEABLE_CONFIGS'):      # "W:chunkMiB:db:aff[:nt],..."
+if os.environ.get('PAGEABLE_CONFIGS'):      # "W:chunkMiB:db:aff[:nt[:mode]],..."
     CONFIGS = [tuple(int(x) if i in (0, 1, 2, 4) else x for i, x in enumerate(c.split(':')))
                for c in os.environ['PAGEABLE_CONFIGS'].split(',')]
 
@@ -105,6 +106,7 @@ def one():
     out = dict(W=W, chunk_MiB=pg['chunk_bytes'] >> 20, db=os.environ.get('MPIX_REDOP_PAGEABLE_DB', '1'),
                aff=os.environ.get('MPIX_REDOP_PAGEABLE_AFFINITY', 'none'),
                nt=os.environ.get('MPIX_REDOP_PAGEABLE_NT', '1'),
+               mode=os.environ.get('MPIX_REDOP_PAGEABLE_MODE', 'worker'),
                ms=round(ts[len(ts) // 2] * 1e3, 2), best_ms=round(ts[0] * 1e3, 2),
                GiBs=round(3 * n * 4 / ts[len(ts) // 2] / (1 << 30), 2), checked=ok,
                memcpy_1thread_GBs=memcpy_rate(b, pinned, 1),
@@ -133,7 +135,8 @@ def sweep(path):
         for cfg in CONFIGS:
             W, ck, db, aff = cfg[:4]
             nt = cfg[4] if len(cfg) > 4 else 1
-            env = dict(os.environ, MPIX_REDOP_PAGEABLE_THREADS=str(W),
+            mode = cfg[5] if len(cfg) > 5 else 'worker'
+            env = dict(os.environ, MPIX_REDOP_PAGEABLE_THREADS=str(W), MPIX_REDOP_PAGEABLE_MODE=mode,
                        MPIX_REDOP_PAGEABLE_CHUNK=str(ck << 20), MPIX_REDOP_PAGEABLE_DB=str(db),
                        MPIX_REDOP_PAGEABLE_AFFINITY=aff, MPIX_REDOP_PAGEABLE_NT=str(nt),
                        MPIX_REDOP_PIPE_TRACE='1')
