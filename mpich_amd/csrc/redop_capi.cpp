@@ -1154,7 +1154,31 @@ int waved(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext, u
     const uint64_t chunk = half / ext;
     if (chunk == 0)
         return -1;
-    const int64_t n = (int64_t) ((count + chunk - 1) / chunk);
+    // chunk sizes ramp up (chunk/8, /4, /2) so the first kernel starts after a
+    // short copy-in, and down again at the end so the last copy-out is short;
+    // full chunks in between.  Offsets and counts in elements.
+    std::vector<std::pair<uint64_t, uint64_t>> chunks;
+    {
+        uint64_t off = 0;
+        for (int r = 3; r >= 1 && off < count; --r) {
+            const uint64_t c = std::max<uint64_t>(chunk >> r, 1);
+            const uint64_t m = std::min(c, count - off);
+            chunks.emplace_back(off, m);
+            off += m;
+        }
+        const uint64_t tail_split = chunk;      // the last full chunk's worth goes in halves
+        while (count - off > chunk + tail_split) {
+            chunks.emplace_back(off, chunk);
+            off += chunk;
+        }
+        for (int r = 1; off < count; r = r < 3 ? r + 1 : 3) {
+            const uint64_t c = std::max<uint64_t>(chunk >> r, 1);
+            const uint64_t m = (count - off <= c || r == 3) ? std::min(count - off, chunk) : c;
+            chunks.emplace_back(off, m);
+            off += m;
+        }
+    }
+    const int64_t n = (int64_t) chunks.size();
     const int W = nthreads < 1 ? 1 : nthreads;
     SpinBarrier bar(W);
     std::atomic<int> err{MPIX_REDOP_SUCCESS};
@@ -1163,8 +1187,8 @@ int waved(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext, u
         err.compare_exchange_strong(z, rc);
     };
     auto span = [&](int64_t k, uint64_t *off, uint64_t *cnt) {
-        *off = (uint64_t) k * chunk;
-        *cnt = std::min<uint64_t>(chunk, count - *off);
+        *off = chunks[(size_t) k].first;
+        *cnt = chunks[(size_t) k].second;
     };
     // worker w's slice of a chunk of `bytes`: 4 KiB-aligned parts
     auto slice = [&](int w, size_t bytes, size_t *lo, size_t *len) {

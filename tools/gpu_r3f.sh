@@ -13,12 +13,12 @@ step() {    # name timeout cmd...: stop the script on a fault / abort / time lim
     return 0
 }
 step tests 300 python3 -u -m pytest -q -x --timeout 200 --timeout-method thread -p no:cacheprovider tests/test_gpu_parity.py -k "pageable or host"
-step pageable 900 env PAGEABLE_CONFIGS=8:16:1:none:1:worker,8:32:1:none:1:wave,8:64:1:none:1:wave,12:64:1:none:1:wave,8:16:1:none:1:wave,12:32:1:none:1:wave,15:64:1:none:1:wave,8:64:1:gpu:1:wave python3 tools/pageable_probe.py sweep $O/r03_pageable_wave.jsonl
+step pageable 900 env PAGEABLE_CONFIGS=8:16:1:none:1:worker,8:32:1:none:1:wave,8:64:1:none:1:wave,12:64:1:none:1:wave,8:128:1:none:1:wave,12:128:1:none:1:wave,8:64:1:none:0:wave python3 tools/pageable_probe.py sweep $O/r03_pageable_wave_ramp.jsonl
 cat $O/steps.txt
 tail -n 2 $O/tests.out
 python3 -c "
 import json
-for l in open('$O/r03_pageable_wave.jsonl'):
+for l in open('$O/r03_pageable_wave_ramp.jsonl'):
     d=json.loads(l)
     print(d.get('mode'), d.get('W'), d.get('chunk_MiB'), d.get('aff'), d.get('ms'), d.get('best_ms'), d.get('frac_of_pcie'), d.get('checked'), d.get('error','')[:300])
 "
