@@ -628,7 +628,12 @@ def end_to_end(result, n, dev=None):
     finally:
         redop.check(redop.set_pageable(prev['threads'], prev['chunk_bytes']))
     pg['workers_x_chunk'] = '%d x %d MiB' % (prev['threads'] or 8, prev['chunk_bytes'] >> 20)
-    pg['note'] = 'pageable (numpy) host buffers; never `value`'
+    pg['form'] = os.environ.get('MPIX_REDOP_PAGEABLE_MODE', 'wave')
+    pg['vs_pinned'] = round(result['end_to_end_host']['ms_per_call'] / pg['workers']['ms_per_call'], 4)
+    pg['note'] = ('pageable (numpy) host buffers; never `value`; workers = the library\'s host '
+                  'threads (wave form: all copy one chunk into page-locked memory while one '
+                  'zero-copy kernel combines the previous one), staged = hipMemcpyAsync through '
+                  'device scratch; vs_pinned = pinned call time / workers call time')
     result['end_to_end_pageable'] = pg
 
 

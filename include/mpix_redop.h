@@ -365,20 +365,27 @@ int MPIX_Redop_set_launch(int block_threads, int max_grid);
 int MPIX_Redop_get_launch(int *block_threads, int *unroll, int *max_grid);
 
 /* ---- large pageable host operands (performance knob) ----
- * threads > 0: operands of at least 2 * threads * chunk_bytes bytes go
- * through that many host workers, which copy chunks into pinned slots of
- * their own, each combined by a zero-copy kernel; smaller ones, and all of
- * them with threads = 0, are staged through device scratch with
- * hipMemcpyAsync.  Same bits either way.  Defaults 8 workers x 16 MiB (env
- * MPIX_REDOP_PAGEABLE_THREADS / MPIX_REDOP_PAGEABLE_CHUNK at first use);
- * threads 0..16, chunk 64 KiB..256 MiB.  The slots are one set per device
- * for the whole process (threads x 2 x chunk of page-locked memory, 256 MiB
- * at the defaults, freed by MPIX_Redop_finalize); a call that finds the set
- * in use by another thread stages its operands instead.  Each worker copies
- * its next chunk while the kernel of its current one runs (two buffers per
- * worker; env MPIX_REDOP_PAGEABLE_DB=0 for one), and env
- * MPIX_REDOP_PAGEABLE_AFFINITY=gpu pins the workers to the CPUs of the GPU's
- * NUMA node (or to an explicit cpulist such as "64-127"; default none). */
+ * threads > 0: pageable operands of at least chunk_bytes go through that many
+ * host threads (the caller is one of them).  Default form, "wave": the
+ * threads copy one chunk at a time into a page-locked buffer together (each
+ * a slice), and ONE zero-copy kernel combines that chunk while they copy the
+ * next one in and the previous result out; three chunk buffers rotate, and
+ * the chunk sizes ramp up and down at both ends (short pipeline fill).  Env
+ * MPIX_REDOP_PAGEABLE_MODE=worker selects the round-2 form instead: each
+ * thread copies, combines and copies back chunks of its own (operands of at
+ * least 2 * threads * chunk_bytes; env MPIX_REDOP_PAGEABLE_DB=1 gives every
+ * thread two buffers).  Smaller operands, and all of them with threads = 0,
+ * are staged through device scratch with hipMemcpyAsync.  Same bits every
+ * way.  Defaults 8 threads x 64 MiB (env MPIX_REDOP_PAGEABLE_THREADS /
+ * MPIX_REDOP_PAGEABLE_CHUNK at first use); threads 0..16, chunk 64 KiB..256
+ * MiB.  The buffers are one set per device for the whole process (wave: 3 x
+ * 2 x chunk of page-locked memory, 384 MiB at the defaults; worker: threads
+ * x 2 x chunk, twice that with two buffers), freed by MPIX_Redop_finalize; a
+ * call that finds the set in use by another thread stages its operands
+ * instead.  Copies into the page-locked buffers use non-temporal stores (env
+ * MPIX_REDOP_PAGEABLE_NT=0: memcpy), and env MPIX_REDOP_PAGEABLE_AFFINITY=gpu
+ * pins the threads to the CPUs of the GPU's NUMA node (or to an explicit
+ * cpulist such as "64-127"; default none). */
 int MPIX_Redop_set_pageable(int threads, MPIX_Aint chunk_bytes);
 int MPIX_Redop_get_pageable(int *threads, MPIX_Aint *chunk_bytes);
 

@@ -255,30 +255,34 @@ size_t g_stage_chunk = (size_t) 64 << 20;
 // pageable hipMemcpy calls (each a driver-side bounce of its own);
 // MPIX_REDOP_BOUNCE_BYTES, 0 disables
 size_t g_bounce_bytes = (size_t) 1 << 20;
-// pageable operands of at least two chunks per worker: this many host
-// workers, each copying chunks of g_pipe_chunk bytes into a pinned slot of its
-// own that a zero-copy kernel then combines (MPIX_REDOP_PAGEABLE_THREADS, 0 =
-// always stream the chunks through device scratch with hipMemcpyAsync;
-// MPIX_REDOP_PAGEABLE_CHUNK).  8 x 16 MiB: 60 GiB/s end to end at 1 GiB
-// against 52 staged; with fewer chunks than that the workers cannot overlap
-// and staging is faster (profiles/r01_pageable_sweep.txt)
+// large pageable operands (at least one chunk in the wave form below, two
+// chunks per worker in the worker form): this many host threads copy chunks
+// of g_pipe_chunk bytes into pinned buffers that zero-copy kernels combine
+// (MPIX_REDOP_PAGEABLE_THREADS, 0 = always stream the chunks through device
+// scratch with hipMemcpyAsync; MPIX_REDOP_PAGEABLE_CHUNK).  Wave form, 8 x
+// 64 MiB: 1 GiB in 45-46 ms, 0.88 x the pinned zero-copy call
+// (profiles/r03_pageable_wave_ramp.jsonl)
 std::atomic<int> g_pipe_threads{8};
-std::atomic<size_t> g_pipe_chunk{(size_t) 16 << 20};
-// Each worker keeps two slots and copies chunk k + W into one while the kernel
-// of chunk k reads the other (MPIX_REDOP_PAGEABLE_DB=0: one slot, copy and
-// kernel in turn), and the workers can be pinned to the CPUs of the GPU's own
-// NUMA node (MPIX_REDOP_PAGEABLE_AFFINITY=gpu, or an explicit cpulist such as
-// "64-127"; "none" leaves them where the scheduler puts them)
-std::atomic<bool> g_pipe_db{true};
+std::atomic<size_t> g_pipe_chunk{(size_t) 64 << 20};
+// Worker form only: with MPIX_REDOP_PAGEABLE_DB=1 each worker keeps two slots
+// and copies chunk k + W into one while the kernel of chunk k reads the other
+// (default one slot: measured no faster, twice the pinned memory,
+// profiles/r03_pageable_sweep.jsonl).  Both forms: the workers can be pinned
+// to the CPUs of the GPU's own NUMA node (MPIX_REDOP_PAGEABLE_AFFINITY=gpu, or
+// an explicit cpulist such as "64-127"; default "none" leaves them where the
+// scheduler puts them -- pinning measured no faster either)
+std::atomic<bool> g_pipe_db{false};
 std::string g_pipe_affinity = "none";
-// MPIX_REDOP_PAGEABLE_MODE=wave: all workers copy the same chunk in together
-// (each a slice), ONE zero-copy kernel per chunk runs while they copy the next
-// one in and the one before out -- three pinned chunk buffers in rotation.
-// Per-chunk zero-copy kernels pay a fixed ramp of ~0.16 ms each
-// (profiles/r03_pinned_chunks.json), so this form can use large chunks without
-// a long pipeline fill.  "worker" (default until measured otherwise): each
-// worker its own chunks, as above.
-std::atomic<int> g_pipe_wave{0};
+// Pageable form (MPIX_REDOP_PAGEABLE_MODE): "wave" (default) -- all workers
+// copy the same chunk in together (each a slice), ONE zero-copy kernel per
+// chunk runs while they copy the next one in and the one before out, three
+// pinned chunk buffers in rotation, chunk sizes ramped at both ends.  A
+// zero-copy kernel pays a ramp of ~0.16 ms however large
+// (profiles/r03_pinned_chunks.json), so large chunks win, and the ramped ends
+// keep the pipeline fill short: 1 GiB in 45-46 ms at 8 x 64 MiB against
+// 53 ms for the worker form (profiles/r03_pageable_wave_ramp.jsonl).
+// "worker": each worker copies, combines and copies back chunks of its own.
+std::atomic<int> g_pipe_wave{1};
 // Support-predicate knobs, the pattern of MPIR_CVAR_ENABLE_YAKSA_REDUCTION and
 // MPIR_CVAR_YAKSA_REDUCTION_THRESHOLD (typerep_yaksa_pack.c:44-64,229-240):
 // MPIX_REDOP_ENABLE=0 makes every predicate answer 0 (the caller keeps its CPU
@@ -331,7 +335,7 @@ void read_env()
     if (const char *s = getenv("MPIX_REDOP_PAGEABLE_DB"))
         g_pipe_db = atoi(s) != 0;
     if (const char *s = getenv("MPIX_REDOP_PAGEABLE_MODE"))
-        g_pipe_wave = strcmp(s, "wave") == 0;
+        g_pipe_wave = strcmp(s, "worker") != 0;
     if (const char *s = getenv("MPIX_REDOP_PAGEABLE_AFFINITY"))
         g_pipe_affinity = s;
     if (const char *s = getenv("MPIX_REDOP_PAGEABLE_CHUNK")) {
@@ -1677,7 +1681,7 @@ int MPIX_Reduce_local(const void *inbuf, void *inoutbuf, MPIX_Aint count, MPIX_D
     const int pipe_threads = g_pipe_threads.load();
     const bool wave = g_pipe_wave.load() != 0;
     if (pageable && zc && pipe_threads > 0 &&
-        (uint64_t) count * ext >= (wave ? 4 : 2 * (uint64_t) pipe_threads) * g_pipe_chunk.load()) {
+        (uint64_t) count * ext >= (wave ? 1 : 2 * (uint64_t) pipe_threads) * g_pipe_chunk.load()) {
         // pageable operands through the workers' pinned slots; a pinned
         // operand is used through its device mapping
         rc = (wave ? waved : pipelined)(win == Where::Pageable ? inbuf : pin,
