@@ -255,7 +255,7 @@ size_t g_stage_chunk = (size_t) 64 << 20;
 // pageable hipMemcpy calls (each a driver-side bounce of its own);
 // MPIX_REDOP_BOUNCE_BYTES, 0 disables
 size_t g_bounce_bytes = (size_t) 1 << 20;
-// large pageable operands (at least two chunks in the wave form below, two
+// large pageable operands (at least one chunk in the wave form below, two
 // chunks per worker in the worker form): this many host threads copy chunks
 // of g_pipe_chunk bytes into pinned buffers that zero-copy kernels combine
 // (MPIX_REDOP_PAGEABLE_THREADS, 0 = always stream the chunks through device
@@ -403,7 +403,7 @@ struct PipeSet {
     // wave mode: 3 chunk buffers (in half + inout half each), one stream
     char *ring = nullptr, *ring_dev = nullptr;
     size_t ring_half = 0;
-    hipStream_t ring_s[3] = {nullptr, nullptr, nullptr};    // buffer b's kernels on ring_s[b]
+    hipStream_t ring_s = nullptr;
     hipEvent_t ring_ev[3] = {nullptr, nullptr, nullptr};
     size_t half = 0;        // slot half size; slots [0, threads) hold host != nullptr
     int nbuf = 0;           // buffers per worker (2: double-buffered)
@@ -1129,16 +1129,14 @@ int waved(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext, u
         return -1;
     const size_t half = (g_pipe_chunk.load() + 255) & ~(size_t) 255;
     if (P.ring_half < half) {
-        for (hipStream_t rs : P.ring_s)
-            if (rs)
-                (void) hipStreamSynchronize(rs);
+        if (P.ring_s)
+            (void) hipStreamSynchronize(P.ring_s);
         if (P.ring)
             (void) hipHostFree(P.ring);
         P.ring = P.ring_dev = nullptr;
         P.ring_half = 0;
-        for (hipStream_t &rs : P.ring_s)
-            if (!rs && hipStreamCreateWithFlags(&rs, hipStreamNonBlocking) != hipSuccess)
-                return -1;
+        if (!P.ring_s && hipStreamCreateWithFlags(&P.ring_s, hipStreamNonBlocking) != hipSuccess)
+            return -1;
         for (hipEvent_t &e : P.ring_ev)
             if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
                 return -1;
@@ -1214,11 +1212,9 @@ int waved(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext, u
                 char *d = P.ring_dev + (size_t) b * 2 * half;
                 const void *kin = in_pg ? (const void *) d : (const char *) in + off * ext;
                 void *kio = io_pg ? (void *) (d + half) : (char *) io + off * ext;
-                // consecutive chunks on different streams: a kernel's start
-                // overlaps the previous one's tail (the zero-copy ramp)
-                int rc = enqueue(kin, kio, cnt, it, ext, op, P.ring_s[b]);
+                int rc = enqueue(kin, kio, cnt, it, ext, op, P.ring_s);
                 if (rc == MPIX_REDOP_SUCCESS)
-                    rc = hip_err(hipEventRecord(P.ring_ev[b], P.ring_s[b]));
+                    rc = hip_err(hipEventRecord(P.ring_ev[b], P.ring_s));
                 if (rc)
                     fail(rc);
             }
@@ -1266,8 +1262,7 @@ int waved(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext, u
     work(0);
     for (std::thread &t : pool)
         t.join();
-    for (hipStream_t rs : P.ring_s)     // nothing left reading the buffers
-        (void) hipStreamSynchronize(rs);
+    (void) hipStreamSynchronize(P.ring_s);      // nothing left reading the buffers
     return err.load();
 }
 
@@ -1584,7 +1579,7 @@ int MPIX_Redop_finalize(void)
     for (int i = 0; i < kMaxDev; ++i) {     // the process-wide pageable worker slots
         PipeSet &P = g_pipes[i];
         std::lock_guard<std::mutex> l(P.mu);
-        if (!P.slot[0].s && !P.slot[0].host && !P.ring && !P.ring_s[0])
+        if (!P.slot[0].s && !P.slot[0].host && !P.ring && !P.ring_s)
             continue;
         DeviceGuard g(i);
         for (PipeSlot &sl : P.slot) {
@@ -1601,12 +1596,10 @@ int MPIX_Redop_finalize(void)
         }
         P.half = 0;
         P.nbuf = 0;
-        for (hipStream_t &rs : P.ring_s)
-            if (rs) {
-                (void) hipStreamSynchronize(rs);
-                (void) hipStreamDestroy(rs);
-                rs = nullptr;
-            }
+        if (P.ring_s) {
+            (void) hipStreamSynchronize(P.ring_s);
+            (void) hipStreamDestroy(P.ring_s);
+        }
         for (hipEvent_t &e : P.ring_ev)
             if (e) {
                 (void) hipEventDestroy(e);
@@ -1616,6 +1609,7 @@ int MPIX_Redop_finalize(void)
             (void) hipHostFree(P.ring);
         P.ring = P.ring_dev = nullptr;
         P.ring_half = 0;
+        P.ring_s = nullptr;
     }
     return MPIX_REDOP_SUCCESS;
 }
@@ -1687,7 +1681,7 @@ int MPIX_Reduce_local(const void *inbuf, void *inoutbuf, MPIX_Aint count, MPIX_D
     const int pipe_threads = g_pipe_threads.load();
     const bool wave = g_pipe_wave.load() != 0;
     if (pageable && zc && pipe_threads > 0 &&
-        (uint64_t) count * ext >= (wave ? 2 : 2 * (uint64_t) pipe_threads) * g_pipe_chunk.load()) {
+        (uint64_t) count * ext >= (wave ? 1 : 2 * (uint64_t) pipe_threads) * g_pipe_chunk.load()) {
         // pageable operands through the workers' pinned slots; a pinned
         // operand is used through its device mapping
         rc = (wave ? waved : pipelined)(win == Where::Pageable ? inbuf : pin,

@@ -13,8 +13,8 @@ step() {    # name timeout cmd...: stop the script on a fault / abort / time lim
     return 0
 }
 step tests 300 python3 -u -m pytest -q -x --timeout 200 --timeout-method thread -p no:cacheprovider tests/test_gpu_parity.py -k "pageable or host"
-for B in 134217728 1073741824; do
-  step size_$B 600 env PAGEABLE_BYTES=$B PAGEABLE_CONFIGS=8:64:0:none:1:wave,8:128:0:none:1:wave,0:64:0:none:1:wave python3 tools/pageable_probe.py sweep $O/r03_pageable_size_$B.jsonl
+for B in 67108864 268435456 1073741824; do
+  step size_$B 600 env PAGEABLE_BYTES=$B PAGEABLE_CONFIGS=8:64:0:none:1:wave,0:64:0:none:1:wave python3 tools/pageable_probe.py sweep $O/r03_pageable_size_$B.jsonl
 done
 cat $O/steps.txt
 tail -n 2 $O/tests.out
