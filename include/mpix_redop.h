@@ -365,7 +365,7 @@ int MPIX_Redop_set_launch(int block_threads, int max_grid);
 int MPIX_Redop_get_launch(int *block_threads, int *unroll, int *max_grid);
 
 /* ---- large pageable host operands (performance knob) ----
- * threads > 0: pageable operands of at least chunk_bytes go through that many
+ * threads > 0: pageable operands of at least 2 * chunk_bytes go through that many
  * host threads (the caller is one of them).  Default form, "wave": the
  * threads copy one chunk at a time into a page-locked buffer together (each
  * a slice), and ONE zero-copy kernel combines that chunk while they copy the
