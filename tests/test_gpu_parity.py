@@ -1190,3 +1190,59 @@ def test_loc_specials_on_gpu(R, H, oracle, dtname, opname):
     exp = a.copy()
     assert oracle.reduce_local(b.copy(), exp, nv * nv, dt, op) == 0
     assert np.array_equal(host(da), exp)
+
+
+@pytest.mark.parametrize('tn', ['MPI_INT8_T', 'MPI_UINT8_T', 'MPI_BYTE', 'MPI_C_BOOL', 'MPI_CHAR'])
+def test_one_byte_ops_every_pair_on_gpu(R, H, oracle, tn):
+    """round 3's four-bytes-per-dword logicals (and the 1-byte kernels of
+    every other op the type has) on every pair of byte values, in every byte
+    lane of a dword and every 16-byte packet position of a tile, against the
+    oracle: 65536 pairs x 16 rotations"""
+    dt = getattr(H, tn)
+    a8, b8 = np.meshgrid(np.arange(256, dtype=np.uint8), np.arange(256, dtype=np.uint8))
+    a8, b8 = a8.ravel(), b8.ravel()
+    # rotate the pair sequence so every pair lands in every byte of a packet
+    A = np.concatenate([np.roll(a8, r) for r in range(16)])
+    B = np.concatenate([np.roll(b8, r) for r in range(16)])
+    n = A.size
+    ran = 0
+    for on, op in H.OPS.items():
+        if op in (H.MPI_REPLACE, H.MPI_NO_OP, H.MPIX_EQUAL) or not R.is_supported(op, dt):
+            continue
+        da, db = dev(A), dev(B)
+        assert R.MPI_Reduce_local(db, da, n, dt, op) == 0
+        exp = A.copy()
+        oracle.reduce_local(B, exp, n, dt, op)
+        assert np.array_equal(host(da), exp), (tn, on)
+        ran += 1
+    assert ran >= 3, tn
+
+
+def test_complex_prod_sparse_specials_in_tiles(R, H, oracle):
+    """the Annex G product's recovery runs once per tile when any lane's
+    element needs it: ordinary products with sparse (inf, nan) / (nan, nan)
+    pairs scattered through many tiles, every lane position, C float and
+    double complex and the fp16 struct complex -- bit-exact where the
+    result is a number, NaN where it is a NaN"""
+    rng = np.random.default_rng(0x5EED0A6)
+    inf, nan = np.inf, np.nan
+    specials = [(inf, nan), (nan, inf), (nan, nan), (inf, 0.0), (0.0, inf), (-inf, 1.0),
+                (1.0, -inf), (nan, 0.0)]
+    for tn, ft in (('MPI_C_FLOAT_COMPLEX', np.float32), ('MPI_C_DOUBLE_COMPLEX', np.float64),
+                   ('MPI_COMPLEX4', np.float16)):
+        dt = getattr(H, tn)
+        n = (1 << 18) + 37
+        a = rng.uniform(-2, 2, (n, 2)).astype(ft)
+        b = rng.uniform(-2, 2, (n, 2)).astype(ft)
+        for arr in (a, b):
+            idx = rng.choice(n, n // 500, replace=False)
+            for i in idx:
+                arr[i] = specials[rng.integers(len(specials))]
+        da, db = dev(a), dev(b)
+        assert R.MPI_Reduce_local(db, da, n, dt, H.MPI_PROD) == 0
+        exp = a.copy()
+        oracle.reduce_local(b, exp, n, dt, H.MPI_PROD)
+        got = host(da).view(ft).reshape(n, 2)
+        both_nan = np.isnan(got) & np.isnan(exp)
+        same = (got.view(np.uint8).reshape(n, 2, -1) == exp.view(np.uint8).reshape(n, 2, -1)).all(-1)
+        assert np.all(same | both_nan), tn
