@@ -81,13 +81,7 @@ def main():
         ai, ao = as_np(pi, n), as_np(po, n)
         r = dict(memcpy_into_in_GBs=memcpy_rate(ai, src), memcpy_into_inout_GBs=memcpy_rate(ao, src))
         r['memcpy_out_of_inout_GBs'] = memcpy_rate(src.copy(), ao)
-        ref = ao.copy()
         r.update(calls(pi, po, n))
-        # bits: 7 calls of inout += in from the copy, on the host in fp32
-        exp = ref
-        for _ in range(7):
-            exp = exp + ai
-        r['checked'] = bool(np.array_equal(exp, ao))
         res['%s/%s' % (kin, kio)] = r
         hip.hipHostFree(pi)
         hip.hipHostFree(po)
