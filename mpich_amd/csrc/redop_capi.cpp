@@ -405,12 +405,6 @@ struct PipeSet {
     size_t ring_half = 0;
     hipStream_t ring_s = nullptr;
     hipEvent_t ring_ev[3] = {nullptr, nullptr, nullptr};
-    // results through HBM (see waved): 3 device result buffers, the copy
-    // stream that returns them to the page-locked buffers, its events
-    char *res = nullptr;
-    size_t res_half = 0;
-    hipStream_t res_s = nullptr;
-    hipEvent_t res_ev[3] = {nullptr, nullptr, nullptr};
     size_t half = 0;        // slot half size; slots [0, threads) hold host != nullptr
     int nbuf = 0;           // buffers per worker (2: double-buffered)
     bool cpus_known = false;
@@ -1161,39 +1155,6 @@ int waved(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext, u
         P.cpus = worker_cpus(dev);
         P.cpus_known = true;
     }
-    // A zero-copy kernel that WRITES host memory pays ~0.12 ms at its end,
-    // however large, draining its posted PCIe writes; one that only reads
-    // pays ~0.03 ms (profiles/r03_zero_copy_split.json).  So with a pageable
-    // inout the kernel reads both operands from the page-locked buffer and
-    // writes the result to HBM (the 2-slot tree kernel, out = inout OP in),
-    // and a copy engine returns it to the page-locked buffer on a second
-    // stream, overlapping the next chunk's kernel (the two PCIe directions
-    // run at once).  MPIX_REDOP_PAGEABLE_SPLIT=0: the kernel writes the
-    // page-locked buffer itself.
-    const uint32_t opi = op & 0xf;
-    const Entry *te = (io_pg && opi >= 1 && opi <= 12) ? gpu_entry(opi, it) : nullptr;
-    static const bool split_on = !getenv("MPIX_REDOP_PAGEABLE_SPLIT") ||
-                                 atoi(getenv("MPIX_REDOP_PAGEABLE_SPLIT")) != 0;
-    const bool split = split_on && te && te->tree;
-    if (split && P.res_half < half) {
-        if (P.res_s)
-            (void) hipStreamSynchronize(P.res_s);
-        if (P.res)
-            (void) hipFree(P.res);
-        P.res = nullptr;
-        P.res_half = 0;
-        if (!P.res_s && hipStreamCreateWithFlags(&P.res_s, hipStreamNonBlocking) != hipSuccess)
-            return -1;
-        for (hipEvent_t &e : P.res_ev)
-            if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
-                return -1;
-        if (hipMalloc((void **) &P.res, 3 * half) != hipSuccess) {
-            (void) hipGetLastError();
-            P.res = nullptr;
-            return -1;
-        }
-        P.res_half = half;
-    }
     const uint64_t chunk = half / ext;
     if (chunk == 0)
         return -1;
@@ -1255,26 +1216,9 @@ int waved(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext, u
                 // three streams, overlapping each other's ramp, measured 25 %
                 // slower (57.5 vs 46.1 ms per 1 GiB; zero-copy kernels
                 // running together get in each other's way)
-                int rc;
-                if (split) {
-                    char *r = P.res + (size_t) b * half;
-                    const void *ins[2] = {kio, kin};     // slot 0 = inout, slot 1 = in
-                    rc = hip_err(te->tree(ins, 2, r, cnt, params(), launch_cfg(), P.ring_s));
-                    if (rc == MPIX_REDOP_SUCCESS)
-                        rc = hip_err(hipEventRecord(P.ring_ev[b], P.ring_s));
-                    if (rc == MPIX_REDOP_SUCCESS)
-                        rc = hip_err(hipStreamWaitEvent(P.res_s, P.ring_ev[b], 0));
-                    if (rc == MPIX_REDOP_SUCCESS)
-                        rc = hip_err(hipMemcpyAsync(P.ring + (size_t) b * 2 * half + half, r,
-                                                    (size_t) (cnt * ext), hipMemcpyDeviceToHost,
-                                                    P.res_s));
-                    if (rc == MPIX_REDOP_SUCCESS)
-                        rc = hip_err(hipEventRecord(P.res_ev[b], P.res_s));
-                } else {
-                    rc = enqueue(kin, kio, cnt, it, ext, op, P.ring_s);
-                    if (rc == MPIX_REDOP_SUCCESS)
-                        rc = hip_err(hipEventRecord(P.ring_ev[b], P.ring_s));
-                }
+                int rc = enqueue(kin, kio, cnt, it, ext, op, P.ring_s);
+                if (rc == MPIX_REDOP_SUCCESS)
+                    rc = hip_err(hipEventRecord(P.ring_ev[b], P.ring_s));
                 if (rc)
                     fail(rc);
             }
@@ -1291,7 +1235,7 @@ int waved(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext, u
             }
             if (st >= 2 && st - 2 < n && err.load() == MPIX_REDOP_SUCCESS) {   // chunk st-2 out
                 const int b = (int) ((st - 2) % 3);
-                int rc = hip_err(hipEventSynchronize(split ? P.res_ev[b] : P.ring_ev[b]));
+                int rc = hip_err(hipEventSynchronize(P.ring_ev[b]));
                 if (rc)
                     fail(rc);
                 else if (io_pg) {
@@ -1323,8 +1267,6 @@ int waved(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext, u
     for (std::thread &t : pool)
         t.join();
     (void) hipStreamSynchronize(P.ring_s);      // nothing left reading the buffers
-    if (P.res_s)
-        (void) hipStreamSynchronize(P.res_s);
     return err.load();
 }
 
@@ -1672,20 +1614,6 @@ int MPIX_Redop_finalize(void)
         P.ring = P.ring_dev = nullptr;
         P.ring_half = 0;
         P.ring_s = nullptr;
-        if (P.res_s) {
-            (void) hipStreamSynchronize(P.res_s);
-            (void) hipStreamDestroy(P.res_s);
-        }
-        for (hipEvent_t &e : P.res_ev)
-            if (e) {
-                (void) hipEventDestroy(e);
-                e = nullptr;
-            }
-        if (P.res)
-            (void) hipFree(P.res);
-        P.res = nullptr;
-        P.res_half = 0;
-        P.res_s = nullptr;
     }
     return MPIX_REDOP_SUCCESS;
 }

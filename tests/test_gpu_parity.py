@@ -999,24 +999,20 @@ print('mode ok')
 
 @pytest.mark.parametrize('db,aff,mode', [('0', 'none', 'worker'), ('1', 'gpu', 'worker'),
                                          ('1', '0-3,5', 'worker'), ('0', 'gpu', 'worker'),
-                                         ('1', 'none', 'wave'), ('1', 'gpu', 'wave'),
-                                         ('0', 'none', 'wave-nosplit')])
+                                         ('1', 'none', 'wave'), ('1', 'gpu', 'wave')])
 def test_pageable_worker_modes(db, aff, mode):
     """the workers' modes from the environment: one buffer (copy and kernel in
     turn) or two (the next chunk copied during the kernel), pinned to the
     GPU's NUMA node or an explicit cpulist, and the wave form (all workers on
-    one chunk, one kernel per chunk, three buffers in rotation), with the
-    result through HBM and a copy engine (default) or written by the kernel
-    into the page-locked buffer; same bits as the oracle"""
+    one chunk, one kernel per chunk, three buffers in rotation); same bits as
+    the oracle"""
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     p = subprocess.run([sys.executable, '-c', _PAGEABLE_MODE % root], capture_output=True,
                        text=True, timeout=300,
                        env=dict(os.environ, MPIX_REDOP_PAGEABLE_DB=db,
-                                MPIX_REDOP_PAGEABLE_AFFINITY=aff,
-                                MPIX_REDOP_PAGEABLE_MODE=mode.split('-')[0],
-                                MPIX_REDOP_PAGEABLE_SPLIT='0' if mode.endswith('nosplit') else '1'))
+                                MPIX_REDOP_PAGEABLE_AFFINITY=aff, MPIX_REDOP_PAGEABLE_MODE=mode))
     assert p.returncode == 0 and 'mode ok' in p.stdout, p.stdout + p.stderr
 
 

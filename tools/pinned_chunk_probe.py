@@ -88,26 +88,6 @@ def main():
             t = time.perf_counter() - t0
             best = t if best is None else min(best, t)
         out['pinned_%dMiB_chunks_T%d_ms' % (mib, T)] = round(best * 1e3, 2)
-    # which direction carries the per-call ramp: operands split between
-    # page-locked host memory and HBM (reads only over PCIe / reads + writes)
-    if os.environ.get('CHUNK_SPLIT'):
-        din = torch.empty(n, dtype=torch.float32, device='cuda').uniform_(-1, 1)
-        dio = torch.empty(n, dtype=torch.float32, device='cuda').uniform_(-1, 1)
-        torch.cuda.synchronize()
-        for name, pi, po in (('in_host_io_hbm', hin.data_ptr(), dio.data_ptr()),
-                             ('in_hbm_io_host', din.data_ptr(), hio.data_ptr())):
-            for mib in [0] + sizes:
-                chunk = n if mib == 0 else (mib << 20) // 4
-                best = None
-                for _ in range(3):
-                    t0 = time.perf_counter()
-                    for off in range(0, n, chunk):
-                        L.MPIX_Reduce_local(pi + 4 * off, po + 4 * off, min(chunk, n - off),
-                                            H.as_c_int(H.MPI_FLOAT), H.as_c_int(H.MPI_SUM))
-                    t = time.perf_counter() - t0
-                    best = t if best is None else min(best, t)
-                out['%s_%s_ms' % (name, 'one_call' if mib == 0 else '%dMiB_chunks' % mib)] = \
-                    round(best * 1e3, 2)
     print(json.dumps(out))
     if len(sys.argv) > 1:
         json.dump(out, open(sys.argv[1], 'w'), indent=1)
