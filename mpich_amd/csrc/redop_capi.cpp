@@ -1215,7 +1215,15 @@ int waved(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext, u
                 // one stream for all chunks: kernels of consecutive chunks on
                 // three streams, overlapping each other's ramp, measured 25 %
                 // slower (57.5 vs 46.1 ms per 1 GiB; zero-copy kernels
-                // running together get in each other's way)
+                // running together get in each other's way).  The kernel
+                // writes the page-locked buffer itself: a zero-copy kernel
+                // that only reads host memory pays less at its end (~0.03 vs
+                // ~0.12 ms, profiles/r03_zero_copy_split.json), but returning
+                // the result from HBM with a copy engine while the next kernel
+                // reads took 56 ms per GiB against 44.6
+                // (profiles/r03_pageable_split_rejected.jsonl): the copy
+                // engine and the CUs' PCIe reads share the link badly, as the
+                // SDMA-only duplex pattern does (56 ms, bench.py pcie)
                 int rc = enqueue(kin, kio, cnt, it, ext, op, P.ring_s);
                 if (rc == MPIX_REDOP_SUCCESS)
                     rc = hip_err(hipEventRecord(P.ring_ev[b], P.ring_s));
