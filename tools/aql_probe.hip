@@ -84,6 +84,7 @@ struct Args {
 };
 
 static hsa_agent_t g_gpu, g_cpu;
+static hsa_amd_hdp_flush_t g_hdp{};
 static int g_bdf = -1;
 static hsa_amd_memory_pool_t g_karg_pool;
 static bool g_have_pool = false;
@@ -172,8 +173,14 @@ struct Variant {
 static void dispatch(Aql &A, Variant &v, const Args &a, uint32_t grid)
 {
     *v.karg = a;
-    if (v.dev_karg)     // flush the write-combined BAR writes before the CP reads them
+    if (v.dev_karg) {   // BAR writes into VRAM: flush the host data path, then read back
+        __atomic_thread_fence(__ATOMIC_SEQ_CST);
+        if (g_hdp.HDP_MEM_FLUSH_CNTL) {
+            *(volatile uint32_t *) g_hdp.HDP_MEM_FLUSH_CNTL = 1u;
+            (void) *(volatile uint32_t *) g_hdp.HDP_MEM_FLUSH_CNTL;
+        }
         (void) *(volatile uint64_t *) &v.karg->stride;
+    }
     hsa_signal_store_relaxed(A.sig, 1);
     uint64_t idx = hsa_queue_add_write_index_relaxed(A.q, 1);
     while (idx - hsa_queue_load_read_index_scacquire(A.q) >= A.q->size) {
@@ -311,6 +318,9 @@ int main(int argc, char **argv)
     memset(kp, 0, kbytes);
     void *kd = nullptr;
     CK(hsa_amd_agent_iterate_memory_pools(g_gpu, find_vram_pool, nullptr));
+    if (hsa_agent_get_info(g_gpu, (hsa_agent_info_t) HSA_AMD_AGENT_INFO_HDP_FLUSH, &g_hdp) != HSA_STATUS_SUCCESS)
+        memset(&g_hdp, 0, sizeof g_hdp);
+    fprintf(stderr, "HDP flush register %p\n", (void *) g_hdp.HDP_MEM_FLUSH_CNTL);
     if (g_have_vram_fg && hsa_amd_memory_pool_allocate(g_vram_fg, kbytes, 0, &kd) == HSA_STATUS_SUCCESS) {
         if (hsa_amd_agents_allow_access(1, &g_cpu, nullptr, kd) != HSA_STATUS_SUCCESS)
             kd = nullptr;
