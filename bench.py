@@ -610,7 +610,33 @@ def end_to_end(result, n, dev=None):
                                           'them over PCIe (zero-copy); never `value`; '
                                           'frac_of_pcie = measured PCIe floor of the same '
                                           'traffic / call time')
-    del hin, hio
+    # SURVEY.md §8(d)'s end-to-end as written: hipMemcpyAsync H2D(in, inout),
+    # the kernel, D2H(inout) from the same page-locked buffers, one stream,
+    # whole 1 GiB operands (no chunk pipelining), timed as a whole
+    d = dev if dev is not None else torch.device('cuda', 0)
+    din = torch.empty(n, dtype=torch.float32, device=d)
+    dio = torch.empty(n, dtype=torch.float32, device=d)
+    cs = torch.cuda.Stream(d)
+
+    def copy_call():
+        with torch.cuda.stream(cs):
+            din.copy_(hin, non_blocking=True)
+            dio.copy_(hio, non_blocking=True)
+            redop.check(redop.reduce_local_async(din, dio, n, H.MPI_FLOAT, H.MPI_SUM, cs))
+            hio.copy_(dio, non_blocking=True)
+        cs.synchronize()
+    copy_call()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        copy_call()
+    tc = (time.perf_counter() - t0) / reps
+    result['end_to_end_host']['memcpy_kernel_memcpy'] = dict(
+        gibs=round(3 * n * 4 / GIB / tc, 2), ms_per_call=round(tc * 1e3, 2),
+        frac_of_pcie=round(t_floor / tc, 4),
+        note='SURVEY 8(d) end-to-end as written: hipMemcpyAsync H2D of both operands, the '
+             'kernel, hipMemcpyAsync D2H of inout, from the same page-locked buffers on one '
+             'stream, whole operands; the zero-copy call above is the library\'s own form')
+    del hin, hio, din, dio
     pin_ = np.random.default_rng(0x5EED0007).random(n, dtype=np.float32)
     pio_ = np.random.default_rng(0x5EED0008).random(n, dtype=np.float32)
     prev = redop.get_pageable()
@@ -824,6 +850,13 @@ def multi_gpu(args, world, rank, dev):
     return result
 
 
+def _no_shared(e):
+    """a leg over symmetric memory when MPIX_Comm_alloc_shared found no
+    verified mapping (MPI_ERR_OTHER on every rank, mpix_coll.h): reported,
+    not timed, and the other legs go on"""
+    return {'error': 'no symmetric memory (%s); leg not timed' % e, 'schedule_ran': None}
+
+
 def rsb_secondary(args, world, rank, dev, out):
     """the other schedules on the same RCCL communicator: pairwise (all P-1
     links in one group + one multi-input combine), pipelined pairwise, the
@@ -854,7 +887,11 @@ def rsb_secondary(args, world, rank, dev, out):
     shared = None
     for name, algo, on_shared in legs:
         if on_shared and shared is None:
-            shared = cc.shared_tensor(total, torch.float32)
+            try:        # collective: every rank gets the memory, or none does
+                shared = cc.shared_tensor(total, torch.float32)
+            except redop.RedopError as e:
+                out[name] = _no_shared(e)
+                continue
             shared.copy_(send)
             torch.cuda.synchronize()
         src = shared if on_shared else send
@@ -971,8 +1008,12 @@ def allreduce_secondary(args, world, rank, dev, res):
         if name == 'rccl_all_reduce' and dist.get_backend() != 'nccl':
             continue
         if name == 'c_pull_shared':
-            sh_in = cc.shared_tensor(n, torch.float32)
-            sh_out = cc.shared_tensor(n, torch.float32)
+            try:
+                sh_in = cc.shared_tensor(n, torch.float32)
+                sh_out = cc.shared_tensor(n, torch.float32)
+            except redop.RedopError as e:
+                res[name] = _no_shared(e)
+                continue
             sh_in.copy_(send)
             torch.cuda.synchronize()
         fn()
@@ -1001,9 +1042,9 @@ def allreduce_secondary(args, world, rank, dev, res):
             sched = schedule_ran(cc, asked[name], 'ar')
         res[name] = dict(sched, ms=round(t * 1e3, 3),
                          busbw_GBs=round(2 * (world - 1) / world * n * 4 / t / 1e9, 2))
-    if sh_in is not None:
-        cc.free_shared(sh_in.data_ptr())
-        cc.free_shared(sh_out.data_ptr())
+    for t in (sh_in, sh_out):
+        if t is not None:
+            cc.free_shared(t.data_ptr())
     del send, recv, ws, ref, sh_in, sh_out
     torch.cuda.empty_cache()
 

@@ -1,0 +1,34 @@
+# Rehearsal of the N>1 bench flow on the one-GPU box (every rank on device 0,
+# gloo control plane, staged transport -- RCCL refuses two ranks on one GPU):
+# the line must show `schedule_ran` for every leg.  Run twice: as is, and with
+# MPIX_COLL_WINDOW_FAULT=1 (rank 1 publishes a window its memory does not
+# hold), where every pull leg must be reported as "fell back to ..." and not
+# timed under the pull's name.
+# usage (on the GPU box): P=4 bash tools/gpu_rehearse.sh
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+P=${P:-4}
+O=gpurun_out/rehearse
+rm -rf $O && mkdir -p $O
+summ() {
+python3 -c "
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+print('value', d.get('value'), 'schedule_ran', d.get('schedule_ran'), 'error', d.get('error'))
+for sec in ('reduce_scatter_block_other', 'allreduce'):
+    for k, v in d.get(sec, {}).items():
+        if isinstance(v, dict):
+            print(' ', sec, k, 'ran:', v.get('schedule_ran'), 'ms:', v.get('ms'), 'error:', v.get('error'))
+" $1
+}
+for mode in normal fault; do
+    if [ $mode = fault ]; then export MPIX_COLL_WINDOW_FAULT=1; fi
+    MPIX_BENCH_SAME_DEVICE=1 MPIX_BENCH_BACKEND=gloo timeout -k 10 500 python3 -m torch.distributed.run \
+        --nnodes=1 --nproc-per-node $P --master-addr 127.0.0.1 --master-port 29541 bench.py --gpus $P \
+        --steps 3 --warmup 1 --count 67108864 --rsb-bytes 268435456 > $O/n${P}_$mode.json 2> $O/n${P}_$mode.err
+    rc=$?
+    echo "$mode rc=$rc"
+    summ $O/n${P}_$mode.json || tail -20 $O/n${P}_$mode.err
+    if [ $rc -ne 0 ]; then exit $rc; fi
+done
