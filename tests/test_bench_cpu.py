@@ -139,3 +139,15 @@ def test_state_before_first_collective():
     finally:
         for c in comms:
             c.free()
+
+
+def test_leg_without_symmetric_memory_is_reported_not_fatal():
+    """MPIX_Comm_alloc_shared answers MPI_ERR_OTHER on every rank when no
+    verified mapping could be made (mpix_coll.h); the bench then reports that
+    leg with its reason and no time, and goes on with the others (found by the
+    window-fault rehearsal, profiles/r03_rehearsal_n4.json)"""
+    import bench
+    from mpich_amd import redop
+    leg = bench._no_shared(redop.RedopError(15, 'MPIX_Comm_alloc_shared'))
+    assert leg['schedule_ran'] is None and 'ms' not in leg
+    assert leg['error'].startswith('no symmetric memory') and 'MPIX_Comm_alloc_shared' in leg['error']
