@@ -364,6 +364,18 @@ const char *MPIX_Redop_error_string(int code);
 int MPIX_Redop_set_launch(int block_threads, int max_grid);
 int MPIX_Redop_get_launch(int *block_threads, int *unroll, int *max_grid);
 
+/* ---- store policy of the contiguous kernel (performance knob, not semantics) ----
+ * Blocks of a contiguous launch that run on an XCD whose bit is set in
+ * xcd_mask (HW_REG_XCC_ID, bits 0-7), blocks b with b % every == phase
+ * (every > 0), and the last tail_blocks blocks store their result
+ * write-through (the line leaves the XCD's L2 at once) instead of
+ * non-temporally (the line stays in L2, dirty, until evicted or written back
+ * at the end of the kernel).  Same bits either way.  Env MPIX_REDOP_WT_XCD /
+ * MPIX_REDOP_WT_EVERY / MPIX_REDOP_WT_PHASE / MPIX_REDOP_WT_TAIL override
+ * the defaults at first use. */
+int MPIX_Redop_set_store_policy(int xcd_mask, int every, int phase, int tail_blocks);
+int MPIX_Redop_get_store_policy(int *xcd_mask, int *every, int *phase, int *tail_blocks);
+
 /* ---- large pageable host operands (performance knob) ----
  * threads > 0: pageable operands of at least 2 * chunk_bytes go through that many
  * host threads (the caller is one of them).  Default form, "wave": the

@@ -240,6 +240,10 @@ const Entry *gpu_entry(uint32_t opi, uint32_t it)
 // ---------------------------------------------------------------- state
 std::atomic<long long> g_ftrue{1}, g_ffalse{0};
 std::atomic<int> g_block{256}, g_max_grid{0};
+// MPIX_REDOP_WT_TAIL: the last this-many blocks of a contiguous launch store
+// write-through, so less of the result is left dirty in the XCD L2s for the
+// end-of-kernel write-back (0 = off)
+std::atomic<int> g_wt_tail{0}, g_wt_every{0}, g_wt_phase{0}, g_wt_xcd{0};
 // completion wait of the synchronous calls: 0 block (hipStreamSynchronize),
 // 1 spin on an event, 2 spin on a pinned host word that a one-workgroup
 // contiguous kernel stores itself and the stream writes after any other
@@ -313,6 +317,16 @@ void read_env()
         if (b >= 64 && b <= 1024 && b % 64 == 0)
             g_block = b;
     }
+    if (const char *s = getenv("MPIX_REDOP_WT_TAIL"))
+        g_wt_tail = atoi(s) > 0 ? atoi(s) : 0;
+    if (const char *s = getenv("MPIX_REDOP_WT_EVERY"))
+        g_wt_every = atoi(s) > 0 ? atoi(s) : 0;
+    if (const char *s = getenv("MPIX_REDOP_WT_PHASE"))
+        g_wt_phase = atoi(s) > 0 ? atoi(s) : 0;
+    if (g_wt_every > 0)
+        g_wt_phase = g_wt_phase % g_wt_every;
+    if (const char *s = getenv("MPIX_REDOP_WT_XCD"))
+        g_wt_xcd = (int) (strtol(s, nullptr, 0) & 0xff);
     if (const char *s = getenv("MPIX_REDOP_MAXGRID"))
         g_max_grid = atoi(s) > 0 ? atoi(s) : 0;
     if (const char *s = getenv("MPIX_REDOP_SYNC"))
@@ -491,7 +505,8 @@ DevState *dev_state(int dev)
 LaunchCfg launch_cfg()
 {
     std::call_once(g_env_once, read_env);
-    return LaunchCfg{g_block.load(), g_max_grid.load()};
+    return LaunchCfg{g_block.load(), g_max_grid.load(), g_wt_tail.load(), g_wt_every.load(),
+                     g_wt_phase.load(), g_wt_xcd.load()};
 }
 
 Params params() { return Params{g_ftrue.load(), g_ffalse.load()}; }
@@ -2146,6 +2161,33 @@ int MPIX_Redop_set_launch(int block_threads, int max_grid)
         return MPIX_REDOP_ERR_ARG;
     g_block = block_threads;
     g_max_grid = max_grid;
+    return MPIX_REDOP_SUCCESS;
+}
+
+int MPIX_Redop_set_store_policy(int xcd_mask, int every, int phase, int tail_blocks)
+{
+    launch_cfg();
+    if (xcd_mask < 0 || xcd_mask > 0xff || every < 0 || phase < 0 ||
+        (every > 0 && phase >= every) || tail_blocks < 0)
+        return MPIX_REDOP_ERR_ARG;
+    g_wt_xcd = xcd_mask;
+    g_wt_every = every;
+    g_wt_phase = phase;
+    g_wt_tail = tail_blocks;
+    return MPIX_REDOP_SUCCESS;
+}
+
+int MPIX_Redop_get_store_policy(int *xcd_mask, int *every, int *phase, int *tail_blocks)
+{
+    launch_cfg();
+    if (xcd_mask)
+        *xcd_mask = g_wt_xcd.load();
+    if (every)
+        *every = g_wt_every.load();
+    if (phase)
+        *phase = g_wt_phase.load();
+    if (tail_blocks)
+        *tail_blocks = g_wt_tail.load();
     return MPIX_REDOP_SUCCESS;
 }
 

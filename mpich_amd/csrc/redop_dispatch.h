@@ -21,6 +21,13 @@ struct Params {
     uint32_t *done = nullptr;       // pinned, fine-grained host word
     uint32_t *done_ctr = nullptr;   // device word, 0 between launches
     uint32_t done_seq = 0;
+    // blocks from this index on store write-through (sc0 sc1: the line leaves
+    // the XCD's L2 at once instead of staying dirty until the end-of-kernel
+    // write-back); 0xffffffff = none (LaunchCfg::wt_tail)
+    uint32_t wt_from = 0xffffffffu;
+    uint32_t wt_every = 0;      // and blocks b with b % wt_every == wt_phase (0 = none)
+    uint32_t wt_phase = 0;
+    uint32_t wt_xcd = 0;        // and every block running on an XCD whose bit is set
 };
 
 constexpr unsigned kSignalMaxGrid = 4;
@@ -28,6 +35,10 @@ constexpr unsigned kSignalMaxGrid = 4;
 struct LaunchCfg {
     int block;          // threads per block (multiple of 64)
     int max_grid;       // 0 = no cap (one tile per block)
+    int wt_tail;        // contiguous kernel: the last wt_tail blocks store write-through
+    int wt_every;       // ... and blocks b with b % wt_every == wt_phase
+    int wt_phase;
+    int wt_xcd;         // ... and blocks on the XCDs (HW_REG_XCC_ID) of this bit mask
 };
 
 // One (op, type) pair: launchers for the contiguous and the vector-target form.

@@ -56,6 +56,21 @@ template <bool NT> __device__ __forceinline__ void st16(v4u *p, v4u v)
         *p = v;
 }
 
+// the XCD this wave runs on (0-7; a hardware register, read-only)
+__device__ __forceinline__ unsigned xcc_id()
+{
+    unsigned x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    return x;
+}
+
+// write-through 16-byte store (global_store_dwordx4 ... sc0 sc1)
+__device__ __forceinline__ void st16_wt(v4u *p, v4u v)
+{
+    typedef __attribute__((address_space(1))) v4u gv4u;
+    *(volatile gv4u *) (gv4u *) p = v;
+}
+
 // 16-byte load from an address that is only element-aligned: gfx950 global
 // loads accept unaligned addresses, so this is still one global_load_dwordx4.
 __device__ __forceinline__ v4u ld16u(const char *p)
@@ -146,6 +161,16 @@ k_contig(const typename C::unit *__restrict__ in, typename C::unit *__restrict__
         else
             return ld16u(cin + 16 * k);
     };
+    bool wt = blockIdx.x >= prm.wt_from ||          // uniform per block
+              (prm.wt_every && blockIdx.x % prm.wt_every == prm.wt_phase);
+    if (prm.wt_xcd)
+        wt = wt || ((prm.wt_xcd >> (xcc_id() & 7)) & 1);
+    auto st = [&](v4u *p, v4u v) {
+        if (wt)
+            st16_wt(p, v);
+        else
+            st16<NTS>(p, v);
+    };
     for (uint64_t i = (uint64_t) blockIdx.x * tile + threadIdx.x; i < npk; i += stride) {
         if (i + (U - 1) * nt < npk) {
             v4u a[U], b[U];
@@ -181,11 +206,11 @@ k_contig(const typename C::unit *__restrict__ in, typename C::unit *__restrict__
                 }
 #pragma unroll
                 for (int u = 0; u < U; ++u)
-                    st16<NTS>(vio + i + u * nt, r[u]);
+                    st(vio + i + u * nt, r[u]);
             } else {
 #pragma unroll
                 for (int u = 0; u < U; ++u)
-                    st16<NTS>(vio + i + u * nt, combine16<C>(a[u], b[u], prm));
+                    st(vio + i + u * nt, combine16<C>(a[u], b[u], prm));
             }
         } else {
             for (int u = 0; u < U; ++u) {
@@ -570,6 +595,11 @@ hipError_t launch_contig(const void *in, void *io, uint64_t count, const Params 
         Params p = prm;
         if (grid > (prm.done_ctr ? kSignalMaxGrid : 1u))
             p.done = nullptr;
+        if (cfg.wt_tail > 0)
+            p.wt_from = grid > (unsigned) cfg.wt_tail ? grid - (unsigned) cfg.wt_tail : 0u;
+        p.wt_every = cfg.wt_every > 0 ? (unsigned) cfg.wt_every : 0u;
+        p.wt_phase = (unsigned) cfg.wt_phase;
+        p.wt_xcd = (unsigned) cfg.wt_xcd & 0xffu;
         signalled = p.done != nullptr;
         if ((ai & 15) == (ao & 15))
             hipLaunchKernelGGL(

@@ -71,6 +71,8 @@ def lib():
             'MPIX_Redop_set_fortran_booleans': ([i32, i32], i32),
             'MPIX_Redop_set_launch': ([i32, i32], i32),
             'MPIX_Redop_get_launch': ([ctypes.POINTER(i32)] * 3, i32),
+            'MPIX_Redop_set_store_policy': ([i32, i32, i32, i32], i32),
+            'MPIX_Redop_get_store_policy': ([ctypes.POINTER(i32)] * 4, i32),
             'MPIX_Redop_set_pageable': ([i32, aint], i32),
             'MPIX_Redop_get_pageable': ([ctypes.POINTER(i32), ctypes.POINTER(aint)], i32),
             'MPIX_Redop_last_error': ([], i32),
@@ -392,6 +394,20 @@ def get_launch():
     b, u, g = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
     lib().MPIX_Redop_get_launch(ctypes.byref(b), ctypes.byref(u), ctypes.byref(g))
     return dict(block=b.value, unroll=u.value, max_grid=g.value)
+
+
+def set_store_policy(xcd_mask=0, every=0, phase=0, tail_blocks=0):
+    """contiguous kernel: blocks on the XCDs of xcd_mask, blocks b with
+    b % every == phase, and the last tail_blocks blocks store write-through
+    (performance knob, same bits)"""
+    return lib().MPIX_Redop_set_store_policy(xcd_mask, every, phase, tail_blocks)
+
+
+def get_store_policy():
+    x, e, p, t = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    check(lib().MPIX_Redop_get_store_policy(ctypes.byref(x), ctypes.byref(e), ctypes.byref(p),
+                                            ctypes.byref(t)))
+    return dict(xcd_mask=x.value, every=e.value, phase=p.value, tail_blocks=t.value)
 
 
 def error_string(code):
