@@ -240,9 +240,16 @@ const Entry *gpu_entry(uint32_t opi, uint32_t it)
 // ---------------------------------------------------------------- state
 std::atomic<long long> g_ftrue{1}, g_ffalse{0};
 std::atomic<int> g_block{256}, g_max_grid{0};
-// MPIX_REDOP_WT_TAIL: the last this-many blocks of a contiguous launch store
-// write-through, so less of the result is left dirty in the XCD L2s for the
-// end-of-kernel write-back (0 = off)
+// Store policy of the contiguous, multi-input and tree kernels
+// (MPIX_Redop_set_store_policy): the blocks running on the XCDs of g_wt_xcd
+// store write-through (sc0 sc1), the others non-temporally.  Two XCDs of eight
+// writing through make the 1 GiB fp32 SUM kernel 8-9 % faster at every operand
+// placement tried, and every config-3 row 1-10 % faster (median 8 %); one XCD
+// gains 4 %, three or four XCDs lose 1-5 %, all eight lose 3 %
+// (profiles/r03_wt_probe_xcd.json, r03_wt_types_xcd88.json,
+// r03_wt_sync_sweeps.txt).  Default: XCDs 3 and 7 on devices of 8 XCDs (SPX),
+// off otherwise.  g_wt_every / g_wt_phase / g_wt_tail select blocks by index
+// instead (the probes' forms).
 std::atomic<int> g_wt_tail{0}, g_wt_every{0}, g_wt_phase{0}, g_wt_xcd{0};
 // completion wait of the synchronous calls: 0 block (hipStreamSynchronize),
 // 1 spin on an event, 2 spin on a pinned host word that a one-workgroup
@@ -316,6 +323,17 @@ void read_env()
         int b = atoi(s);
         if (b >= 64 && b <= 1024 && b % 64 == 0)
             g_block = b;
+    }
+    {
+        int ndev = 0;
+        bool spx = hipGetDeviceCount(&ndev) == hipSuccess && ndev > 0;
+        for (int d = 0; spx && d < ndev; ++d) {
+            int x = 0;
+            spx = hipDeviceGetAttribute(&x, hipDeviceAttributeNumberOfXccs, d) == hipSuccess &&
+                  x == 8;
+        }
+        (void) hipGetLastError();
+        g_wt_xcd = spx ? 0x88 : 0;
     }
     if (const char *s = getenv("MPIX_REDOP_WT_TAIL"))
         g_wt_tail = atoi(s) > 0 ? atoi(s) : 0;
@@ -2168,7 +2186,7 @@ int MPIX_Redop_set_store_policy(int xcd_mask, int every, int phase, int tail_blo
 {
     launch_cfg();
     if (xcd_mask < 0 || xcd_mask > 0xff || every < 0 || phase < 0 ||
-        (every > 0 && phase >= every) || tail_blocks < 0)
+        phase >= (every > 0 ? every : 1) || tail_blocks < 0)
         return MPIX_REDOP_ERR_ARG;
     g_wt_xcd = xcd_mask;
     g_wt_every = every;

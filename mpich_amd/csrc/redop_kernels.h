@@ -71,6 +71,25 @@ __device__ __forceinline__ void st16_wt(v4u *p, v4u v)
     *(volatile gv4u *) (gv4u *) p = v;
 }
 
+// the store policy of this block (Params::wt_*): write-through or not,
+// uniform per block
+__device__ __forceinline__ bool wt_block(const Params &prm)
+{
+    bool wt = blockIdx.x >= prm.wt_from ||
+              (prm.wt_every && blockIdx.x % prm.wt_every == prm.wt_phase);
+    if (prm.wt_xcd)
+        wt = wt || ((prm.wt_xcd >> (xcc_id() & 7)) & 1);
+    return wt;
+}
+
+template <bool NT> __device__ __forceinline__ void st16_pol(v4u *p, v4u v, bool wt)
+{
+    if (wt)
+        st16_wt(p, v);
+    else
+        st16<NT>(p, v);
+}
+
 // 16-byte load from an address that is only element-aligned: gfx950 global
 // loads accept unaligned addresses, so this is still one global_load_dwordx4.
 __device__ __forceinline__ v4u ld16u(const char *p)
@@ -161,16 +180,8 @@ k_contig(const typename C::unit *__restrict__ in, typename C::unit *__restrict__
         else
             return ld16u(cin + 16 * k);
     };
-    bool wt = blockIdx.x >= prm.wt_from ||          // uniform per block
-              (prm.wt_every && blockIdx.x % prm.wt_every == prm.wt_phase);
-    if (prm.wt_xcd)
-        wt = wt || ((prm.wt_xcd >> (xcc_id() & 7)) & 1);
-    auto st = [&](v4u *p, v4u v) {
-        if (wt)
-            st16_wt(p, v);
-        else
-            st16<NTS>(p, v);
-    };
+    const bool wt = wt_block(prm);
+    auto st = [&](v4u *p, v4u v) { st16_pol<NTS>(p, v, wt); };
     for (uint64_t i = (uint64_t) blockIdx.x * tile + threadIdx.x; i < npk; i += stride) {
         if (i + (U - 1) * nt < npk) {
             v4u a[U], b[U];
@@ -264,6 +275,7 @@ k_contig_multi(MultiIn<typename C::unit> ins, int k, typename C::unit *__restric
     const uint64_t nt = blockDim.x;
     const uint64_t tile = nt * U;
     const uint64_t stride = (uint64_t) gridDim.x * tile;
+    const bool wt = wt_block(prm);
     for (uint64_t i = (uint64_t) blockIdx.x * tile + threadIdx.x; i < npk; i += stride) {
         v4u acc[U];
 #pragma unroll
@@ -285,7 +297,7 @@ k_contig_multi(MultiIn<typename C::unit> ins, int k, typename C::unit *__restric
 #pragma unroll
         for (int u = 0; u < U; ++u)
             if (i + u * nt < npk)
-                st16<true>(vio + i + u * nt, acc[u]);
+                st16_pol<true>(vio + i + u * nt, acc[u], wt);
     }
     if (blockIdx.x == 0) {
         for (uint64_t t = threadIdx.x; t < head; t += nt) {
@@ -358,6 +370,7 @@ k_contig_tree(MultiIn<typename C::unit> ins, int k, uint32_t pres, typename C::u
     const uint64_t stride = (uint64_t) gridDim.x * nt * U;
     auto cv = [&](v4u a, v4u b) { return combine16<C>(a, b, prm); };
     auto ce = [&](T a, T b) { return C::apply(a, b, prm); };
+    const bool wt = wt_block(prm);
     for (uint64_t i = (uint64_t) blockIdx.x * nt * U + threadIdx.x; i < npk; i += stride) {
         v4u v[U][KMAX];
 #pragma unroll
@@ -371,7 +384,7 @@ k_contig_tree(MultiIn<typename C::unit> ins, int k, uint32_t pres, typename C::u
             if (i + u * nt >= npk)
                 continue;
             tree_fold<KMAX>(v[u], k, pres, cv);
-            st16<true>(vout + i + u * nt, v[u][0]);
+            st16_pol<true>(vout + i + u * nt, v[u][0], wt);
         }
     }
     if (blockIdx.x == 0) {
@@ -570,6 +583,16 @@ static inline unsigned grid_for(uint64_t work_per_block_units, uint64_t n, int m
     return (unsigned) g;
 }
 
+// The store policy (LaunchCfg::wt_*) of a launch of `grid` blocks.
+inline void set_store_policy(Params &p, const LaunchCfg &cfg, unsigned grid)
+{
+    if (cfg.wt_tail > 0)
+        p.wt_from = grid > (unsigned) cfg.wt_tail ? grid - (unsigned) cfg.wt_tail : 0u;
+    p.wt_every = cfg.wt_every > 0 ? (unsigned) cfg.wt_every : 0u;
+    p.wt_phase = (unsigned) cfg.wt_phase;
+    p.wt_xcd = (unsigned) cfg.wt_xcd & 0xffu;
+}
+
 // Contiguous launcher: chooses the packet or the element-wise kernel.
 template <class C>
 hipError_t launch_contig(const void *in, void *io, uint64_t count, const Params &prm,
@@ -595,11 +618,7 @@ hipError_t launch_contig(const void *in, void *io, uint64_t count, const Params 
         Params p = prm;
         if (grid > (prm.done_ctr ? kSignalMaxGrid : 1u))
             p.done = nullptr;
-        if (cfg.wt_tail > 0)
-            p.wt_from = grid > (unsigned) cfg.wt_tail ? grid - (unsigned) cfg.wt_tail : 0u;
-        p.wt_every = cfg.wt_every > 0 ? (unsigned) cfg.wt_every : 0u;
-        p.wt_phase = (unsigned) cfg.wt_phase;
-        p.wt_xcd = (unsigned) cfg.wt_xcd & 0xffu;
+        set_store_policy(p, cfg, grid);
         signalled = p.done != nullptr;
         if ((ai & 15) == (ao & 15))
             hipLaunchKernelGGL(
@@ -642,8 +661,10 @@ hipError_t launch_multi(const void *const *ins, int k, void *io, uint64_t count,
         uint32_t ntail = (uint32_t) (count - tail_start);
         constexpr int U = 2;
         unsigned grid = grid_for((uint64_t) cfg.block * U, npk, cfg.max_grid);
+        Params p = prm;
+        set_store_policy(p, cfg, grid);
         hipLaunchKernelGGL((k_contig_multi<C, U>), dim3(grid), dim3(cfg.block), 0, s, mi, k, tio,
-                           head, npk, tail_start, ntail, prm);
+                           head, npk, tail_start, ntail, p);
     } else {
         unsigned grid = grid_for((uint64_t) cfg.block * 4, count, cfg.max_grid);
         hipLaunchKernelGGL((k_elem_multi<C>), dim3(grid), dim3(cfg.block), 0, s, mi, k, tio, count,
@@ -671,7 +692,6 @@ hipError_t launch_tree(const void *const *ins, int k, void *out, uint64_t count,
         pres |= 1u << q;
         aligned = aligned && ((reinterpret_cast<uintptr_t>(ins[q]) & 15) == (ao & 15));
     }
-    (void) cfg;
     T *tout = static_cast<T *>(out);
     if (aligned) {
         uint64_t head = ((16 - (ao & 15)) & 15) / sizeof(T);
@@ -680,15 +700,16 @@ hipError_t launch_tree(const void *const *ins, int k, void *out, uint64_t count,
         uint64_t npk = (count - head) / E;
         uint64_t tail_start = head + npk * E;
         uint32_t ntail = (uint32_t) (count - tail_start);
+        Params p = prm;
+        const unsigned grid = grid_for(k == 2 ? 256 * 4 : 256, npk, 0);
+        set_store_policy(p, cfg, grid);
         if (k == 2)     // out = a OP b: the contiguous kernel's 4 packets per lane
-            hipLaunchKernelGGL((k_contig_tree<C, 2, 4>), dim3(grid_for(256 * 4, npk, 0)),
-                               dim3(256), 0, s, mi, k, pres, tout, head, npk, tail_start, ntail,
-                               prm);
+            hipLaunchKernelGGL((k_contig_tree<C, 2, 4>), dim3(grid), dim3(256), 0, s, mi, k, pres,
+                               tout, head, npk, tail_start, ntail, p);
         else            // one 16-slot form for every k (an 8-slot form, more waves in
                         // flight, measured 4-9 % slower at k = 4 and 8)
-            hipLaunchKernelGGL((k_contig_tree<C, kMaxMulti, 1>), dim3(grid_for(256, npk, 0)),
-                               dim3(256), 0, s, mi, k, pres, tout, head, npk, tail_start, ntail,
-                               prm);
+            hipLaunchKernelGGL((k_contig_tree<C, kMaxMulti, 1>), dim3(grid), dim3(256), 0, s, mi,
+                               k, pres, tout, head, npk, tail_start, ntail, p);
     } else {
         hipLaunchKernelGGL((k_elem_tree<C>), dim3(grid_for(256 * 4, count, 0)), dim3(256), 0, s,
                            mi, k, pres, tout, count, prm);

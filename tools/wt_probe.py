@@ -53,7 +53,7 @@ def main(path):
     for off in OFFSETS:
         e = N + off // 4
         places['slab_in_at_1GiB+%d' % off] = (slab[e:e + N], slab[:N])
-    key = lambda pat: '%#x:%d:%d' % pat
+    key = lambda pat: '0x%x:%d:%d' % pat
     res = {p: {key(pat): [] for pat in PATTERNS} for p in places}
     for _ in range(3):
         for pname, (xin, xio) in places.items():
@@ -67,7 +67,7 @@ def main(path):
     for pname, d in res.items():
         med = {k: round(sorted(v)[1], 4) for k, v in d.items()}
         out['kernel_ms'][pname] = med
-        out['vs_none'][pname] = {k: round(med['0:0:0'] / v, 4) for k, v in med.items()}
+        out['vs_none'][pname] = {k: round(med['0x0:0:0'] / v, 4) for k, v in med.items()}
     sizes = {}
     for mib in (16, 64, 256, 1024):
         m = mib * (1 << 20) // 4
