@@ -77,6 +77,7 @@ def bench_lib():
     L = ctypes.CDLL(path)
     L.mpix_bench_triad.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                    ctypes.c_float, ctypes.c_uint64, ctypes.c_void_p]
+    L.mpix_bench_triad_xcd.argtypes = L.mpix_bench_triad.argtypes + [ctypes.c_uint]
     L.mpix_bench_call_latency.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                           ctypes.POINTER(ctypes.c_double),
@@ -448,6 +449,18 @@ def single_gpu(args, dev):
         triad = nbytes_alg / (tri_avg * 1e-3) / 1e9
         result['roofline']['triad_measured_GBs'] = round(triad, 1)
         result['roofline']['frac_of_triad'] = round(achieved / triad, 4)
+        # the same triad with the library's store policy (the blocks of two
+        # XCDs store write-through): how much of the combine's lead over the
+        # plain triad is the policy, which any streaming kernel can use
+        pol = redop.get_store_policy()
+        if pol['xcd_mask']:
+            trx_avg, _, _ = event_time_per_launch(
+                lambda: B.mpix_bench_triad_xcd(a3.data_ptr(), inb.data_ptr(), inout.data_ptr(),
+                                               ctypes.c_float(0.5), n, stream.cuda_stream,
+                                               pol['xcd_mask']), kreps, stream)
+            trx = nbytes_alg / (trx_avg * 1e-3) / 1e9
+            result['roofline']['triad_store_policy_GBs'] = round(trx, 1)
+            result['roofline']['frac_of_triad_store_policy'] = round(achieved / trx, 4)
         del a3
         result['sync_call_latency'] = sync_call_latency(B, dev)
         result['chunked_async_c'] = chunked_async_c(

@@ -13,12 +13,24 @@
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
+typedef __attribute__((address_space(1))) f4 gf4;
+
+// xcd_mask: the blocks on these XCDs (HW_REG_XCC_ID) store write-through
+// (sc0 sc1), the rest non-temporally -- the library's store policy, so the
+// triad can be read with and without it (0: the plain STREAM triad)
 template <int U>
 __global__ void __launch_bounds__(256) k_triad(f4 *__restrict__ a, const f4 *__restrict__ b,
-                                               const f4 *__restrict__ c, float q, uint64_t n4)
+                                               const f4 *__restrict__ c, float q, uint64_t n4,
+                                               unsigned xcd_mask)
 {
     const uint64_t nt = blockDim.x;
     uint64_t i = (uint64_t) blockIdx.x * nt * U + threadIdx.x;
+    bool wt = false;
+    if (xcd_mask) {
+        unsigned x;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+        wt = (xcd_mask >> (x & 7)) & 1;
+    }
     f4 x[U], y[U];
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -28,12 +40,16 @@ __global__ void __launch_bounds__(256) k_triad(f4 *__restrict__ a, const f4 *__r
         }
 #pragma unroll
     for (int u = 0; u < U; ++u)
-        if (i + u * nt < n4)
-            __builtin_nontemporal_store(x[u] + q * y[u], a + i + u * nt);
+        if (i + u * nt < n4) {
+            if (wt)
+                *(volatile gf4 *) (gf4 *) (a + i + u * nt) = x[u] + q * y[u];
+            else
+                __builtin_nontemporal_store(x[u] + q * y[u], a + i + u * nt);
+        }
 }
 
-extern "C" int mpix_bench_triad(float *a, const float *b, const float *c, float q, uint64_t n,
-                                void *stream)
+extern "C" int mpix_bench_triad_xcd(float *a, const float *b, const float *c, float q, uint64_t n,
+                                    void *stream, unsigned xcd_mask)
 {
     if (n % 4 || ((uintptr_t) a | (uintptr_t) b | (uintptr_t) c) % 16)
         return 12;
@@ -43,8 +59,14 @@ extern "C" int mpix_bench_triad(float *a, const float *b, const float *c, float 
     if (grid == 0)
         grid = 1;
     hipLaunchKernelGGL((k_triad<U>), dim3((unsigned) grid), dim3(T), 0, (hipStream_t) stream,
-                       (f4 *) a, (const f4 *) b, (const f4 *) c, q, n4);
+                       (f4 *) a, (const f4 *) b, (const f4 *) c, q, n4, xcd_mask & 0xffu);
     return hipGetLastError() == hipSuccess ? 0 : 15;
+}
+
+extern "C" int mpix_bench_triad(float *a, const float *b, const float *c, float q, uint64_t n,
+                                void *stream)
+{
+    return mpix_bench_triad_xcd(a, b, c, q, n, stream, 0);
 }
 
 // Per-call host time of a synchronous reduce entry point (passed as a
