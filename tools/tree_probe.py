@@ -33,7 +33,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--mib', type=int, default=256)
     ap.add_argument('--out', default=None)
+    ap.add_argument('--xcd', type=lambda x: int(x, 0), default=None,
+                    help='store policy XCD mask (MPIX_Redop_set_store_policy); default: the library\'s')
     a = ap.parse_args()
+    if a.xcd is not None:
+        redop.check(redop.set_store_policy(a.xcd, 0, 0, 0))
     n = a.mib * (1 << 20) // 4
     s = torch.cuda.Stream()
     rows = []
@@ -89,7 +93,8 @@ def main():
                         memcpy_ms=round(tm * 1e3, 4),
                         memcpy_GBs=round(2 * 7 * n * 4 / tm / 1e9, 1))
         del src, dst
-    line = json.dumps({'tree_probe': rows, 'copy_multi': copy_row})
+    line = json.dumps({'tree_probe': rows, 'copy_multi': copy_row,
+                       'store_policy': redop.get_store_policy()})
     print(line)
     if a.out:
         with open(a.out, 'w') as f:
