@@ -240,7 +240,7 @@ const Entry *gpu_entry(uint32_t opi, uint32_t it)
 // ---------------------------------------------------------------- state
 std::atomic<long long> g_ftrue{1}, g_ffalse{0};
 std::atomic<int> g_block{256}, g_max_grid{0};
-// Store policy of the contiguous, multi-input and tree kernels
+// Store policy of the contiguous and multi-input kernels and the two-slot tree
 // (MPIX_Redop_set_store_policy): the blocks running on the XCDs of g_wt_xcd
 // store write-through (sc0 sc1), the others non-temporally.  Two XCDs of eight
 // writing through make the 1 GiB fp32 SUM kernel 8-9 % faster at every operand

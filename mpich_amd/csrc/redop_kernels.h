@@ -702,7 +702,10 @@ hipError_t launch_tree(const void *const *ins, int k, void *out, uint64_t count,
         uint32_t ntail = (uint32_t) (count - tail_start);
         Params p = prm;
         const unsigned grid = grid_for(k == 2 ? 256 * 4 : 256, npk, 0);
-        set_store_policy(p, cfg, grid);
+        // the store policy pays for the k = 2 form (+5 %); the 16-slot form
+        // gains nothing at k = 4 / 8 / 16 (profiles/r03_tree_probe_policy.json)
+        if (k == 2)
+            set_store_policy(p, cfg, grid);
         if (k == 2)     // out = a OP b: the contiguous kernel's 4 packets per lane
             hipLaunchKernelGGL((k_contig_tree<C, 2, 4>), dim3(grid), dim3(256), 0, s, mi, k, pres,
                                tout, head, npk, tail_start, ntail, p);
