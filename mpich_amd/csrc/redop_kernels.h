@@ -211,13 +211,20 @@ k_contig(const typename C::unit *__restrict__ in, typename C::unit *__restrict__
                 for (int u = 0; u < U; ++u)
                     r[u] = combine16_fast<C>(a[u], b[u], prm, need);
                 if (__builtin_expect(need, 0)) {
+                    // the rare full form: one packet at a time from memory
+                    // again (inout is not written yet), so the tile's
+                    // registers are dead here and the slow path cannot push
+                    // the kernel past the 128-VGPR cap into scratch
+#pragma unroll 1
+                    for (int u = 0; u < U; ++u) {
+                        const uint64_t k = i + u * nt;
+                        st(vio + k, combine16<C>(ld16<NTL>(vio + k), ldin(k), prm));
+                    }
+                } else {
 #pragma unroll
                     for (int u = 0; u < U; ++u)
-                        r[u] = combine16<C>(a[u], b[u], prm);
+                        st(vio + i + u * nt, r[u]);
                 }
-#pragma unroll
-                for (int u = 0; u < U; ++u)
-                    st(vio + i + u * nt, r[u]);
             } else {
 #pragma unroll
                 for (int u = 0; u < U; ++u)
