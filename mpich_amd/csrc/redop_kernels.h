@@ -108,8 +108,24 @@ struct HasApply4<C, decltype((void) C::apply4(0u, 0u))> {
     static constexpr bool value = sizeof(typename C::unit) == 1;
 };
 
+// ... or apply4p(dword, dword, prm) when they need the runtime parameters
+template <class C, class = void> struct HasApply4P {
+    static constexpr bool value = false;
+};
+template <class C>
+struct HasApply4P<C, decltype((void) C::apply4p(0u, 0u, *(const Params *) nullptr))> {
+    static constexpr bool value = sizeof(typename C::unit) == 1;
+};
+
 template <class C> __device__ __forceinline__ v4u combine16(v4u a, v4u b, const Params &prm)
 {
+    if constexpr (HasApply4P<C>::value) {
+        v4u r;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            r[e] = C::apply4p(a[e], b[e], prm);
+        return r;
+    }
     if constexpr (HasApply4<C>::value) {
         v4u r;
 #pragma unroll

@@ -102,11 +102,34 @@ template <typename T> MPIX_DEV T flog_to(int c, const Params &p)
 {
     return (T) (c ? p.ftrue : p.ffalse);
 }
+// Kind-1 logicals four per dword (combine16 uses apply4p when a 1-byte
+// combiner has it; the byte-array form needed scratch on gfx950): bit 7 of
+// every byte that is .TRUE., i.e. differs from .FALSE. as flog_from compares
+// (in int: a .FALSE. outside -128..127 equals no byte), and the results as
+// the low bytes of .TRUE. / .FALSE. as flog_to casts them.  Byte for byte
+// the same as apply() (tests/test_swar.py).
+MPIX_DEV uint32_t flog_true_bytes(uint32_t x, const Params &p)
+{
+    const int f = (int) p.ffalse;
+    if (f < -128 || f > 127)
+        return 0x80808080u;
+    return nz_bytes(x ^ ((uint32_t) (uint8_t) f * 0x01010101u));
+}
+MPIX_DEV uint32_t flog_to_bytes(uint32_t t, const Params &p)
+{
+    const uint32_t m = (t >> 7) * 0xffu;
+    return ((uint32_t) (uint8_t) p.ftrue * 0x01010101u & m) |
+           ((uint32_t) (uint8_t) p.ffalse * 0x01010101u & ~m);
+}
 template <typename T> struct FLand {
     using unit = T;
     static MPIX_DEV T apply(T a, T b, const Params &p)
     {
         return flog_to<T>(flog_from(a, p) & flog_from(b, p), p);
+    }
+    static MPIX_DEV uint32_t apply4p(uint32_t a, uint32_t b, const Params &p)
+    {
+        return flog_to_bytes(flog_true_bytes(a, p) & flog_true_bytes(b, p), p);
     }
 };
 template <typename T> struct FLor {
@@ -115,12 +138,20 @@ template <typename T> struct FLor {
     {
         return flog_to<T>(flog_from(a, p) | flog_from(b, p), p);
     }
+    static MPIX_DEV uint32_t apply4p(uint32_t a, uint32_t b, const Params &p)
+    {
+        return flog_to_bytes(flog_true_bytes(a, p) | flog_true_bytes(b, p), p);
+    }
 };
 template <typename T> struct FLxor {
     using unit = T;
     static MPIX_DEV T apply(T a, T b, const Params &p)
     {
         return flog_to<T>(flog_from(a, p) ^ flog_from(b, p), p);
+    }
+    static MPIX_DEV uint32_t apply4p(uint32_t a, uint32_t b, const Params &p)
+    {
+        return flog_to_bytes(flog_true_bytes(a, p) ^ flog_true_bytes(b, p), p);
     }
 };
 

@@ -31,3 +31,48 @@ def test_swar_logicals_every_byte_pair():
         for k in got:
             g = got[k].astype(np.uint32).view(np.uint8).reshape(-1, 4)
             assert np.array_equal(g, exp[k].astype(np.uint8)), (k, lane)
+
+
+def _to_int32(v):
+    """C's (int) conversion of a long long (two's complement wrap)"""
+    v &= 0xffffffff
+    return v - (1 << 32) if v >= (1 << 31) else v
+
+
+def test_swar_fortran_logical1_every_byte_pair():
+    """FLand/FLor/FLxor<int8_t>::apply4p (redop_ops.h: flog_true_bytes,
+    flog_to_bytes) against the per-element rule of mpii_fortlogical.h:13-29 as
+    the kernels' apply() restates it: a byte is .TRUE. unless (int) byte ==
+    (int) .FALSE., and the result is (int8_t) (.TRUE. or .FALSE.), for
+    .TRUE./.FALSE. encodings inside and outside the kind's range"""
+    a8, b8 = np.meshgrid(np.arange(256, dtype=np.uint8), np.arange(256, dtype=np.uint8))
+    a8, b8 = a8.ravel(), b8.ravel()
+    rng = np.random.default_rng(0x5EED5B)
+    for ftrue, ffalse in ((1, 0), (-1, 0), (0, 1), (255, 0), (1, -1), (7, 300), (1, 1 << 33),
+                          (-1 << 40, 0x80)):
+        f = _to_int32(ffalse)
+        fits = -128 <= f <= 127
+        trb, fab = np.uint32(ftrue & 0xff), np.uint32(ffalse & 0xff)
+        for lane in range(4):
+            fill_a = rng.integers(0, 256, (a8.size, 4), dtype=np.uint8)
+            fill_b = rng.integers(0, 256, (a8.size, 4), dtype=np.uint8)
+            fill_a[:, lane], fill_b[:, lane] = a8, b8
+            A = fill_a.copy().view(np.uint32).ravel()
+            B = fill_b.copy().view(np.uint32).ravel()
+
+            def true_bytes(x):
+                if not fits:
+                    return np.full_like(x, 0x80808080)
+                return nz_bytes(x ^ np.uint32((f & 0xff) * 0x01010101))
+
+            def to_bytes(t):
+                m = (t >> np.uint32(7)) * np.uint32(0xff)
+                return (trb * np.uint32(0x01010101) & m) | (fab * np.uint32(0x01010101) & ~m)
+            ta, tb = true_bytes(A), true_bytes(B)
+            got = {'land': to_bytes(ta & tb), 'lor': to_bytes(ta | tb), 'lxor': to_bytes(ta ^ tb)}
+            la = fill_a.astype(np.int8).astype(np.int32) != f      # flog_from in int
+            lb = fill_b.astype(np.int8).astype(np.int32) != f
+            for k, c in (('land', la & lb), ('lor', la | lb), ('lxor', la ^ lb)):
+                exp = np.where(c, np.uint8(ftrue & 0xff), np.uint8(ffalse & 0xff))
+                g = got[k].astype(np.uint32).view(np.uint8).reshape(-1, 4)
+                assert np.array_equal(g, exp), (k, lane, ftrue, ffalse)
