@@ -92,8 +92,11 @@ struct CopySegs {
     uint64_t bytes[kMaxMultiInputs];
 };
 
-__global__ void __launch_bounds__(256) k_copy_multi(CopySegs sg)
+// wt_xcd: the store policy of the contiguous kernel (blocks on these XCDs
+// store write-through)
+__global__ void __launch_bounds__(256) k_copy_multi(CopySegs sg, unsigned wt_xcd)
 {
+    const bool wt = wt_xcd && ((wt_xcd >> (xcc_id() & 7)) & 1);
     const int q = blockIdx.y;
     const unsigned char *src = sg.src[q];
     unsigned char *dst = sg.dst[q];
@@ -107,7 +110,7 @@ __global__ void __launch_bounds__(256) k_copy_multi(CopySegs sg)
         const v4u *vs = reinterpret_cast<const v4u *>(src + head);
         v4u *vd = reinterpret_cast<v4u *>(dst + head);
         for (uint64_t k = t0; k < npk; k += stride)
-            st16<true>(vd + k, ld16<true>(vs + k));
+            st16_pol<true>(vd + k, ld16<true>(vs + k), wt);
         if (blockIdx.x == 0) {
             for (uint64_t t = threadIdx.x; t < head; t += blockDim.x)
                 dst[t] = src[t];
@@ -121,7 +124,7 @@ __global__ void __launch_bounds__(256) k_copy_multi(CopySegs sg)
 }
 
 hipError_t launch_copy_multi(const void *const *srcs, void *const *dsts, const uint64_t *bytes,
-                             int n, hipStream_t s)
+                             int n, hipStream_t s, unsigned wt_xcd)
 {
     CopySegs sg{};
     uint64_t most = 0;
@@ -133,7 +136,7 @@ hipError_t launch_copy_multi(const void *const *srcs, void *const *dsts, const u
     }
     // about 2048 workgroups in all: each segment's share of the 256 CUs
     unsigned gx = grid_for(256ull * 16 * 4, most, (int) (2048 / (unsigned) n));
-    hipLaunchKernelGGL(k_copy_multi, dim3(gx, (unsigned) n), dim3(256), 0, s, sg);
+    hipLaunchKernelGGL(k_copy_multi, dim3(gx, (unsigned) n), dim3(256), 0, s, sg, wt_xcd & 0xffu);
     return hipGetLastError();
 }
 

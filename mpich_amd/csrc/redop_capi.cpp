@@ -2016,7 +2016,8 @@ int MPIX_Copy_multi_async(const void *const *srcs, void *const *dsts, const MPIX
     if (!m)
         return set_err(MPIX_REDOP_SUCCESS);
     launch_cfg();
-    return set_err(hip_err(mpix::launch_copy_multi(ds, dd, nb, m, (hipStream_t) stream)));
+    return set_err(hip_err(mpix::launch_copy_multi(ds, dd, nb, m, (hipStream_t) stream,
+                                                   (unsigned) launch_cfg().wt_xcd)));
 }
 
 int MPIX_Ipc_export(const void *devptr, void *handle_out, MPIX_Aint *offset_out)

@@ -70,7 +70,7 @@ hipError_t launch_equal(const void *in, void *io, uint64_t n, hipStream_t s);
 
 // up to kMaxMultiInputs independent device copies in one launch
 hipError_t launch_copy_multi(const void *const *srcs, void *const *dsts, const uint64_t *bytes,
-                             int n, hipStream_t s);
+                             int n, hipStream_t s, unsigned wt_xcd = 0);
 
 // compile-time unroll of the packet kernel (packets per lane per operand)
 int unroll();
