@@ -57,7 +57,8 @@ template <int M> __device__ __forceinline__ void st(v4u *p, v4u v)
         *(volatile gv4u *) (gv4u *) p = v;
 }
 
-template <int U, int LA, int SA, int LB, int SB>
+// ORD: 0 all inout loads then all in loads (shipped), 1 alternating, 2 in first
+template <int U, int LA, int SA, int LB, int SB, int ORD = 0>
 __device__ __forceinline__ void tile(const v4u *__restrict__ in, v4u *__restrict__ io, uint64_t npk,
                                      uint64_t i, uint64_t nt)
 {
@@ -73,12 +74,27 @@ __device__ __forceinline__ void tile(const v4u *__restrict__ in, v4u *__restrict
         return;
     }
     v4u a[U], b[U];
+    if constexpr (ORD == 0) {
 #pragma unroll
-    for (int u = 0; u < U; ++u)
-        a[u] = ld<LA>(io + i + u * nt);
+        for (int u = 0; u < U; ++u)
+            a[u] = ld<LA>(io + i + u * nt);
 #pragma unroll
-    for (int u = 0; u < U; ++u)
-        b[u] = ld<LA>(in + i + u * nt);
+        for (int u = 0; u < U; ++u)
+            b[u] = ld<LA>(in + i + u * nt);
+    } else if constexpr (ORD == 1) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            a[u] = ld<LA>(io + i + u * nt);
+            b[u] = ld<LA>(in + i + u * nt);
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            b[u] = ld<LA>(in + i + u * nt);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            a[u] = ld<LA>(io + i + u * nt);
+    }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -91,7 +107,7 @@ __device__ __forceinline__ void tile(const v4u *__restrict__ in, v4u *__restrict
 }
 
 // group A = XCDs in `mask` (loads LA, stores SA), group B = the others (LB, SB)
-template <int U, int LA, int SA, int LB, int SB>
+template <int U, int LA, int SA, int LB, int SB, int ORD = 0>
 __global__ void __launch_bounds__(1024) k_pol(const v4u *__restrict__ in, v4u *__restrict__ io,
                                               uint64_t npk, unsigned mask)
 {
@@ -100,9 +116,9 @@ __global__ void __launch_bounds__(1024) k_pol(const v4u *__restrict__ in, v4u *_
     if (i >= npk)
         return;
     if ((mask >> xcc()) & 1)
-        tile<U, LA, SA, LB, SB>(in, io, npk, i, nt);
+        tile<U, LA, SA, LB, SB, ORD>(in, io, npk, i, nt);
     else
-        tile<U, LB, SB, LA, SA>(in, io, npk, i, nt);
+        tile<U, LB, SB, LA, SA, ORD>(in, io, npk, i, nt);
 }
 
 struct Var {
@@ -113,11 +129,11 @@ struct Var {
     std::vector<float> ms;
 };
 
-template <int U, int LA, int SA, int LB, int SB>
+template <int U, int LA, int SA, int LB, int SB, int ORD = 0>
 void launch(const v4u *in, v4u *io, uint64_t npk, unsigned mask, int block, hipStream_t s)
 {
     const uint64_t tile = (uint64_t) block * U;
-    hipLaunchKernelGGL((k_pol<U, LA, SA, LB, SB>), dim3((unsigned) ((npk + tile - 1) / tile)),
+    hipLaunchKernelGGL((k_pol<U, LA, SA, LB, SB, ORD>), dim3((unsigned) ((npk + tile - 1) / tile)),
                        dim3(block), 0, s, in, io, npk, mask);
 }
 
@@ -161,6 +177,11 @@ int main()
         {"store_plain_0x08 (one XCD)", launch<4, 0, 1, 0, 0>, 0x08, 256, {}},
         {"store_plain_0x8c (three XCDs)", launch<4, 0, 1, 0, 0>, 0x8c, 256, {}},
         {"store_wt_0x88 U=4 block 192", launch<4, 0, 2, 0, 0>, 0x88, 192, {}},
+        {"store_wt_0x88 loads alternating", launch<4, 0, 2, 0, 0, 1>, 0x88, 256, {}},
+        {"store_wt_0x88 in loads first", launch<4, 0, 2, 0, 0, 2>, 0x88, 256, {}},
+        {"all_nt loads alternating", launch<4, 0, 0, 0, 0, 1>, 0x00, 256, {}},
+        {"store_wt_0x88 U=3", launch<3, 0, 2, 0, 0>, 0x88, 256, {}},
+        {"store_wt_0x88 U=6", launch<6, 0, 2, 0, 0>, 0x88, 256, {}},
     };
     // parity: every variant from the same inout gives the plain kernel's bits
     // (device-to-device copies on the launch stream: a hipMemcpy D2D may
