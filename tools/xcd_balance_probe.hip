@@ -72,6 +72,15 @@ __global__ void __launch_bounds__(256) k_rec(const v4u *__restrict__ in, v4u *__
 // Persistent form: G blocks take 16 KiB tiles by ticket (the next ticket is
 // fetched while the current tile is in flight), so an XCD that runs faster
 // takes more tiles; tiles per XCD are counted in cnt[8].
+// LIGHT: the loop's barrier waits for LDS only (s_waitcnt lgkmcnt(0);
+// s_barrier), not for the tile's stores as __syncthreads()'s workgroup fence
+// does (s_waitcnt vmcnt(0)), so stores drain while the next tile loads
+__device__ __forceinline__ void bar_lds()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+template <bool LIGHT>
 __global__ void __launch_bounds__(256) k_pers(const v4u *__restrict__ in, v4u *__restrict__ io,
                                               uint64_t ntiles, unsigned mask, unsigned *ctr,
                                               unsigned *cnt)
@@ -106,7 +115,10 @@ __global__ void __launch_bounds__(256) k_pers(const v4u *__restrict__ in, v4u *_
                 __builtin_nontemporal_store(__builtin_bit_cast(v4u, p), io + i + u * NT);
         }
         ++mine;
-        __syncthreads();
+        if (LIGHT)
+            bar_lds();
+        else
+            __syncthreads();
         cur ^= 1;
         t = s_t[cur];
     }
@@ -160,17 +172,23 @@ int main()
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    const unsigned grids[] = {0, 1024, 2048, 4096, 0, 1024, 2048, 4096};
-    for (int r = 0; r < 8; ++r) {
-        const unsigned G = grids[r];
+    // grid 0: the one-tile-per-block kernel; > 0: persistent with __syncthreads;
+    // < 0 (as int): persistent with the LDS-only barrier
+    const int grids[] = {0, 2048, -1024, -2048, -4096, 0, 2048, -1024, -2048, -4096};
+    for (int r = 0; r < 10; ++r) {
+        const bool light = grids[r] < 0;
+        const unsigned G = (unsigned) (grids[r] < 0 ? -grids[r] : grids[r]);
         float tot = 0;
         unsigned cnt[8] = {0};
         for (int rep = 0; rep < 11; ++rep) {
             CK(hipMemsetAsync(ctr, 0, 64, 0));
             CK(hipEventRecord(e0, 0));
-            if (G)
-                hipLaunchKernelGGL(k_pers, dim3(G), dim3(NT), 0, 0, in, io, (uint64_t) grid, 0x88u,
-                                   ctr, ctr + 4);
+            if (G && light)
+                hipLaunchKernelGGL(k_pers<true>, dim3(G), dim3(NT), 0, 0, in, io, (uint64_t) grid,
+                                   0x88u, ctr, ctr + 4);
+            else if (G)
+                hipLaunchKernelGGL(k_pers<false>, dim3(G), dim3(NT), 0, 0, in, io, (uint64_t) grid,
+                                   0x88u, ctr, ctr + 4);
             else
                 hipLaunchKernelGGL(k_rec, dim3(grid), dim3(NT), 0, 0, in, io, npk, 0x88u, rec);
             CK(hipEventRecord(e1, 0));
@@ -186,7 +204,8 @@ int main()
                     cnt[k] = h2[4 + k];
             }
         }
-        printf("%s{\"grid\": %u, \"ms\": %.4f, \"tiles_per_xcd\": [", r ? ", " : "", G, tot / 10);
+        printf("%s{\"grid\": %u, \"lds_only_barrier\": %s, \"ms\": %.4f, \"tiles_per_xcd\": [",
+               r ? ", " : "", G, light ? "true" : "false", tot / 10);
         for (int k = 0; k < 8; ++k)
             printf("%s%u", k ? ", " : "", cnt[k]);
         printf("]}");
