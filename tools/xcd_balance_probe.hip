@@ -126,6 +126,49 @@ __global__ void __launch_bounds__(256) k_pers(const v4u *__restrict__ in, v4u *_
         atomicAdd(&cnt[x], mine);
 }
 
+// Tile stealing: a grid of (ntiles - K) blocks, each takes tiles by ticket
+// until they run out -- most blocks do one tile, and the blocks that finish
+// while tickets remain (those on the fast XCDs) take the rest.
+__global__ void __launch_bounds__(256) k_steal(const v4u *__restrict__ in, v4u *__restrict__ io,
+                                               uint64_t ntiles, unsigned mask, unsigned *ctr,
+                                               unsigned *cnt)
+{
+    __shared__ unsigned s_t;
+    const unsigned x = xcc();
+    const bool wt = (mask >> x) & 1;
+    unsigned mine = 0;
+    for (;;) {
+        if (threadIdx.x == 0)
+            s_t = atomicAdd(ctr, 1u);
+        __syncthreads();
+        const unsigned t = s_t;
+        if (t >= ntiles)
+            break;
+        const uint64_t i = (uint64_t) t * NT * U + threadIdx.x;
+        v4u a[U], b[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            a[u] = __builtin_nontemporal_load(io + i + u * NT);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            b[u] = __builtin_nontemporal_load(in + i + u * NT);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            float4 p = __builtin_bit_cast(float4, a[u]), q = __builtin_bit_cast(float4, b[u]);
+            p.x += q.x; p.y += q.y; p.z += q.z; p.w += q.w;
+            if (wt)
+                *(volatile gv4u *) (gv4u *) (io + i + u * NT) = __builtin_bit_cast(v4u, p);
+            else
+                __builtin_nontemporal_store(__builtin_bit_cast(v4u, p), io + i + u * NT);
+        }
+        ++mine;
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    if (threadIdx.x == 0 && mine > 1)
+        atomicAdd(&cnt[x], mine - 1);       // extra tiles taken on this XCD
+}
+
 int main()
 {
     const size_t bytes = (size_t) 1 << 30;
@@ -206,6 +249,40 @@ int main()
         }
         printf("%s{\"grid\": %u, \"lds_only_barrier\": %s, \"ms\": %.4f, \"tiles_per_xcd\": [",
                r ? ", " : "", G, light ? "true" : "false", tot / 10);
+        for (int k = 0; k < 8; ++k)
+            printf("%s%u", k ? ", " : "", cnt[k]);
+        printf("]}");
+    }
+    printf("], \"steal\": [");
+    const double fr[] = {0.0, 0.0, 0.01, 0.03, 0.06, 0.0, 0.01, 0.03, 0.06};
+    for (int r = 0; r < 9; ++r) {
+        const bool plain = r == 0;
+        const unsigned G = grid - (unsigned) (fr[r] * grid);
+        float tot = 0;
+        unsigned cnt[8] = {0};
+        for (int rep = 0; rep < 11; ++rep) {
+            CK(hipMemsetAsync(ctr, 0, 64, 0));
+            CK(hipEventRecord(e0, 0));
+            if (plain)
+                hipLaunchKernelGGL(k_rec, dim3(grid), dim3(NT), 0, 0, in, io, npk, 0x88u, rec);
+            else
+                hipLaunchKernelGGL(k_steal, dim3(G), dim3(NT), 0, 0, in, io, (uint64_t) grid, 0x88u,
+                                   ctr, ctr + 4);
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            if (rep)
+                tot += ms;
+            if (!plain && rep == 10) {
+                unsigned h2[12];
+                CK(hipMemcpy(h2, ctr, 48, hipMemcpyDeviceToHost));
+                for (int k = 0; k < 8; ++k)
+                    cnt[k] = h2[4 + k];
+            }
+        }
+        printf("%s{\"one_tile_per_block\": %s, \"blocks\": %u, \"ms\": %.4f, \"extra_tiles_per_xcd\": [",
+               r ? ", " : "", plain ? "true" : "false", plain ? grid : G, tot / 10);
         for (int k = 0; k < 8; ++k)
             printf("%s%u", k ? ", " : "", cnt[k]);
         printf("]}");
