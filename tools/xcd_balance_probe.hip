@@ -34,13 +34,20 @@ __device__ __forceinline__ unsigned xcc()
 
 constexpr int U = 4, NT = 256;
 
+// ROT: block b takes tile 8*(b/8) + (b % 8 + b/8) % 8 -- a rotation inside
+// every group of eight tiles, so the blocks of one XCD (b % 8 fixed under
+// round-robin dispatch) visit every address residue mod 8 tiles instead of one
+template <bool ROT = false>
 __global__ void __launch_bounds__(256) k_rec(const v4u *__restrict__ in, v4u *__restrict__ io,
                                              uint64_t npk, unsigned mask, uint64_t *rec)
 {
     const uint64_t t0 = wall_clock64();
     const unsigned x = xcc();
     const bool wt = (mask >> x) & 1;
-    const uint64_t i = (uint64_t) blockIdx.x * NT * U + threadIdx.x;
+    uint64_t tileno = blockIdx.x;
+    if (ROT)
+        tileno = (tileno & ~7ull) | (((tileno & 7) + (tileno >> 3)) & 7);
+    const uint64_t i = tileno * NT * U + threadIdx.x;
     if (i + (U - 1) * NT < npk) {
         v4u a[U], b[U];
 #pragma unroll
@@ -184,11 +191,18 @@ int main()
     CK(hipDeviceSynchronize());
     std::vector<uint64_t> h((size_t) grid * 3);
     printf("{\"probe\": \"xcd_balance_probe\", \"grid\": %u, \"runs\": [", grid);
-    const unsigned masks[] = {0x00, 0x88, 0x00, 0x88};
-    for (int r = 0; r < 4; ++r) {
+    const unsigned masks[] = {0x00, 0x88, 0x00, 0x88, 0x00, 0x88, 0x00, 0x88};
+    for (int r = 0; r < 8; ++r) {
+        const bool rot = r >= 4;
+        auto go = [&]() {
+            if (rot)
+                hipLaunchKernelGGL(k_rec<true>, dim3(grid), dim3(NT), 0, 0, in, io, npk, masks[r], rec);
+            else
+                hipLaunchKernelGGL(k_rec<false>, dim3(grid), dim3(NT), 0, 0, in, io, npk, masks[r], rec);
+        };
         for (int w = 0; w < 3; ++w)     // warm-up launches, then the recorded one
-            hipLaunchKernelGGL(k_rec, dim3(grid), dim3(NT), 0, 0, in, io, npk, masks[r], rec);
-        hipLaunchKernelGGL(k_rec, dim3(grid), dim3(NT), 0, 0, in, io, npk, masks[r], rec);
+            go();
+        go();
         CK(hipDeviceSynchronize());
         CK(hipMemcpy(h.data(), rec, h.size() * 8, hipMemcpyDeviceToHost));
         uint64_t t_start = ~0ull, t_end = 0;
@@ -201,8 +215,8 @@ int main()
             ++nblk[x];
             dur[x] += h[3 * b + 2] - h[3 * b + 1];
         }
-        printf("%s{\"mask\": %u, \"span_us\": %.2f, \"xcd\": [", r ? ", " : "", masks[r],
-               (t_end - t_start) / 100.0);
+        printf("%s{\"mask\": %u, \"rotated\": %s, \"span_us\": %.2f, \"xcd\": [", r ? ", " : "",
+               masks[r], rot ? "true" : "false", (t_end - t_start) / 100.0);
         for (int x = 0; x < 8; ++x)
             printf("%s{\"blocks\": %llu, \"last_end_us\": %.2f, \"mean_block_us\": %.3f}", x ? ", " : "",
                    (unsigned long long) nblk[x], (last[x] - t_start) / 100.0,
@@ -233,7 +247,7 @@ int main()
                 hipLaunchKernelGGL(k_pers<false>, dim3(G), dim3(NT), 0, 0, in, io, (uint64_t) grid,
                                    0x88u, ctr, ctr + 4);
             else
-                hipLaunchKernelGGL(k_rec, dim3(grid), dim3(NT), 0, 0, in, io, npk, 0x88u, rec);
+                hipLaunchKernelGGL(k_rec<false>, dim3(grid), dim3(NT), 0, 0, in, io, npk, 0x88u, rec);
             CK(hipEventRecord(e1, 0));
             CK(hipEventSynchronize(e1));
             float ms;
@@ -253,6 +267,25 @@ int main()
             printf("%s%u", k ? ", " : "", cnt[k]);
         printf("]}");
     }
+    printf("], \"timed\": [");
+    for (int r = 0; r < 6; ++r) {
+        const bool rot = r % 2;
+        float tot = 0;
+        for (int rep = 0; rep < 11; ++rep) {
+            CK(hipEventRecord(e0, 0));
+            if (rot)
+                hipLaunchKernelGGL(k_rec<true>, dim3(grid), dim3(NT), 0, 0, in, io, npk, 0x88u, rec);
+            else
+                hipLaunchKernelGGL(k_rec<false>, dim3(grid), dim3(NT), 0, 0, in, io, npk, 0x88u, rec);
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            if (rep)
+                tot += ms;
+        }
+        printf("%s{\"rotated\": %s, \"ms\": %.4f}", r ? ", " : "", rot ? "true" : "false", tot / 10);
+    }
     printf("], \"steal\": [");
     const double fr[] = {0.0, 0.0, 0.01, 0.03, 0.06, 0.0, 0.01, 0.03, 0.06};
     for (int r = 0; r < 9; ++r) {
@@ -264,7 +297,7 @@ int main()
             CK(hipMemsetAsync(ctr, 0, 64, 0));
             CK(hipEventRecord(e0, 0));
             if (plain)
-                hipLaunchKernelGGL(k_rec, dim3(grid), dim3(NT), 0, 0, in, io, npk, 0x88u, rec);
+                hipLaunchKernelGGL(k_rec<false>, dim3(grid), dim3(NT), 0, 0, in, io, npk, 0x88u, rec);
             else
                 hipLaunchKernelGGL(k_steal, dim3(G), dim3(NT), 0, 0, in, io, (uint64_t) grid, 0x88u,
                                    ctr, ctr + 4);
