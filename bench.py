@@ -12,7 +12,9 @@ op_fns.c loop) on a bounded sample of the same workload on this host's cores,
 `host_crossover` where the GPU path starts to beat one core on host-resident
 operands (the floor of MPIX_Redop_is_supported_buffers).
 
-N > 1 (torchrun, one rank per GPU; BASELINE configs[3] and north_star's
+N > 1 (one rank per GPU, started either by torchrun or -- `bench.py --gpus N`
+with no WORLD_SIZE in the environment -- by this script itself as N child
+processes, see launch_ranks; BASELINE configs[3] and north_star's
 "1/2/4/8-GPU reduce-scatter throughput ... absolute GB/s and fraction of
 roofline"): one step = one MPI_Reduce_scatter_block (fp32 SUM, a 4 GiB vector
 per rank, recvcount = 2^30 / N) by the reference's recursive-halving schedule
@@ -50,9 +52,14 @@ XGMI_LINK_GBS = 153.0       # one xGMI link, one direction (task brief: 7 x ~153
 GIB = float(1 << 30)
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
-    p.add_argument('--gpus', type=int, default=1)
+    p.add_argument('--gpus', type=int, default=None,
+                   help='ranks, one per GPU (default: WORLD_SIZE under a launcher, else 1); '
+                        'N > 1 without a launcher starts the N rank processes itself')
+    p.add_argument('--dry-run', action='store_true',
+                   help='bootstrap the ranks (gloo) and print the line skeleton without '
+                        'touching a GPU: checks the launch path on any host')
     p.add_argument('--steps', type=int, default=50)
     p.add_argument('--warmup', type=int, default=5)
     p.add_argument('--count', type=int, default=1 << 28, help='fp32 elements per operand')
@@ -69,7 +76,7 @@ def parse():
                    help='watchdog (s) over the N>1 value leg (bootstrap, parity check, timed steps)')
     p.add_argument('--pmc', default=os.path.join(ROOT, 'profiles', 'r03_pmc_summary.json'),
                    help='PMC traffic summary (from tools/pmc_summary.py) to quote as traffic')
-    return p.parse_args()
+    return p.parse_args(argv)
 
 
 def bench_lib():
@@ -1106,11 +1113,146 @@ def _watchdog(seconds, emit, note=True, code=3):
     return t
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get('WORLD_SIZE', '1'))
+def world_plan(args, env=None):
+    """Who runs the ranks, decided before anything touches a GPU.
+
+    Returns ('single', 1), ('launch', N) -- this process starts the N ranks
+    itself -- or ('rank', N) under an external launcher (torchrun sets
+    WORLD_SIZE); raises SystemExit with the reason when --gpus and the
+    environment disagree, so an N-GPU request never yields a 1-GPU line."""
+    env = os.environ if env is None else env
+    ws = env.get('WORLD_SIZE')
+    if ws is not None:
+        world = int(ws)
+        if args.gpus is not None and args.gpus != world:
+            raise SystemExit('bench.py: --gpus %d but WORLD_SIZE=%d (launcher and request '
+                             'disagree)' % (args.gpus, world))
+        return ('rank', world) if world > 1 else ('single', 1)
+    n = 1 if args.gpus is None else args.gpus
+    if n < 1:
+        raise SystemExit('bench.py: --gpus must be >= 1')
+    return ('launch', n) if n > 1 else ('single', 1)
+
+
+def check_devices(world, env=None):
+    """one GPU per rank, unless the 1-GPU rehearsal knob shares device 0 (or
+    the dry run touches none); torch.cuda.device_count() does not initialise
+    the HIP runtime on this image"""
+    env = os.environ if env is None else env
+    if env.get('MPIX_BENCH_SAME_DEVICE') == '1':
+        return
+    have = torch.cuda.device_count()
+    if have < world:
+        raise SystemExit('bench.py: %d ranks need %d GPUs, this node shows %d' % (world, world, have))
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """Start N fresh rank processes of this script (subprocess, never exec:
+    this process has not touched the GPU and stays off it), one per GPU, with
+    the RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* rendezvous torchrun would give
+    them -- the in-library bootstrap of the reference (rccl.c:33-43: unique id
+    on rank 0, broadcast, ncclCommInitRank) then runs inside the ranks through
+    torch.distributed.  Rank 0's stdout is relayed line by line; the run fails
+    (non-zero) if any rank does, the others are then stopped, and it also
+    fails unless rank 0 printed exactly one JSON line with n_gpus == N."""
+    import signal
+    import subprocess
+    port = os.environ.get('MASTER_PORT') or str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK='0', MASTER_ADDR='127.0.0.1',
+                   MASTER_PORT=port, MPIX_BENCH_LAUNCHED='1')
+        procs.append(subprocess.Popen([sys.executable, '-u', os.path.abspath(__file__)] + argv,
+                                      env=env, stdout=subprocess.PIPE if r == 0 else None))
+
+    def stop(*_):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+    old = {s: signal.signal(s, lambda sig, frm: (stop(), sys.exit(128 + sig)))
+           for s in (signal.SIGTERM, signal.SIGINT)}
+    lines = []
+    import threading
+
+    def relay():
+        for raw in procs[0].stdout:
+            line = raw.decode(errors='replace')
+            sys.stdout.write(line)
+            sys.stdout.flush()
+            if line.lstrip().startswith('{'):
+                lines.append(line)
+    t = threading.Thread(target=relay, daemon=True)
+    t.start()
+    rc, failed = 0, None
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and failed is None:
+                failed, rc = procs.index(p), c
+                stop()      # a peer stuck in a collective with the failed rank
+        if live:
+            time.sleep(0.2)
+    t.join(timeout=10)
+    for s, h in old.items():
+        signal.signal(s, h)
+    if failed is not None:
+        sys.stderr.write('bench.py: rank %d exited with status %d\n' % (failed, rc))
+        return rc if rc > 0 else 1
+    try:
+        got = json.loads(lines[-1]) if len(lines) == 1 else None
+    except ValueError:
+        got = None
+    if not got or got.get('n_gpus') != n:
+        sys.stderr.write('bench.py: rank 0 printed %d JSON line(s), none an n_gpus=%d line\n'
+                         % (len(lines), n))
+        return 1
+    return 0
+
+
+def dry_run(world, rank):
+    """the launch path without a GPU: ranks rendezvous over gloo, count
+    themselves with an all-reduce, and rank 0 prints the line's skeleton"""
+    seen = 1
+    if world > 1:
+        dist.init_process_group('gloo')
+        t = torch.ones(1)
+        dist.all_reduce(t)
+        seen = int(t.item())
+        dist.barrier()
+    if rank == 0:
+        print(json.dumps({'metric': METRIC_RSB if world > 1 else METRIC, 'value': None,
+                          'n_gpus': world, 'ranks_seen': seen, 'dry_run': True,
+                          'launcher': 'bench.py' if os.environ.get('MPIX_BENCH_LAUNCHED')
+                          else ('external' if world > 1 else None)}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0 if seen == world else 1
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    mode, world = world_plan(args)
+    if not args.dry_run:
+        check_devices(world)
+    if mode == 'launch':
+        return launch_ranks(world, argv)
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    if args.dry_run:
+        return dry_run(world, rank)
     # rehearsal knobs for a 1-GPU box (never set by the driver): every rank on
     # device 0 and a gloo control plane + transport; RCCL refuses two ranks on
     # one device (profiles/r01_rccl_probe.txt)

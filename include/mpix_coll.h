@@ -254,6 +254,14 @@ int MPIX_Allreduce_async(const void *sendbuf, void *recvbuf, MPIX_Aint count,
 /* stream the blocking forms use: the communicator's own (NULL) by default */
 int MPIX_Comm_set_stream(MPIX_Comm comm, void *stream);
 
+/* Largest single message the transport is handed: a schedule's message above
+ * `bytes` is posted as several consecutive messages to the same peer in the
+ * same exchange group (both sides split identically, so the k-th send of a
+ * pair matches its k-th receive in posting order, equal sizes).  Default 1 GiB
+ * on RCCL communicators (no count reaches 2^31; 0 or more than 1 GiB is refused
+ * there), 0 = never split on the others. */
+int MPIX_Comm_set_max_message(MPIX_Comm comm, MPIX_Aint bytes);
+
 /* Stream-ordered barrier: one 1-byte message to and from every peer on the
  * transport (on RCCL the stream passes it only once every peer's stream has
  * reached its own barrier). */
@@ -292,10 +300,12 @@ int MPIX_Comm_free_shared(MPIX_Comm comm, void *ptr);
  * communicators only. */
 /* Which schedule actually ran -- an explicitly requested algorithm may not be
  * able to run (a pull whose windows failed verification on some rank, a
- * device pair without peer access, MULTIPATH on a shape it does not cover), in
- * which case the schedule with the same bits runs instead; this is how a
- * caller tells.  pulls_enabled: 1 while the pull schedules can run on this
- * communicator; last_rs_algorithm / last_allreduce_algorithm: the MPIX_RSB_* /
+ * device pair without peer access, MULTIPATH on a shape it does not cover or
+ * with a step too small for its relay slots), in which case the schedule with
+ * the same bits runs instead; this is how a caller tells.  pulls_enabled: 1
+ * while the pull schedules can run on this communicator (0 once it is known to
+ * span nodes; before the first pull that is not yet known and counts as 1);
+ * last_rs_algorithm / last_allreduce_algorithm: the MPIX_RSB_* /
  * MPIX_ALLREDUCE_* value of the schedule the last reduce-scatter / allreduce
  * ran (AUTO resolved; -1 before the first); window_retries: pull-window
  * verification attempts that failed so far; fallbacks: calls whose requested

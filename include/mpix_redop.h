@@ -370,11 +370,14 @@ int MPIX_Redop_get_launch(int *block_threads, int *unroll, int *max_grid);
  * (every > 0), and the last tail_blocks blocks store their result
  * write-through (the line leaves the XCD's L2 at once) instead of
  * non-temporally (the line stays in L2, dirty, until evicted or written back
- * at the end of the kernel).  Same bits either way.  Default: xcd_mask 0x88
- * (two XCDs of eight write through: 8-9 % faster at 1 GiB) when every visible
- * device has 8 XCDs, else 0; every = tail_blocks = 0.  Env MPIX_REDOP_WT_XCD /
+ * at the end of the kernel).  Same bits either way.  Default (xcd_mask -1):
+ * 0x88 (two XCDs of eight write through: 8-9 % faster at 1 GiB) when every
+ * visible device has 8 XCDs, else 0, settled at the first kernel launch --
+ * get_store_policy reports -1 until then, the settled mask after; set -1 to
+ * return to it.  every = tail_blocks = 0.  Env MPIX_REDOP_WT_XCD /
  * MPIX_REDOP_WT_EVERY / MPIX_REDOP_WT_PHASE / MPIX_REDOP_WT_TAIL override
- * the defaults at first use. */
+ * the defaults at first use.  Neither call, nor any support predicate or
+ * other knob, makes a HIP call. */
 int MPIX_Redop_set_store_policy(int xcd_mask, int every, int phase, int tail_blocks);
 int MPIX_Redop_get_store_policy(int *xcd_mask, int *every, int *phase, int *tail_blocks);
 

@@ -67,6 +67,7 @@ def lib():
             'MPIX_Comm_create_custom': ([i32, i32, vp, vp, i32, ctypes.POINTER(vp)], i32),
             'MPIX_Comm_set_combine': ([vp, vp], i32),
             'MPIX_Comm_set_stream': ([vp, vp], i32),
+            'MPIX_Comm_set_max_message': ([vp, ctypes.c_ssize_t], i32),
             'MPIX_Comm_barrier': ([vp], i32),
             'MPIX_Comm_alloc_shared': ([vp, sz, ctypes.POINTER(vp)], i32),
             'MPIX_Comm_free_shared': ([vp, vp], i32),
@@ -145,6 +146,11 @@ class Comm:
     def set_stream(self, stream):
         redop.check(lib().MPIX_Comm_set_stream(self.h, None if stream is None else
                                                redop._stream_ptr(stream)), 'MPIX_Comm_set_stream')
+
+    def set_max_message(self, nbytes):
+        """MPIX_Comm_set_max_message: messages above nbytes go as several
+        same-peer messages in one exchange group (0: never split)"""
+        redop.check(lib().MPIX_Comm_set_max_message(self.h, nbytes), 'MPIX_Comm_set_max_message')
 
     def barrier(self):
         redop.check(lib().MPIX_Comm_barrier(self.h), 'MPIX_Comm_barrier')

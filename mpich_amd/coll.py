@@ -34,8 +34,9 @@ import torch.distributed as dist
 from . import ccl
 from . import redop
 
-# largest single message handed to gloo (the RCCL transport splits at the
-# same size in C++): bigger ones go as several same-peer messages in one group
+# largest single message handed to gloo, as on RCCL: libmpix_coll splits
+# bigger ones into several same-peer messages of one group
+# (MPIX_Comm_set_max_message) before the exchange function sees them
 MAX_MSG_BYTES = 1 << 30
 
 _comms = {}
@@ -51,9 +52,8 @@ def _gloo_exchange(group):
         p2p = []
         for peer, is_recv, addr, nbytes in ops:
             t = torch.frombuffer((ctypes.c_char * nbytes).from_address(addr), dtype=torch.uint8)
-            for k in range(0, nbytes, MAX_MSG_BYTES):
-                p2p.append(dist.P2POp(dist.irecv if is_recv else dist.isend,
-                                      t[k:k + MAX_MSG_BYTES], g2l(peer), group=group))
+            p2p.append(dist.P2POp(dist.irecv if is_recv else dist.isend, t, g2l(peer),
+                                  group=group))
         for w in dist.batch_isend_irecv(p2p):
             w.wait()
         return 0
@@ -72,6 +72,7 @@ def comm_for(group=None, device=True):
         else:
             c = ccl.comm_create_custom(rank, size, _gloo_exchange(group),
                                        ccl.XPORT_STAGED if device else ccl.XPORT_HOST)
+            c.set_max_message(MAX_MSG_BYTES)
         _comms[key] = c
     return c
 

@@ -117,6 +117,7 @@ struct MPIX_Comm_s {
     int last_rs = -1, last_ar = -1;
     int fallbacks = 0, win_retries = 0;
     int same_node = -1;                // every rank on this host (IPC possible): -1 not yet asked
+    size_t max_msg = 0;                // MPIX_Comm_set_max_message: split above this (0: never)
     struct Nonce { int rank, attempt; uint64_t n0, n1; };
     std::vector<Nonce> nonce_hist;     // every window nonce published (MPIX_COLL_TRACE)
     struct Shared {                    // MPIX_Comm_alloc_shared windows
@@ -173,23 +174,40 @@ int set_device(MPIX_Comm c)
 hipStream_t stream_of(void *s) { return static_cast<hipStream_t>(s); }
 
 // ------------------------------------------------------------ transports
+// RCCL communicators split at 1 GiB: no count reaches 2^31 in RCCL
 constexpr size_t kMaxMsg = size_t(1) << 30;
+
+// Messages above `max` bytes go as several consecutive messages to the same
+// peer within the one exchange group; both sides split the same lengths the
+// same way, so the k-th send of a pair matches its k-th receive in posting
+// order with equal sizes (what ncclSend/ncclRecv pairing requires).
+void split_messages(std::vector<MPIX_P2p_op> *ops, size_t max)
+{
+    if (!max)
+        return;
+    bool any = false;
+    for (const MPIX_P2p_op &o : *ops)
+        any |= o.bytes > max;
+    if (!any)
+        return;
+    std::vector<MPIX_P2p_op> out;
+    for (const MPIX_P2p_op &o : *ops) {
+        char *p = static_cast<char *>(o.buf);
+        for (size_t off = 0; off < o.bytes; off += max)
+            out.push_back(MPIX_P2p_op{o.peer, o.is_recv, p + off,
+                                      o.bytes - off < max ? o.bytes - off : max});
+    }
+    ops->swap(out);
+}
 
 int exchange_ccl(MPIX_Comm c, const MPIX_P2p_op *ops, int nops, hipStream_t s)
 {
     if (ncclGroupStart() != ncclSuccess)
         return MPIX_REDOP_ERR_OTHER;
     ncclResult_t r = ncclSuccess;
-    for (int i = 0; i < nops && r == ncclSuccess; ++i) {
-        // messages above kMaxMsg go as several to the same peer in this
-        // group (matched in posting order): no count reaches 2^31 in RCCL
-        char *p = static_cast<char *>(ops[i].buf);
-        for (size_t off = 0; off < ops[i].bytes && r == ncclSuccess; off += kMaxMsg) {
-            size_t n = ops[i].bytes - off < kMaxMsg ? ops[i].bytes - off : kMaxMsg;
-            r = ops[i].is_recv ? ncclRecv(p + off, n, ncclUint8, ops[i].peer, c->nccl, s)
-                               : ncclSend(p + off, n, ncclUint8, ops[i].peer, c->nccl, s);
-        }
-    }
+    for (int i = 0; i < nops && r == ncclSuccess; ++i)
+        r = ops[i].is_recv ? ncclRecv(ops[i].buf, ops[i].bytes, ncclUint8, ops[i].peer, c->nccl, s)
+                           : ncclSend(ops[i].buf, ops[i].bytes, ncclUint8, ops[i].peer, c->nccl, s);
     ncclResult_t r2 = ncclGroupEnd();
     return (r == ncclSuccess && r2 == ncclSuccess) ? MPIX_REDOP_SUCCESS : MPIX_REDOP_ERR_OTHER;
 }
@@ -353,6 +371,7 @@ int exchange(MPIX_Comm c, const std::vector<MPIX_P2p_op> &ops, hipStream_t s)
             nz.push_back(o);
     if (nz.empty())
         return MPIX_REDOP_SUCCESS;
+    split_messages(&nz, c->max_msg);
     if (coll_trace()) {     // one line per exchange step: what this rank posts
         std::string line = "[mpix_coll rank " + std::to_string(c->rank) + "/" +
                            std::to_string(c->size) + "]";
@@ -1563,6 +1582,7 @@ int allreduce_rsag(char *rb, size_t count, MPIX_Datatype dt, MPIX_Op op, MPIX_Co
         };
         auto real = [&](int nr) { return nr < rem ? nr * 2 + 1 : nr + rem; };
         int mask = 1, send_idx = 0, recv_idx = 0, last_idx = pof2;
+        bool mp_fell = false;
         while (mask < pof2) {                                               // :138-189
             int newdst = newrank ^ mask;
             size_t send_cnt, recv_cnt;
@@ -1576,8 +1596,15 @@ int allreduce_rsag(char *rb, size_t count, MPIX_Datatype dt, MPIX_Op op, MPIX_Co
                 recv_cnt = sum(recv_idx, last_idx);
             }
             const size_t parts = (size_t) pof2 / 2;
-            if (multipath && rem == 0 && pof2 >= 4 && count % pof2 == 0 &&
-                send_cnt >= parts * (parts - 1)) {
+            const bool mp_step = multipath && rem == 0 && pof2 >= 4 && count % pof2 == 0 &&
+                                 send_cnt >= parts * (parts - 1);
+            if (multipath && !mp_step && !mp_fell) {
+                // a step too small for the relay slots runs the plain
+                // exchange: the call is then reported as the plain schedule
+                mp_fell = true;
+                ran_instead(c, &c->last_ar, MPIX_ALLREDUCE_REDUCE_SCATTER_ALLGATHER);
+            }
+            if (mp_step) {
                 // send_cnt == recv_cnt here; relay slots fit in send_cnt elements
                 const size_t slot = (send_cnt + parts - 1) / parts * ext;
                 TRY(multipath_exchange(c, rb + disps[send_idx] * ext, tmp + disps[recv_idx] * ext,
@@ -2239,7 +2266,7 @@ int allreduce_entry(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_Da
                  ? allreduce_ring(rb, (size_t) count, dt, op, c, tmp, s, ext)
                  : allreduce_rsag(rb, (size_t) count, dt, op, c, tmp, s, ext,
                                   algorithm != MPIX_ALLREDUCE_RSAG_RD_ALLGATHER,
-                                  algorithm == MPIX_ALLREDUCE_RSAG_MULTIPATH);
+                                  c->last_ar == MPIX_ALLREDUCE_RSAG_MULTIPATH);
     return finish(c, release_scratch(c, tmp, rc, s), s, blocking);
 }
 
@@ -2291,6 +2318,7 @@ int MPIX_Comm_create_ccl(int rank, int size, const void *id, MPIX_Comm *comm)
     memcpy(&uid, id, sizeof uid);
     MPIX_Comm c = new_comm(rank, size, K_CCL);
     c->device = dev;
+    c->max_msg = kMaxMsg;
     if (ncclCommInitRank(&c->nccl, size, uid, rank) != ncclSuccess) {     // rccl.c:43
         delete c;
         return MPIX_REDOP_ERR_OTHER;
@@ -2375,6 +2403,14 @@ int MPIX_Comm_set_combine(MPIX_Comm comm, MPIX_Combine_fn fn)
     return MPIX_REDOP_SUCCESS;
 }
 
+int MPIX_Comm_set_max_message(MPIX_Comm comm, MPIX_Aint bytes)
+{
+    if (!comm || bytes < 0 || (comm->kind == K_CCL && (bytes == 0 || (size_t) bytes > kMaxMsg)))
+        return MPIX_REDOP_ERR_ARG;
+    comm->max_msg = (size_t) bytes;
+    return MPIX_REDOP_SUCCESS;
+}
+
 int MPIX_Comm_set_stream(MPIX_Comm comm, void *stream)
 {
     if (!comm)
@@ -2440,9 +2476,11 @@ int MPIX_Comm_get_state(MPIX_Comm comm, int *pulls_enabled, int *last_rs_algorit
 {
     if (!comm)
         return MPIX_REDOP_ERR_ARG;
+    // same_node -1 (not asked yet: settled by the first pull's record
+    // exchange) counts as enabled; a communicator found to span nodes is not
     if (pulls_enabled)
         *pulls_enabled = !comm->host() && !comm->combine && comm->size <= 16 &&
-                         !comm->win_broken && comm->pulls_possible();
+                         !comm->win_broken && comm->same_node != 0 && comm->pulls_possible();
     if (last_rs_algorithm)
         *last_rs_algorithm = comm->last_rs;
     if (last_allreduce_algorithm)

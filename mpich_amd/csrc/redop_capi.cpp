@@ -250,7 +250,12 @@ std::atomic<int> g_block{256}, g_max_grid{0};
 // r03_wt_sync_sweeps.txt).  Default: XCDs 3 and 7 on devices of 8 XCDs (SPX),
 // off otherwise.  g_wt_every / g_wt_phase / g_wt_tail select blocks by index
 // instead (the probes' forms).
-std::atomic<int> g_wt_tail{0}, g_wt_every{0}, g_wt_phase{0}, g_wt_xcd{0};
+// g_wt_xcd = kWtAuto until the first launch settles the default (resolve_wt,
+// the only HIP query of the knobs: reading or setting them, and the support
+// predicates, never start the HIP runtime).
+constexpr int kWtAuto = -1;
+std::atomic<int> g_wt_tail{0}, g_wt_every{0}, g_wt_phase{0}, g_wt_xcd{kWtAuto};
+std::once_flag g_wt_once;
 // completion wait of the synchronous calls: 0 block (hipStreamSynchronize),
 // 1 spin on an event, 2 spin on a pinned host word that a one-workgroup
 // contiguous kernel stores itself and the stream writes after any other
@@ -323,17 +328,6 @@ void read_env()
         int b = atoi(s);
         if (b >= 64 && b <= 1024 && b % 64 == 0)
             g_block = b;
-    }
-    {
-        int ndev = 0;
-        bool spx = hipGetDeviceCount(&ndev) == hipSuccess && ndev > 0;
-        for (int d = 0; spx && d < ndev; ++d) {
-            int x = 0;
-            spx = hipDeviceGetAttribute(&x, hipDeviceAttributeNumberOfXccs, d) == hipSuccess &&
-                  x == 8;
-        }
-        (void) hipGetLastError();
-        g_wt_xcd = spx ? 0x88 : 0;
     }
     if (const char *s = getenv("MPIX_REDOP_WT_TAIL"))
         g_wt_tail = atoi(s) > 0 ? atoi(s) : 0;
@@ -520,11 +514,43 @@ DevState *dev_state(int dev)
     return &d;
 }
 
-LaunchCfg launch_cfg()
+// The environment knobs, read once; no HIP call (CPU-only entry points --
+// the support predicates, the knob getters and setters -- come through here).
+void env()
 {
     std::call_once(g_env_once, read_env);
+}
+
+// The default store policy, settled at the first launch that needs it: XCDs
+// 3 and 7 write through when every visible device has 8 XCDs (SPX), else
+// none.  While g_wt_xcd is kWtAuto (no MPIX_REDOP_WT_XCD, no explicit mask
+// from MPIX_Redop_set_store_policy, or -1 set there) the launches use it.
+std::atomic<int> g_wt_default{kWtAuto};
+int wt_default()
+{
+    std::call_once(g_wt_once, [] {
+        int ndev = 0;
+        bool spx = hipGetDeviceCount(&ndev) == hipSuccess && ndev > 0;
+        for (int d = 0; spx && d < ndev; ++d) {
+            int x = 0;
+            spx = hipDeviceGetAttribute(&x, hipDeviceAttributeNumberOfXccs, d) == hipSuccess &&
+                  x == 8;
+        }
+        (void) hipGetLastError();
+        g_wt_default = spx ? 0x88 : 0;
+    });
+    return g_wt_default.load();
+}
+
+// Launch geometry and store policy of a kernel about to be enqueued.
+LaunchCfg launch_cfg()
+{
+    env();
+    int wt = g_wt_xcd.load();
+    if (wt == kWtAuto)
+        wt = wt_default();
     return LaunchCfg{g_block.load(), g_max_grid.load(), g_wt_tail.load(), g_wt_every.load(),
-                     g_wt_phase.load(), g_wt_xcd.load()};
+                     g_wt_phase.load(), wt};
 }
 
 Params params() { return Params{g_ftrue.load(), g_ffalse.load()}; }
@@ -2080,7 +2106,7 @@ int MPIX_Redop_has_gpu_path(MPIX_Op op, MPIX_Datatype datatype)
 // reduce_local.c:68 passes it, only asks about the pair), then the pair
 int MPIX_Redop_is_supported(MPIX_Op op, MPIX_Aint count, MPIX_Datatype datatype)
 {
-    launch_cfg();
+    env();
     if (!g_enable.load())
         return 0;
     uint32_t it = to_internal((uint32_t) datatype);
@@ -2118,7 +2144,7 @@ int MPIX_Redop_is_supported_buffers(MPIX_Op op, MPIX_Aint count, MPIX_Datatype d
 int MPIX_Redop_set_support(int enable, MPIX_Aint threshold_bytes, MPIX_Aint host_floor_bytes,
                            MPIX_Aint pinned_floor_bytes)
 {
-    launch_cfg();
+    env();
     g_enable = enable != 0;
     g_threshold = (long long) threshold_bytes;
     g_host_floor = (long long) host_floor_bytes;
@@ -2129,7 +2155,7 @@ int MPIX_Redop_set_support(int enable, MPIX_Aint threshold_bytes, MPIX_Aint host
 int MPIX_Redop_get_support(int *enable, MPIX_Aint *threshold_bytes, MPIX_Aint *host_floor_bytes,
                            MPIX_Aint *pinned_floor_bytes)
 {
-    launch_cfg();
+    env();
     if (enable)
         *enable = g_enable.load() ? 1 : 0;
     if (threshold_bytes)
@@ -2175,7 +2201,7 @@ int MPIX_Redop_set_fortran_booleans(int true_value, int false_value)
 
 int MPIX_Redop_set_launch(int block_threads, int max_grid)
 {
-    launch_cfg();
+    env();
     if (block_threads < 64 || block_threads > 1024 || block_threads % 64 || max_grid < 0)
         return MPIX_REDOP_ERR_ARG;
     g_block = block_threads;
@@ -2185,8 +2211,8 @@ int MPIX_Redop_set_launch(int block_threads, int max_grid)
 
 int MPIX_Redop_set_store_policy(int xcd_mask, int every, int phase, int tail_blocks)
 {
-    launch_cfg();
-    if (xcd_mask < 0 || xcd_mask > 0xff || every < 0 || phase < 0 ||
+    env();
+    if (xcd_mask < kWtAuto || xcd_mask > 0xff || every < 0 || phase < 0 ||
         phase >= (every > 0 ? every : 1) || tail_blocks < 0)
         return MPIX_REDOP_ERR_ARG;
     g_wt_xcd = xcd_mask;
@@ -2198,9 +2224,11 @@ int MPIX_Redop_set_store_policy(int xcd_mask, int every, int phase, int tail_blo
 
 int MPIX_Redop_get_store_policy(int *xcd_mask, int *every, int *phase, int *tail_blocks)
 {
-    launch_cfg();
-    if (xcd_mask)
-        *xcd_mask = g_wt_xcd.load();
+    env();
+    if (xcd_mask) {     // -1: the default, not settled yet (no launch so far)
+        const int x = g_wt_xcd.load();
+        *xcd_mask = x == kWtAuto ? g_wt_default.load() : x;
+    }
     if (every)
         *every = g_wt_every.load();
     if (phase)
@@ -2212,7 +2240,7 @@ int MPIX_Redop_get_store_policy(int *xcd_mask, int *every, int *phase, int *tail
 
 int MPIX_Redop_set_pageable(int threads, MPIX_Aint chunk_bytes)
 {
-    launch_cfg();
+    env();
     if (threads < 0 || threads > 16 || chunk_bytes < 65536 || chunk_bytes > ((MPIX_Aint) 256 << 20))
         return MPIX_REDOP_ERR_ARG;
     g_pipe_threads = threads;
@@ -2222,7 +2250,7 @@ int MPIX_Redop_set_pageable(int threads, MPIX_Aint chunk_bytes)
 
 int MPIX_Redop_get_pageable(int *threads, MPIX_Aint *chunk_bytes)
 {
-    launch_cfg();
+    env();
     if (threads)
         *threads = g_pipe_threads.load();
     if (chunk_bytes)
@@ -2232,13 +2260,13 @@ int MPIX_Redop_get_pageable(int *threads, MPIX_Aint *chunk_bytes)
 
 int MPIX_Redop_get_launch(int *block_threads, int *unroll, int *max_grid)
 {
-    LaunchCfg c = launch_cfg();
+    env();
     if (block_threads)
-        *block_threads = c.block;
+        *block_threads = g_block.load();
     if (unroll)
         *unroll = mpix::unroll();
     if (max_grid)
-        *max_grid = c.max_grid;
+        *max_grid = g_max_grid.load();
     return MPIX_REDOP_SUCCESS;
 }
 
@@ -2282,7 +2310,6 @@ static void opfn_failed(const char *name, int rc, MPIX_Datatype type)
 #define MPIX_OPFN(name, handle)                                                           \
     void name(void *invec, void *inoutvec, MPIX_Aint *len, MPIX_Datatype *type)           \
     {                                                                                     \
-        launch_cfg();                                                                     \
         int rc_ = MPIX_Reduce_local(invec, inoutvec, *len, *type, handle);               \
         if (rc_ != MPIX_REDOP_SUCCESS)                                                    \
             opfn_failed(#name, rc_, *type);                                               \

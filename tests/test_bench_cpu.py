@@ -151,3 +151,105 @@ def test_leg_without_symmetric_memory_is_reported_not_fatal():
     leg = bench._no_shared(redop.RedopError(15, 'MPIX_Comm_alloc_shared'))
     assert leg['schedule_ran'] is None and 'ms' not in leg
     assert leg['error'].startswith('no symmetric memory') and 'MPIX_Comm_alloc_shared' in leg['error']
+
+
+# ------------------------------------------------------- the rank launcher
+# `python3 bench.py --gpus N` must yield the
+# N-rank line by itself (no torchrun), and never a 1-GPU line for N > 1.
+
+def _bench(args, env_extra=None, drop=('WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_PORT')):
+    env = {k: v for k, v in os.environ.items() if k not in drop}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, 'bench.py')] + args, cwd=ROOT,
+                          capture_output=True, text=True, timeout=120, env=env)
+
+
+@pytest.mark.parametrize('n', [2, 3])
+def test_gpus_n_launches_n_ranks_itself(n):
+    import json
+    p = _bench(['--gpus', str(n), '--dry-run', '--no-extras', '--no-cpu-baseline'])
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith('{')]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    assert d['n_gpus'] == n and d['ranks_seen'] == n and d['launcher'] == 'bench.py', d
+
+
+def test_gpus_1_dry_run_is_single():
+    import json
+    p = _bench(['--dry-run'])
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = json.loads(p.stdout.strip().splitlines()[-1])
+    assert d['n_gpus'] == 1 and d['launcher'] is None
+
+
+def test_world_size_and_gpus_disagree_exits_nonzero():
+    p = _bench(['--gpus', '4', '--dry-run'], env_extra={'WORLD_SIZE': '2', 'RANK': '0'}, drop=())
+    assert p.returncode != 0
+    assert 'disagree' in p.stderr and '{' not in p.stdout
+
+
+def test_too_few_gpus_exits_nonzero_before_any_rank():
+    """this container shows no GPU: --gpus 2 without the rehearsal knob must
+    refuse, not fall back to one rank"""
+    p = _bench(['--gpus', '2', '--no-extras', '--no-cpu-baseline'],
+               env_extra={'HIP_VISIBLE_DEVICES': '', 'CUDA_VISIBLE_DEVICES': ''})
+    assert p.returncode != 0
+    assert 'need 2 GPUs' in p.stderr and '{' not in p.stdout
+
+
+def test_failing_rank_fails_the_launch():
+    """a rank that dies (here every rank does: an unknown process-group
+    backend, or no GPU to select in this container) ends the whole launch
+    non-zero, with the failed rank named, and the survivors are stopped"""
+    p = _bench(['--gpus', '2', '--steps', '1'],
+               env_extra={'MPIX_BENCH_SAME_DEVICE': '1', 'MPIX_BENCH_BACKEND': 'nosuchbackend'})
+    assert p.returncode != 0
+    assert 'exited with status' in p.stderr
+
+
+def test_world_plan_rules():
+    import bench
+    a = bench.parse(['--gpus', '8'])
+    assert bench.world_plan(a, {}) == ('launch', 8)
+    assert bench.world_plan(a, {'WORLD_SIZE': '8'}) == ('rank', 8)
+    assert bench.world_plan(bench.parse([]), {}) == ('single', 1)
+    assert bench.world_plan(bench.parse([]), {'WORLD_SIZE': '4'}) == ('rank', 4)
+    assert bench.world_plan(bench.parse(['--gpus', '1']), {'WORLD_SIZE': '1'}) == ('single', 1)
+    with pytest.raises(SystemExit):
+        bench.world_plan(a, {'WORLD_SIZE': '2'})
+    with pytest.raises(SystemExit):
+        bench.world_plan(bench.parse(['--gpus', '0']), {})
+
+
+def test_multipath_allreduce_small_step_reported_as_plain(oracle):
+    """rsag_multipath needs send_cnt >= parts * (parts - 1) at
+    every reduce-scatter step; a step below that runs the plain exchange, and
+    the call must then be reported as reduce_scatter_allgather (P = 4: count 4
+    halves to a 1-element second step; count 8 keeps 2 per step)"""
+    import bench
+    from mpich_amd import ccl
+    P = 4
+    comms = ccl.comm_create_local(P)
+    for c in comms:
+        c.set_combine(oracle.combine_fn_address())
+    MPI_FLOAT, MPI_SUM = 0x4c00040a, 0x58000003
+    try:
+        for count, fell in ((4, True), (8, False), (4096, False)):
+            sends = [np.arange(count, dtype=np.float32) + r for r in range(P)]
+            outs = [np.zeros(count, np.float32) for _ in range(P)]
+            before = comms[0].state()['fallbacks']
+            rcs = _threads(comms, lambda r, c: ccl.allreduce(sends[r], outs[r], count, MPI_FLOAT,
+                                                              MPI_SUM, c, 'rsag_multipath'))
+            assert rcs == [0] * P
+            want = sum(sends)
+            for r in range(P):
+                assert np.array_equal(outs[r], want), (count, r)
+                got = bench.schedule_ran(comms[r], 'rsag_multipath', 'ar')
+                assert ('error' in got) == fell, (count, got)
+                assert got['schedule_ran'] == ('reduce_scatter_allgather' if fell
+                                               else 'rsag_multipath'), (count, got)
+            assert comms[0].state()['fallbacks'] - before == (1 if fell else 0)
+    finally:
+        for c in comms:
+            c.free()

@@ -1,0 +1,30 @@
+"""bench.py's N > 1 path end to end on one GPU: `bench.py --gpus 2` starts
+its two ranks itself (no torchrun), both on device 0 over the gloo staged
+transport (the rehearsal knobs; RCCL refuses two ranks on one device), runs
+the recursive-halving reduce-scatter value leg with its bit-exact parity gate,
+and rank 0's one line carries n_gpus = 2 and the schedule that ran."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.gpu
+def test_bench_gpus_2_self_launched_line():
+    env = {k: v for k, v in os.environ.items()
+           if k not in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_PORT')}
+    env.update(MPIX_BENCH_SAME_DEVICE='1', MPIX_BENCH_BACKEND='gloo')
+    p = subprocess.run([sys.executable, os.path.join(ROOT, 'bench.py'), '--gpus', '2',
+                        '--steps', '2', '--warmup', '1', '--count', str(1 << 22),
+                        '--rsb-bytes', str(16 << 20), '--no-extras', '--no-cpu-baseline'],
+                       cwd=ROOT, capture_output=True, text=True, timeout=100, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith('{')]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    assert d['n_gpus'] == 2 and d['schedule_ran'] == 'recursive_halving', d
+    assert d['parity']['bit_exact_all_ranks'] and d['value'] > 0, d

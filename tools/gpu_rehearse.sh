@@ -24,8 +24,8 @@ for sec in ('reduce_scatter_block_other', 'allreduce'):
 }
 for mode in normal fault; do
     if [ $mode = fault ]; then export MPIX_COLL_WINDOW_FAULT=1; fi
-    MPIX_BENCH_SAME_DEVICE=1 MPIX_BENCH_BACKEND=gloo timeout -k 10 500 python3 -m torch.distributed.run \
-        --nnodes=1 --nproc-per-node $P --master-addr 127.0.0.1 --master-port 29541 bench.py --gpus $P \
+    # bench.py starts the P ranks itself (no torchrun): the driver's own form
+    MPIX_BENCH_SAME_DEVICE=1 MPIX_BENCH_BACKEND=gloo timeout -k 10 500 python3 bench.py --gpus $P \
         --steps 3 --warmup 1 --count 67108864 --rsb-bytes 268435456 > $O/n${P}_$mode.json 2> $O/n${P}_$mode.err
     rc=$?
     echo "$mode rc=$rc"
