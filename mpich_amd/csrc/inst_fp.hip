@@ -28,6 +28,16 @@ const Entry *cplx_half_ops(int opi)
     return (opi == 3 || opi == 4) ? &tab[opi - 3] : nullptr;
 }
 
+// MPI_LONG_DOUBLE (x87 in 16 bytes) and MPI_REAL16 (binary128): MAX / MIN
+// only -- compare and select (redop_ops.h); SUM / PROD stay with the caller's
+// CPU op table (MPIX_Redop_is_supported answers 0 for them)
+template <class Max, class Min>
+const Entry *select_ops(int opi)
+{
+    static const Entry tab[2] = { entry<Max>(), entry<Min>() };
+    return (opi == 1 || opi == 2) ? &tab[opi - 1] : nullptr;
+}
+
 const Entry *bf16_ops(int opi)
 {
     static const Entry e = entry<Bf16Sum>();
@@ -46,6 +56,8 @@ const Entry *lookup_fp(int raw, int opi)
         case 0x4c840800u: return cplx_ops<float>(opi);
         case 0x4c841000u: return cplx_ops<double>(opi);
         case 0x4c850200u: return bf16_ops(opi);
+        case 0x4c851000u: return select_ops<X87Max, X87Min>(opi);
+        case 0x4c831000u: return select_ops<QuadMax, QuadMin>(opi);
         default: return nullptr;
     }
 }

@@ -427,7 +427,35 @@ k_contig_tree(MultiIn<typename C::unit> ins, int k, uint32_t pres, typename C::u
     }
 }
 
+// The same fold as a compile-time recursion over slot ranges [LO, LO + LEN):
+// left half = inout, right half = in, an absent half passes the other through
+// -- tree_fold's association exactly, with at most log2(KMAX) + 1 partial
+// results live instead of KMAX slots (the 32-byte units would not fit the
+// registers otherwise).  Returns whether any slot of the range is present.
+template <int LO, int LEN, class T, class L, class F>
+__device__ __forceinline__ bool tree_fold_rec(T &out, int k, uint32_t pres, L &load, F &f)
+{
+    if constexpr (LEN == 1) {
+        if (LO < k && ((pres >> LO) & 1u)) {
+            out = load(LO);
+            return true;
+        }
+        return false;
+    } else {
+        T a, b;
+        const bool ha = tree_fold_rec<LO, LEN / 2>(a, k, pres, load, f);
+        if (LO + LEN / 2 >= k) {
+            out = a;
+            return ha;
+        }
+        const bool hb = tree_fold_rec<LO + LEN / 2, LEN / 2>(b, k, pres, load, f);
+        out = (ha && hb) ? f(a, b) : (hb ? b : a);
+        return ha || hb;
+    }
+}
+
 // the same fold element by element, for operands not sharing a 16-byte phase
+// (and every 32-byte unit)
 template <class C>
 __global__ void __launch_bounds__(256)
 k_elem_tree(MultiIn<typename C::unit> ins, int k, uint32_t pres, typename C::unit *__restrict__ out,
@@ -437,13 +465,20 @@ k_elem_tree(MultiIn<typename C::unit> ins, int k, uint32_t pres, typename C::uni
     auto ce = [&](T a, T b) { return C::apply(a, b, prm); };
     const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
     for (uint64_t t = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x; t < n; t += stride) {
-        T v[kMaxMulti];
+        if constexpr (sizeof(T) > 16) {
+            auto load = [&](int q) { return ins.p[q][t]; };
+            T r;
+            tree_fold_rec<0, kMaxMulti>(r, k, pres, load, ce);
+            out[t] = r;
+        } else {
+            T v[kMaxMulti];
 #pragma unroll
-        for (int q = 0; q < kMaxMulti; ++q)
-            if (q < k && ((pres >> q) & 1u))
-                v[q] = ins.p[q][t];
-        tree_fold<kMaxMulti>(v, k, pres, ce);
-        out[t] = v[0];
+            for (int q = 0; q < kMaxMulti; ++q)
+                if (q < k && ((pres >> q) & 1u))
+                    v[q] = ins.p[q][t];
+            tree_fold<kMaxMulti>(v, k, pres, ce);
+            out[t] = v[0];
+        }
     }
 }
 
@@ -622,12 +657,17 @@ hipError_t launch_contig(const void *in, void *io, uint64_t count, const Params 
                          const LaunchCfg &cfg, hipStream_t s)
 {
     using T = typename C::unit;
-    constexpr uint64_t E = 16 / sizeof(T);
+    constexpr uint64_t E = sizeof(T) <= 16 ? 16 / sizeof(T) : 1;
     const T *tin = static_cast<const T *>(in);
     T *tio = static_cast<T *>(io);
     bool signalled = false;
     uintptr_t ai = reinterpret_cast<uintptr_t>(in), ao = reinterpret_cast<uintptr_t>(io);
-    if ((ao % sizeof(T)) == 0 && (ai % sizeof(T)) == 0) {
+    if constexpr (sizeof(T) > 16) {
+        // 32-byte units (the long double / binary128 pairs): one element per
+        // lane, two 16-byte loads per operand, no packet form
+        unsigned grid = grid_for((uint64_t) cfg.block * 4, count, cfg.max_grid);
+        hipLaunchKernelGGL((k_elem<C>), dim3(grid), dim3(cfg.block), 0, s, tin, tio, count, prm);
+    } else if ((ao % sizeof(T)) == 0 && (ai % sizeof(T)) == 0) {
         uint64_t head = ((16 - (ao & 15)) & 15) / sizeof(T);
         if (head > count)
             head = count;
@@ -666,15 +706,17 @@ hipError_t launch_multi(const void *const *ins, int k, void *io, uint64_t count,
                         const LaunchCfg &cfg, hipStream_t s)
 {
     using T = typename C::unit;
-    constexpr uint64_t E = 16 / sizeof(T);
+    constexpr uint64_t E = sizeof(T) <= 16 ? 16 / sizeof(T) : 1;
     MultiIn<T> mi{};
     uintptr_t ao = reinterpret_cast<uintptr_t>(io);
-    bool aligned = (ao % sizeof(T)) == 0;
+    bool aligned = sizeof(T) <= 16 && (ao % sizeof(T)) == 0;
     for (int q = 0; q < k; ++q) {
         mi.p[q] = static_cast<const T *>(ins[q]);
         aligned = aligned && ((reinterpret_cast<uintptr_t>(ins[q]) & 15) == (ao & 15));
     }
     T *tio = static_cast<T *>(io);
+    if constexpr (sizeof(T) > 16)
+        aligned = false;
     if (aligned) {
         uint64_t head = ((16 - (ao & 15)) & 15) / sizeof(T);
         if (head > count)
@@ -686,8 +728,9 @@ hipError_t launch_multi(const void *const *ins, int k, void *io, uint64_t count,
         unsigned grid = grid_for((uint64_t) cfg.block * U, npk, cfg.max_grid);
         Params p = prm;
         set_store_policy(p, cfg, grid);
-        hipLaunchKernelGGL((k_contig_multi<C, U>), dim3(grid), dim3(cfg.block), 0, s, mi, k, tio,
-                           head, npk, tail_start, ntail, p);
+        if constexpr (sizeof(T) <= 16)
+            hipLaunchKernelGGL((k_contig_multi<C, U>), dim3(grid), dim3(cfg.block), 0, s, mi, k,
+                               tio, head, npk, tail_start, ntail, p);
     } else {
         unsigned grid = grid_for((uint64_t) cfg.block * 4, count, cfg.max_grid);
         hipLaunchKernelGGL((k_elem_multi<C>), dim3(grid), dim3(cfg.block), 0, s, mi, k, tio, count,
@@ -703,10 +746,10 @@ hipError_t launch_tree(const void *const *ins, int k, void *out, uint64_t count,
                        const LaunchCfg &cfg, hipStream_t s)
 {
     using T = typename C::unit;
-    constexpr uint64_t E = 16 / sizeof(T);
+    constexpr uint64_t E = sizeof(T) <= 16 ? 16 / sizeof(T) : 1;
     MultiIn<T> mi{};
     uintptr_t ao = reinterpret_cast<uintptr_t>(out);
-    bool aligned = (ao % sizeof(T)) == 0;
+    bool aligned = sizeof(T) <= 16 && (ao % sizeof(T)) == 0;
     uint32_t pres = 0;
     for (int q = 0; q < k; ++q) {
         mi.p[q] = static_cast<const T *>(ins[q]);
@@ -729,13 +772,15 @@ hipError_t launch_tree(const void *const *ins, int k, void *out, uint64_t count,
         // gains nothing at k = 4 / 8 / 16 (profiles/r03_tree_probe_policy.json)
         if (k == 2)
             set_store_policy(p, cfg, grid);
-        if (k == 2)     // out = a OP b: the contiguous kernel's 4 packets per lane
-            hipLaunchKernelGGL((k_contig_tree<C, 2, 4>), dim3(grid), dim3(256), 0, s, mi, k, pres,
-                               tout, head, npk, tail_start, ntail, p);
-        else            // one 16-slot form for every k (an 8-slot form, more waves in
-                        // flight, measured 4-9 % slower at k = 4 and 8)
-            hipLaunchKernelGGL((k_contig_tree<C, kMaxMulti, 1>), dim3(grid), dim3(256), 0, s, mi,
-                               k, pres, tout, head, npk, tail_start, ntail, p);
+        if constexpr (sizeof(T) <= 16) {
+            if (k == 2)     // out = a OP b: the contiguous kernel's 4 packets per lane
+                hipLaunchKernelGGL((k_contig_tree<C, 2, 4>), dim3(grid), dim3(256), 0, s, mi, k,
+                                   pres, tout, head, npk, tail_start, ntail, p);
+            else            // one 16-slot form for every k (an 8-slot form, more waves in
+                            // flight, measured 4-9 % slower at k = 4 and 8)
+                hipLaunchKernelGGL((k_contig_tree<C, kMaxMulti, 1>), dim3(grid), dim3(256), 0, s,
+                                   mi, k, pres, tout, head, npk, tail_start, ntail, p);
+        }
     } else {
         hipLaunchKernelGGL((k_elem_tree<C>), dim3(grid_for(256 * 4, count, 0)), dim3(256), 0, s,
                            mi, k, pres, tout, count, prm);
@@ -754,10 +799,14 @@ hipError_t launch_vector(const void *in, void *io, uint64_t count, uint64_t bl, 
     if (bl == st)       // contiguous after all
         return launch_contig<C>(in, io, n, prm, cfg, s);
     unsigned grid = grid_for((uint64_t) cfg.block * 4, n, cfg.max_grid);
-    if (bl == 1 && st == 2 && (reinterpret_cast<uintptr_t>(io) % (2 * sizeof(T))) == 0)
-        hipLaunchKernelGGL((k_vector_s2<C>), dim3(grid_for(256, n, cfg.max_grid)), dim3(256), 0, s,
-                           static_cast<const T *>(in), static_cast<T *>(io), n, prm);
-    else if (bl == 1)
+    bool s2 = false;
+    if constexpr (sizeof(T) <= 16)
+        s2 = bl == 1 && st == 2 && (reinterpret_cast<uintptr_t>(io) % (2 * sizeof(T))) == 0;
+    if (s2) {
+        if constexpr (sizeof(T) <= 16)
+            hipLaunchKernelGGL((k_vector_s2<C>), dim3(grid_for(256, n, cfg.max_grid)), dim3(256), 0,
+                               s, static_cast<const T *>(in), static_cast<T *>(io), n, prm);
+    } else if (bl == 1)
         hipLaunchKernelGGL((k_vector1<C>), dim3(grid), dim3(cfg.block), 0, s,
                            static_cast<const T *>(in), static_cast<T *>(io), n, st, prm);
     else

@@ -1,7 +1,8 @@
 // redop_ops.h -- CDNA4 (gfx950) element combiners for the predefined MPI_Ops.
 //
 // One combiner per (op, element type).  Each has
-//     using unit = <storage of one element, 1..16 bytes>;
+//     using unit = <storage of one element, 1..16 bytes, or 32 for the
+//                   long double / binary128 pairs (element-wise kernels)>;
 //     static __device__ unit apply(unit a, unit b, const Params &p);
 // computing the new inout element from a = inoutvec[i], b = invec[i], which is
 // MPICH's operand order (src/include/mpir_op_util.h:46-53).  The semantics
@@ -322,6 +323,144 @@ template <typename P, bool IsMax> struct Loc {
             r.l = b.l;
         } else if (tie) {
             r.l = (a.l < b.l) ? a.l : b.l;
+        }
+        return r;
+    }
+};
+
+// ------------------------------------------ x87 extended and IEEE binary128
+// MPI_LONG_DOUBLE on x86-64 Linux is the x87 80-bit extended format in a
+// 16-byte slot (MPIR_ALT_FLOAT128, mpir_datatype.h:82; MPIR_OP_TYPE_GROUP(
+// FLOATING_POINT) lists it, mpir_op_util.h:211-217): bytes 0-7 the 64-bit
+// significand with its explicit integer bit J (bit 63), bytes 8-9 sign and
+// 15-bit exponent, bytes 10-15 padding.  MPI_REAL16 is IEEE binary128
+// (MPIR_FLOAT128, __float128).  MAX/MIN/MAXLOC/MINLOC on them only compare and
+// select, so they are done here in integer arithmetic, bit-exact with what gcc
+// makes of op_fns.c on x86-64: fcomi's ordering, and for long double the
+// result stored with fstpt -- the 10 value bytes, inout's padding kept.
+// fcomi (and __gttf2/__lttf2 for binary128) report "unordered" for a NaN and,
+// for x87, for the formats the 387 and later do not support: unnormals
+// (exponent != 0 with J = 0), pseudo-infinities and pseudo-NaNs (exponent
+// 0x7fff with J = 0).  Pseudo-denormals (exponent 0 with J = 1) compare as
+// the normal of exponent 1 with the same significand, as do denormals by
+// value (both are m * 2^(1 - 16383 - 63)); zeros of either sign are equal.
+enum { kCmpLt = 0, kCmpEq = 1, kCmpGt = 2, kCmpUn = 3 };
+
+struct alignas(16) X87 {
+    uint64_t m;     // significand, J = bit 63
+    uint64_t se;    // bits 0-14 exponent, bit 15 sign, bits 16-63 padding
+};
+
+MPIX_DEV int sign_mag_cmp(bool sa, bool sb, int mag, bool both_zero)
+{
+    if (both_zero)
+        return kCmpEq;
+    if (sa != sb)
+        return sa ? kCmpLt : kCmpGt;
+    if (mag == 0)
+        return kCmpEq;
+    return (mag < 0) != sa ? kCmpLt : kCmpGt;
+}
+
+MPIX_DEV int x87_cmp(const X87 &a, const X87 &b)
+{
+    const uint32_t ea = (uint32_t) a.se & 0x7fffu, eb = (uint32_t) b.se & 0x7fffu;
+    const bool ja = (a.m >> 63) != 0, jb = (b.m >> 63) != 0;
+    const bool bad_a = (ea != 0 && !ja) || (ea == 0x7fffu && (a.m << 1) != 0);
+    const bool bad_b = (eb != 0 && !jb) || (eb == 0x7fffu && (b.m << 1) != 0);
+    if (bad_a || bad_b)
+        return kCmpUn;
+    // magnitude key (max(e, 1), m); zero is (1, 0), below every other value
+    const uint32_t ka = ea ? ea : 1u, kb = eb ? eb : 1u;
+    const int mag = ka != kb ? (ka < kb ? -1 : 1) : (a.m != b.m ? (a.m < b.m ? -1 : 1) : 0);
+    return sign_mag_cmp((a.se >> 15) & 1, (b.se >> 15) & 1, mag,
+                        ea == 0 && eb == 0 && a.m == 0 && b.m == 0);
+}
+
+// `a = v` as fstpt does it: the 10 value bytes of v, a's padding kept
+MPIX_DEV X87 x87_store(X87 a, const X87 &v)
+{
+    a.m = v.m;
+    a.se = (a.se & ~(uint64_t) 0xffff) | (v.se & 0xffff);
+    return a;
+}
+
+struct X87Max {
+    using unit = X87;
+    static MPIX_DEV X87 apply(X87 a, X87 b, const Params &)
+    {
+        return x87_cmp(a, b) == kCmpGt ? a : x87_store(a, b);
+    }
+};
+struct X87Min {
+    using unit = X87;
+    static MPIX_DEV X87 apply(X87 a, X87 b, const Params &)
+    {
+        return x87_cmp(a, b) == kCmpLt ? a : x87_store(a, b);
+    }
+};
+
+struct alignas(16) Quad {
+    uint64_t lo, hi;    // hi: sign, 15-bit exponent, top 48 fraction bits
+};
+
+MPIX_DEV int quad_cmp(const Quad &a, const Quad &b)
+{
+    const uint64_t ma = a.hi & 0x7fffffffffffffffull, mb = b.hi & 0x7fffffffffffffffull;
+    const uint64_t inf = 0x7fff000000000000ull;
+    if (ma > inf || (ma == inf && a.lo) || mb > inf || (mb == inf && b.lo))
+        return kCmpUn;
+    const int mag = ma != mb ? (ma < mb ? -1 : 1) : (a.lo != b.lo ? (a.lo < b.lo ? -1 : 1) : 0);
+    return sign_mag_cmp(a.hi >> 63, b.hi >> 63, mag, (ma | a.lo | mb | b.lo) == 0);
+}
+
+struct QuadMax {
+    using unit = Quad;
+    static MPIX_DEV Quad apply(Quad a, Quad b, const Params &) { return quad_cmp(a, b) == kCmpGt ? a : b; }
+};
+struct QuadMin {
+    using unit = Quad;
+    static MPIX_DEV Quad apply(Quad a, Quad b, const Params &) { return quad_cmp(a, b) == kCmpLt ? a : b; }
+};
+
+// MPI_LONG_DOUBLE_INT {long double; int} (pairtypes.c:15-21: extent 32, the
+// int at 16, bytes 20-31 padding) and the builtin pair of binary128
+// (MPIR_2FLOAT128, loc a binary128 too): the loop of op_fns.c:303-352 with
+// the comparisons above.  32-byte units: element-wise kernels only.
+struct alignas(16) LongDoubleInt {
+    X87 v;
+    int32_t l;
+    int32_t pad[3];
+};
+template <bool IsMax> struct LocX87 {
+    using unit = LongDoubleInt;
+    static MPIX_DEV unit apply(unit a, unit b, const Params &)
+    {
+        const int c = x87_cmp(a.v, b.v);
+        unit r = a;
+        if (c == (IsMax ? kCmpLt : kCmpGt)) {
+            r.v = x87_store(a.v, b.v);
+            r.l = b.l;
+        } else if (c == kCmpEq) {
+            r.l = (a.l < b.l) ? a.l : b.l;
+        }
+        return r;
+    }
+};
+struct alignas(16) QuadPair {
+    Quad v, l;
+};
+template <bool IsMax> struct LocQuad {
+    using unit = QuadPair;
+    static MPIX_DEV unit apply(unit a, unit b, const Params &)
+    {
+        const int c = quad_cmp(a.v, b.v);
+        unit r = a;
+        if (c == (IsMax ? kCmpLt : kCmpGt)) {
+            r.v = b.v;
+            r.l = b.l;
+        } else if (c == kCmpEq && quad_cmp(a.l, b.l) != kCmpLt) {
+            r.l = b.l;      // MPL_MIN(a.l, b.l) on the binary128 locs
         }
         return r;
     }

@@ -86,8 +86,10 @@ def test_tables_agree_with_oracle(R, oracle):
 
 def test_support_predicate(R):
     """MPIR_Typerep_reduce_is_supported mirror: everything legal except the
-    types with no gfx950 arithmetic (x87 long double, __float128) and the bf16
-    ops the reference itself asserts on."""
+    arithmetic (SUM/PROD) on the types gfx950 has no arithmetic for (x87 long
+    double, __float128 and their complex forms) and the bf16 ops the reference
+    itself asserts on.  Their compare-and-select ops (MAX/MIN, MAXLOC/MINLOC
+    on MPI_LONG_DOUBLE_INT) have kernels (round 4)."""
     from mpich_amd import handles as H
     unsupported_types = {H.MPI_LONG_DOUBLE, H.MPI_REAL16, H.MPI_COMPLEX32,
                          H.MPI_C_LONG_DOUBLE_COMPLEX, H.MPI_CXX_LONG_DOUBLE_COMPLEX,
@@ -110,7 +112,13 @@ def test_support_predicate(R):
     assert R.is_supported(H.MPI_SUM, H.MPI_FLOAT)
     assert R.is_supported(H.MPI_MAXLOC, H.MPI_SHORT_INT)
     assert not R.is_supported(H.MPI_SUM, H.MPI_LONG_DOUBLE)
+    assert not R.is_supported(H.MPI_PROD, H.MPI_REAL16)
     assert not R.is_supported(H.MPI_BAND, H.MPI_FLOAT)
+    for op in (H.MPI_MAX, H.MPI_MIN):
+        assert R.is_supported(op, H.MPI_LONG_DOUBLE) and R.is_supported(op, H.MPI_REAL16)
+    for op in (H.MPI_MAXLOC, H.MPI_MINLOC):
+        assert R.is_supported(op, H.MPI_LONG_DOUBLE_INT)
+        assert R.is_supported(op, H.MPIR_2FLOAT128)
 
 
 def test_errors_without_gpu(R):

@@ -81,10 +81,10 @@ def test_equal_header_rules_on_device(R, H):
 
 
 @pytest.mark.parametrize('dt_name', ['MPI_LONG_DOUBLE', 'MPI_C_LONG_DOUBLE_COMPLEX',
-                                     'MPI_LONG_DOUBLE_INT'])
+                                     'MPI_REAL16'])
 def test_declined_call_leaves_buffers_untouched(R, H, dt_name):
     dt = getattr(H, dt_name)
-    op = H.MPI_MAXLOC if dt_name.endswith('_INT') else H.MPI_SUM
+    op = H.MPI_SUM      # arithmetic on x87 / binary128: no kernel (MAX/MIN have one)
     assert not R.is_supported(op, dt)
     ext = R.datatype_extent(dt)
     n = 4099

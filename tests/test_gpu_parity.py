@@ -213,11 +213,9 @@ def test_random_parity(R, H, oracle, dtname, opname, kind, size):
 
 @pytest.mark.parametrize('case', gu.load_cases(), ids=lambda c: c['id'] + ' ' + c['name'])
 def test_golden_on_gpu(R, case):
-    sup = R.is_supported(case['op'], case['datatype'])
-    if not sup:
-        # only the x87 long double pairs have no GPU path; they must refuse
-        assert case['datatype'] == 0x8c000004
-        return
+    # every golden case has a GPU path, the MPI_LONG_DOUBLE_INT MAXLOC/MINLOC
+    # cases (opmaxloc.c / opminloc.c) included since round 4
+    assert R.is_supported(case['op'], case['datatype'])
 
     def fn(inb, inoutb, count, dt, op):
         di, dio = dev(inb), dev(inoutb)

@@ -14,11 +14,14 @@ def test_store_policy_arguments():
     from mpich_amd import redop
     old = redop.get_store_policy()
     try:
-        for bad in ((-1, 0, 0, 0), (0x100, 0, 0, 0), (0, -1, 0, 0), (0, 4, 4, 0), (0, 0, 1, 0),
+        for bad in ((-2, 0, 0, 0), (0x100, 0, 0, 0), (0, -1, 0, 0), (0, 4, 4, 0), (0, 0, 1, 0),
                     (0, 0, 0, -1)):
             assert redop.set_store_policy(*bad) != 0, bad
         assert redop.set_store_policy(0x81, 8, 5, 16) == 0
         assert redop.get_store_policy() == dict(xcd_mask=0x81, every=8, phase=5, tail_blocks=16)
+        # -1: back to the default (settled at the first launch; -1 until then)
+        assert redop.set_store_policy(-1, 0, 0, 0) == 0
+        assert redop.get_store_policy()['xcd_mask'] in (-1, 0, 0x88)
     finally:
         assert redop.set_store_policy(old['xcd_mask'], old['every'], old['phase'],
                                       old['tail_blocks']) == 0
