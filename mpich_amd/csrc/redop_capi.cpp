@@ -1244,6 +1244,21 @@ int waved(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext, u
     const int64_t n = (int64_t) chunks.size();
     const int W = nthreads < 1 ? 1 : nthreads;
     SpinBarrier bar(W);
+    // MPIX_REDOP_PIPE_TRACE=1: per step and worker the host times (ns from the
+    // call's start) at which the kernel launch (worker 0), the copy-in, the
+    // wait for the kernel of chunk st - 2, its copy-out and the step's barrier
+    // ended, and the CPU each worker started on -- one JSON line to stderr
+    // (tools/pageable_swing.py reads it)
+    static const bool trace_on = getenv("MPIX_REDOP_PIPE_TRACE") != nullptr;
+    std::vector<int64_t> trace((size_t) (trace_on ? (n + 2) * W * 5 : 0), -1);
+    std::vector<int> trace_cpu((size_t) (trace_on ? W : 0), -1);
+    const auto t0 = std::chrono::steady_clock::now();
+    auto mark = [&](int64_t st, int w, int what) {
+        if (trace_on)
+            trace[((size_t) st * (size_t) W + (size_t) w) * 5 + (size_t) what] =
+                std::chrono::duration_cast<std::chrono::nanoseconds>(
+                    std::chrono::steady_clock::now() - t0).count();
+    };
     std::atomic<int> err{MPIX_REDOP_SUCCESS};
     auto fail = [&](int rc) {
         int z = MPIX_REDOP_SUCCESS;
@@ -1260,6 +1275,8 @@ int waved(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext, u
         *len = std::min(bytes - *lo, per);
     };
     auto work = [&](int w) {
+        if (trace_on)
+            trace_cpu[(size_t) w] = sched_getcpu();
         if (hipSetDevice(dev) != hipSuccess) {
             fail(MPIX_REDOP_ERR_OTHER);
         }
@@ -1288,6 +1305,7 @@ int waved(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext, u
                     rc = hip_err(hipEventRecord(P.ring_ev[b], P.ring_s));
                 if (rc)
                     fail(rc);
+                mark(st, w, 0);
             }
             if (st < n && err.load() == MPIX_REDOP_SUCCESS) {       // copy chunk st in
                 uint64_t off, cnt;
@@ -1299,10 +1317,12 @@ int waved(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext, u
                     copy_to_pinned(h + lo, (const char *) in + off * ext + lo, len);
                 if (len && io_pg)
                     copy_to_pinned(h + half + lo, (const char *) io + off * ext + lo, len);
+                mark(st, w, 1);
             }
             if (st >= 2 && st - 2 < n && err.load() == MPIX_REDOP_SUCCESS) {   // chunk st-2 out
                 const int b = (int) ((st - 2) % 3);
                 int rc = hip_err(hipEventSynchronize(P.ring_ev[b]));
+                mark(st, w, 2);
                 if (rc)
                     fail(rc);
                 else if (io_pg) {
@@ -1314,8 +1334,10 @@ int waved(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext, u
                         memcpy((char *) io + off * ext + lo, P.ring + (size_t) b * 2 * half + half + lo,
                                len);
                 }
+                mark(st, w, 3);
             }
             bar.wait();
+            mark(st, w, 4);
         }
     };
     std::vector<std::thread> pool;
@@ -1334,6 +1356,19 @@ int waved(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext, u
     for (std::thread &t : pool)
         t.join();
     (void) hipStreamSynchronize(P.ring_s);      // nothing left reading the buffers
+    if (trace_on) {
+        fprintf(stderr, "{\"wave_trace\": {\"W\": %d, \"ext\": %llu, \"chunks\": [", W,
+                (unsigned long long) ext);
+        for (int64_t k = 0; k < n; ++k)
+            fprintf(stderr, "%s%llu", k ? "," : "", (unsigned long long) chunks[(size_t) k].second);
+        fprintf(stderr, "], \"cpus\": [");
+        for (int w = 0; w < W; ++w)
+            fprintf(stderr, "%s%d", w ? "," : "", trace_cpu[(size_t) w]);
+        fprintf(stderr, "], \"ns\": [");
+        for (size_t i = 0; i < trace.size(); ++i)
+            fprintf(stderr, "%s%lld", i ? "," : "", (long long) trace[i]);
+        fprintf(stderr, "]}}\n");
+    }
     return err.load();
 }
 
@@ -2310,6 +2345,7 @@ static void opfn_failed(const char *name, int rc, MPIX_Datatype type)
 #define MPIX_OPFN(name, handle)                                                           \
     void name(void *invec, void *inoutvec, MPIX_Aint *len, MPIX_Datatype *type)           \
     {                                                                                     \
+        env();          /* MPIX_REDOP_OPFN_ABORT, even if the call fails at once */      \
         int rc_ = MPIX_Reduce_local(invec, inoutvec, *len, *type, handle);               \
         if (rc_ != MPIX_REDOP_SUCCESS)                                                    \
             opfn_failed(#name, rc_, *type);                                               \
