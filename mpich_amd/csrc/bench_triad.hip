@@ -274,3 +274,78 @@ extern "C" int mpix_bench_launch_floor(void *fn, const void *in, void *io, int64
         return 15;
     return 0;
 }
+
+// Issue cost vs GPU cost of back-to-back calls, separated: calls are issued in
+// bursts of `burst` (fewer than the stream's queue holds, so the host never
+// waits for the GPU while issuing) and the stream is synchronised between
+// bursts.  out[0]: host us per call to issue `fn` (MPIX_Reduce_local_async at
+// `count`); out[1]: us per call of a whole burst including its drain; out[2],
+// out[3]: the same for an empty one-block kernel; out[4 + j]: host us to issue
+// an empty kernel with a j-th argument block size of kArgSizes (bytes).
+template <int N> struct ArgBlock {
+    uint64_t w[N / 8];
+};
+template <int N>
+__global__ void k_empty_args(ArgBlock<N>)
+{
+}
+template <int N>
+static double issue_args_us(hipStream_t s, int burst, int rounds)
+{
+    ArgBlock<N> g{};
+    double tot = 0;
+    for (int r = 0; r < rounds; ++r) {
+        if (hipStreamSynchronize(s) != hipSuccess)
+            return -1;
+        auto a = std::chrono::steady_clock::now();
+        for (int i = 0; i < burst; ++i)
+            hipLaunchKernelGGL(k_empty_args<N>, dim3(1), dim3(64), 0, s, g);
+        tot += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - a).count();
+    }
+    if (hipStreamSynchronize(s) != hipSuccess)
+        return -1;
+    return tot / ((double) burst * rounds);
+}
+
+extern "C" int mpix_bench_issue_burst(void *fn, const void *in, void *io, int64_t count, int dt,
+                                      int op, void *stream, int burst, int rounds, double *out)
+{
+    if (!fn || burst < 1 || rounds < 2 || !out)
+        return 12;
+    async_reduce_fn f = (async_reduce_fn) fn;
+    hipStream_t s = (hipStream_t) stream;
+    using clk = std::chrono::steady_clock;
+    for (int kind = 0; kind < 2; ++kind) {
+        double issue = 0, whole = 0;
+        for (int r = 0; r < rounds + 1; ++r) {      // round 0 warms up
+            if (hipStreamSynchronize(s) != hipSuccess)
+                return 15;
+            auto a = clk::now();
+            for (int i = 0; i < burst; ++i) {
+                if (kind == 0) {
+                    if (int rc = f(in, io, count, dt, op, stream))
+                        return rc;
+                } else {
+                    hipLaunchKernelGGL(k_empty, dim3(1), dim3(64), 0, s, (int *) nullptr);
+                }
+            }
+            auto b = clk::now();
+            if (hipStreamSynchronize(s) != hipSuccess)
+                return 15;
+            auto c = clk::now();
+            if (r) {
+                issue += std::chrono::duration<double, std::micro>(b - a).count();
+                whole += std::chrono::duration<double, std::micro>(c - a).count();
+            }
+        }
+        out[2 * kind] = issue / ((double) burst * rounds);
+        out[2 * kind + 1] = whole / ((double) burst * rounds);
+    }
+    out[4] = issue_args_us<8>(s, burst, rounds);
+    out[5] = issue_args_us<64>(s, burst, rounds);
+    out[6] = issue_args_us<128>(s, burst, rounds);
+    out[7] = issue_args_us<256>(s, burst, rounds);
+    out[8] = issue_args_us<1024>(s, burst, rounds);
+    out[9] = issue_args_us<2048>(s, burst, rounds);
+    return 0;
+}

@@ -196,7 +196,9 @@ def test_long_double_int_other_entry_points(R, H, oracle):
     a, bs = ins[0], ins[1:]
 
     def orc(inb, inout):
-        assert oracle.reduce_local(inb.reshape(-1).copy(), inout.reshape(-1), n, dt, op) == 0
+        cnt = len(inout)        # records (rows of 32 bytes)
+        assert len(inb) == cnt
+        assert oracle.reduce_local(inb.reshape(-1).copy(), inout.reshape(-1), cnt, dt, op) == 0
         return inout
     # stream-ordered
     da = dev(a)
@@ -219,8 +221,9 @@ def test_long_double_int_other_entry_points(R, H, oracle):
     tgt = a.copy()
     src = bs[0][:m].copy()
     want_v = tgt.copy()
-    for j in range(m):
-        orc(src[j:j + 1], want_v[3 * j:3 * j + 1])
+    sel = want_v[0:3 * m:3].copy()         # the target's payload records
+    orc(src, sel)
+    want_v[0:3 * m:3] = sel
     dt_ = dev(tgt)
     R.check(R.reduce_local_vector(dev(src), dt_, m, 1, 3, dt, op))
     assert np.array_equal(host(dt_).reshape(n, 32), want_v)

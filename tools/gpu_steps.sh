@@ -1,0 +1,45 @@
+# GPU command file: run the named steps in order on the GPU box, each under its
+# own time limit, stopping at the first that fails.  Outputs under
+# gpurun_out/steps/ (copied into profiles/ by hand when kept).
+# usage (gpurun): bash tools/gpu_steps.sh <step> [<step> ...]
+#   tests=<pytest -k expr>  the -m gpu tests matching the expression
+#   gputests                the whole -m gpu suite (the driver's tier)
+#   smoke                   __graft_entry__.smoke()
+#   rehearse                bench.py --gpus 4 on the one GPU (gloo, shared device)
+#   swing                   tools/pageable_swing.py, default and GPU-node worker affinity
+#   floor                   tools/call_floor.py
+#   policy                  tools/policy_concurrent.py
+#   bench                   the default bench.py line
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/steps
+mkdir -p $O
+run() {     # run <name> <seconds> <command...>: stdout to $O/<name>.out, stderr to .err
+    local name=$1 secs=$2
+    shift 2
+    echo "== $name ($(date +%T))"
+    timeout -k 10 $secs "$@" > $O/$name.out 2> $O/$name.err
+    local rc=$?
+    echo "== $name rc=$rc"
+    tail -3 $O/$name.out
+    if [ $rc -ne 0 ]; then tail -20 $O/$name.err; fi
+    return $rc
+}
+for step in "$@"; do
+    case $step in
+        tests=*) run tests 600 python3 -u -m pytest tests -x -q -m gpu -k "${step#tests=}" \
+                     --timeout 200 --timeout-method thread -p no:cacheprovider || exit $? ;;
+        gputests) run gputests 1000 python3 -u -m pytest tests -x -q -m gpu --timeout 300 \
+                     --timeout-method thread -p no:cacheprovider || exit $? ;;
+        smoke) run smoke 200 python3 -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
+        rehearse) run rehearse 1100 env P=4 bash tools/gpu_rehearse.sh || exit $? ;;
+        swing) run swing_default 300 python3 tools/pageable_swing.py --label default || exit $?
+               run swing_gpuaff 300 env MPIX_REDOP_PAGEABLE_AFFINITY=gpu python3 \
+                   tools/pageable_swing.py --label gpu_affinity || exit $? ;;
+        floor) run floor 200 python3 tools/call_floor.py || exit $? ;;
+        policy) run policy 300 python3 tools/policy_concurrent.py || exit $? ;;
+        bench) run bench 600 python3 bench.py || exit $? ;;
+        *) echo "unknown step $step"; exit 2 ;;
+    esac
+done
