@@ -68,17 +68,16 @@ def pages_node(arr, samples=64):
 
 
 def gpu_node():
+    """the GPU's NUMA node from sysfs (its PCI function's numa_node)"""
     try:
-        bus = torch.cuda.get_device_properties(0).pci_bus_id
+        pr = torch.cuda.get_device_properties(0)
+        bdf = '%04x:%02x:%02x.0' % (pr.pci_domain_id, pr.pci_bus_id, pr.pci_device_id)
     except Exception:
-        bus = None
-    for cand in ([bus] if bus else []):
-        for p in ('/sys/bus/pci/devices/%s/numa_node' % cand.lower(),):
-            try:
-                return int(open(p).read()), cand
-            except OSError:
-                pass
-    return None, bus
+        return None, None
+    try:
+        return int(open('/sys/bus/pci/devices/%s/numa_node' % bdf).read()), bdf
+    except OSError:
+        return None, bdf
 
 
 def traced(fn):

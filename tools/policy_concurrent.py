@@ -54,7 +54,10 @@ def main():
     acc = torch.rand(m, device=dev)
     csrc = torch.empty(n, dtype=torch.float32, device=dev)
     cdst = torch.empty(n, dtype=torch.float32, device=dev)
-    ks, cs = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    # the copies on a high-priority stream: a hardware queue of its own (two
+    # streams of one priority may share one of the GPU_MAX_HW_QUEUES queues and
+    # then run one after the other); row['overlapped'] checks it on the GPU clock
+    ks, cs = torch.cuda.Stream(dev), torch.cuda.Stream(dev, priority=-1)
     torch.cuda.synchronize()
     kernels = {
         'contig_fp32_sum_1GiB': (lambda: redop.check(redop.reduce_local_async(
@@ -77,6 +80,10 @@ def main():
                         fn()
                         torch.cuda.synchronize()
                         ncopies = 0
+                        t0 = torch.cuda.Event(enable_timing=True)
+                        t0.record(torch.cuda.current_stream())
+                        ks.wait_stream(torch.cuda.current_stream())
+                        cs.wait_stream(torch.cuda.current_stream())
                         if copy_on:
                             # enough copies to outlast the timed launches
                             ncopies = max(8, int(3 * a.reps * nbytes / (2 * n * 4)) + 8)
@@ -87,15 +94,27 @@ def main():
                                 for _ in range(ncopies):
                                     cdst.copy_(csrc)
                                 c1.record(cs)
+                        k0 = torch.cuda.Event(enable_timing=True)
+                        k1 = torch.cuda.Event(enable_timing=True)
                         with torch.cuda.stream(ks):
+                            k0.record(ks)
                             ms = timed(fn, a.reps, ks)
+                            k1.record(ks)
                         torch.cuda.synchronize()
                         row = dict(round=rnd, kernel=kname, concurrent_copy=copy_on,
                                    xcd_mask=pol, kernel_ms=round(ms, 4),
                                    kernel_GBs=round(nbytes / (ms * 1e-3) / 1e9, 1))
+                        row['kernels_span_ms'] = [round(t0.elapsed_time(k0), 3),
+                                                  round(t0.elapsed_time(k1), 3)]
                         if copy_on:
                             cms = c0.elapsed_time(c1) / ncopies
                             row['copy_ms_each'] = round(cms, 4)
+                            # both windows on one clock: the kernels must sit
+                            # inside the copies' window, or nothing overlapped
+                            row['copies_span_ms'] = [round(t0.elapsed_time(c0), 3),
+                                                     round(t0.elapsed_time(c1), 3)]
+                            row['overlapped'] = (t0.elapsed_time(c0) < t0.elapsed_time(k0) and
+                                                 t0.elapsed_time(k1) < t0.elapsed_time(c1))
                         res['rows'].append(row)
     finally:
         dm = default['xcd_mask']
