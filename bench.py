@@ -97,6 +97,11 @@ def bench_lib():
                                            ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                            ctypes.POINTER(ctypes.c_double),
                                            ctypes.POINTER(ctypes.c_double)]
+    L.mpix_bench_chunked_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
+                                           ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                           ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                           ctypes.POINTER(ctypes.c_double)]
     return L
 
 
@@ -131,6 +136,29 @@ def chunked_async_c(B, inb, inout, n, stream, chunk_bytes):
         out.append(dict(chunk_bytes=ck, calls=nch, GiBs=round(3 * nch * ck / total.value / GIB, 1),
                         us_per_call=round(1e6 * total.value / nch, 2),
                         issue_us_per_call=round(1e6 * issue.value / nch, 2)))
+    return out
+
+
+def chunked_batch_c(B, inb, inout, n, stream, chunk_bytes, batch=64):
+    """the same chunked loop with the chunks handed over `batch` at a time
+    through MPIX_Reduce_local_batch_async (one launch per batch): the per-chunk
+    cost of an engine with several chunks ready"""
+    fn = ctypes.cast(redop.lib().MPIX_Reduce_local_batch_async, ctypes.c_void_p).value
+    out = []
+    for ck in chunk_bytes:
+        m = ck // 4
+        nch = n // m
+        issue, total = ctypes.c_double(), ctypes.c_double()
+        rc = B.mpix_bench_chunked_batch(fn, inb.data_ptr(), inout.data_ptr(), nch * m, m, 4,
+                                        H.as_c_int(H.MPI_FLOAT), H.as_c_int(H.MPI_SUM),
+                                        stream.cuda_stream, batch, ctypes.byref(issue),
+                                        ctypes.byref(total))
+        if rc:
+            raise RuntimeError('chunked batch loop failed: MPI error class %d' % rc)
+        out.append(dict(chunk_bytes=ck, batch=batch, calls=(nch + batch - 1) // batch,
+                        GiBs=round(3 * nch * ck / total.value / GIB, 1),
+                        us_per_chunk=round(1e6 * total.value / nch, 3),
+                        issue_us_per_chunk=round(1e6 * issue.value / nch, 3)))
     return out
 
 
@@ -474,6 +502,8 @@ def single_gpu(args, dev):
             B, inb, inout, n, stream,
             (64 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20, 64 << 20) if args.sweep
             else (64 << 10, 1 << 20, 16 << 20))
+        result['chunked_batch_c'] = chunked_batch_c(B, inb, inout, n, stream,
+                                                    (64 << 10, 1 << 20))
         end_to_end(result, n, dev)
         crossover = host_crossover_gpu(B)
         result['configs_3_and_5'] = other_configs(inb, inout, n, stream)

@@ -356,6 +356,27 @@ void MPIX_EQUAL_fn(void *invec, void *inoutvec, MPIX_Aint *len, MPIX_Datatype *t
 int MPIX_Redop_last_error(void);
 const char *MPIX_Redop_error_string(int code);
 
+/* ---- several ready chunks in one launch (stream-ordered) ----
+ * k independent combines inoutbufs[i][j] = OP(inoutbufs[i][j], inbufs[i][j]),
+ * j < counts[i], i < k, of one datatype and op, issued as ONE kernel launch on
+ * `stream`: the same bits as k MPIX_Reduce_local_async calls (each segment is
+ * split into head / packets / tail exactly as a call of its own would be) at
+ * the host cost of one launch (HIP's issue is ~2.5 us per launch,
+ * profiles/r04_call_floor.json).  For the engines that find several vertices
+ * ready at once -- gentran_utils.c:157-167 calls MPIR_Reduce_local per ready
+ * reduce vertex, mpidu_sched.c:309-316 per reduce entry of a schedule round.
+ * 1 <= k <= MPIX_BATCH_MAX, else MPI_ERR_ARG; no triple's target range may
+ * overlap another triple's target or source range (MPI_ERR_BUFFER: the
+ * segments run in no particular order); zero counts are skipped; every
+ * operand must be reachable from the stream's device, as for
+ * MPIX_Reduce_local_async.  All checks happen before any device work.
+ * MPI_REPLACE / MPI_NO_OP / MPIX_EQUAL, operands that are not element-aligned
+ * and the 32-byte pair types are issued one launch per triple. */
+#define MPIX_BATCH_MAX 64
+int MPIX_Reduce_local_batch_async(const void *const *inbufs, void *const *inoutbufs,
+                                  const MPIX_Aint *counts, int k, MPIX_Datatype datatype,
+                                  MPIX_Op op, void *stream);
+
 /* ---- launch geometry (performance knob, not semantics) ----
  * threads per block and a cap on the grid (0 = one tile per block, no
  * grid-stride loop).  The packets-per-thread unroll is a compile-time

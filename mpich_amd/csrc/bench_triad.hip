@@ -349,3 +349,44 @@ extern "C" int mpix_bench_issue_burst(void *fn, const void *in, void *io, int64_
     out[9] = issue_args_us<2048>(s, burst, rounds);
     return 0;
 }
+
+// The chunked loop of mpix_bench_chunked_async, the chunks handed over
+// `batch` at a time through MPIX_Reduce_local_batch_async (`fn`): what an
+// engine with several ready chunks pays per chunk.
+typedef int (*batch_reduce_fn)(const void *const *, void *const *, const int64_t *, int, int,
+                               int, void *);
+extern "C" int mpix_bench_chunked_batch(void *fn, const void *in, void *io, int64_t count,
+                                        int64_t chunk, int elem_size, int dt, int op, void *stream,
+                                        int batch, double *issue_s, double *total_s)
+{
+    if (!fn || chunk < 1 || count < chunk || elem_size < 1 || batch < 1 || batch > 64 ||
+        !issue_s || !total_s)
+        return 12;
+    batch_reduce_fn f = (batch_reduce_fn) fn;
+    hipStream_t s = (hipStream_t) stream;
+    if (hipStreamSynchronize(s) != hipSuccess)
+        return 15;
+    const int64_t nch = count / chunk;
+    std::vector<const void *> ins(64);
+    std::vector<void *> ios(64);
+    std::vector<int64_t> cnt(64, chunk);
+    auto a = std::chrono::steady_clock::now();
+    for (int64_t k = 0; k < nch; k += batch) {
+        const int m = (int) std::min<int64_t>(batch, nch - k);
+        for (int q = 0; q < m; ++q) {
+            const int64_t off = (k + q) * chunk * elem_size;
+            ins[q] = (const char *) in + off;
+            ios[q] = (char *) io + off;
+        }
+        int rc = f(ins.data(), ios.data(), cnt.data(), m, dt, op, stream);
+        if (rc)
+            return rc;
+    }
+    auto b = std::chrono::steady_clock::now();
+    if (hipStreamSynchronize(s) != hipSuccess)
+        return 15;
+    auto c = std::chrono::steady_clock::now();
+    *issue_s = std::chrono::duration<double>(b - a).count();
+    *total_s = std::chrono::duration<double>(c - a).count();
+    return 0;
+}

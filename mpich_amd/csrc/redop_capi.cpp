@@ -1737,6 +1737,72 @@ int MPIX_Reduce_local_async(const void *inbuf, void *inoutbuf, MPIX_Aint count,
                            (hipStream_t) stream));
 }
 
+// Several ready chunks in one launch (include/mpix_redop.h).  Checks first,
+// all before any device work: the arguments, then that no triple's target
+// overlaps another triple's target or source (the batch runs them in no
+// particular order), then that the stream's device can reach every operand.
+static_assert(mpix::kMaxBatchSegs == MPIX_BATCH_MAX, "one batch limit");
+
+int MPIX_Reduce_local_batch_async(const void *const *inbufs, void *const *inoutbufs,
+                                  const MPIX_Aint *counts, int k, MPIX_Datatype datatype,
+                                  MPIX_Op op, void *stream)
+{
+    if (k < 1 || k > MPIX_BATCH_MAX || !inbufs || !inoutbufs || !counts)
+        return set_err(MPIX_REDOP_ERR_ARG);
+    uint32_t it = 0;
+    uint64_t ext = 0;
+    for (int i = 0; i < k; ++i) {
+        int rc = validate(inbufs[i], inoutbufs[i], counts[i], (uint32_t) datatype, (uint32_t) op,
+                          &it, &ext);
+        if (rc != MPIX_REDOP_SUCCESS)
+            return set_err(rc);
+    }
+    for (int i = 0; i < k; ++i) {
+        if (!counts[i])
+            continue;
+        const uint64_t bi = (uint64_t) counts[i] * ext;
+        for (int j = 0; j < k; ++j) {
+            if (j == i || !counts[j])
+                continue;
+            const uint64_t bj = (uint64_t) counts[j] * ext;
+            const uintptr_t ti = (uintptr_t) inoutbufs[i], tj = (uintptr_t) inoutbufs[j],
+                            sj = (uintptr_t) inbufs[j];
+            if ((ti < tj + bj && tj < ti + bi) || (ti < sj + bj && sj < ti + bi))
+                return set_err(MPIX_REDOP_ERR_BUFFER);
+        }
+    }
+    const uint32_t opi = (uint32_t) op & 0xf;
+    const Entry *e = (opi >= 13) ? nullptr : gpu_entry(opi, it);
+    if (opi < 13 && !e)
+        return set_err(MPIX_REDOP_ERR_TYPE);
+    const void *pin[MPIX_BATCH_MAX];
+    void *pio[MPIX_BATCH_MAX];
+    uint64_t cnt[MPIX_BATCH_MAX];
+    int m = 0, launch = -2;
+    for (int i = 0; i < k; ++i) {
+        if (!counts[i])
+            continue;
+        const void *a, *b;
+        if (!reachable(inbufs[i], (hipStream_t) stream, &launch, &a) ||
+            !reachable(inoutbufs[i], (hipStream_t) stream, &launch, &b))
+            return set_err(MPIX_REDOP_ERR_BUFFER);
+        pin[m] = a;
+        pio[m] = (void *) b;
+        cnt[m++] = (uint64_t) counts[i];
+    }
+    if (!m)
+        return set_err(MPIX_REDOP_SUCCESS);
+    if (!e) {       // REPLACE / NO_OP / EQUAL: one call each
+        for (int i = 0; i < m; ++i) {
+            int rc = enqueue(pin[i], pio[i], cnt[i], it, ext, (uint32_t) op, (hipStream_t) stream);
+            if (rc != MPIX_REDOP_SUCCESS)
+                return set_err(rc);
+        }
+        return set_err(MPIX_REDOP_SUCCESS);
+    }
+    return set_err(hip_err(e->batch(pin, pio, cnt, m, params(), launch_cfg(), (hipStream_t) stream)));
+}
+
 int MPIX_Reduce_local(const void *inbuf, void *inoutbuf, MPIX_Aint count, MPIX_Datatype datatype,
                       MPIX_Op op)
 {

@@ -54,7 +54,11 @@ struct Entry {
                       const LaunchCfg &, hipStream_t);
     hipError_t (*tree)(const void *const *ins, int k, void *out, uint64_t count, const Params &,
                        const LaunchCfg &, hipStream_t);
+    hipError_t (*batch)(const void *const *ins, void *const *ios, const uint64_t *counts, int k,
+                        const Params &, const LaunchCfg &, hipStream_t);
 };
+
+constexpr int kMaxBatchSegs = 64;       // MPIX_BATCH_MAX
 
 constexpr int kMaxMultiInputs = 16;
 

@@ -179,17 +179,20 @@ __device__ __forceinline__ v4u combine16_fast(v4u a, v4u b, const Params &prm, b
 // (still one dwordx4 per lane; the lines are shared with the neighbours').
 // GRP: issue all U `inout` packet loads, then all U `in` loads (instead of
 // alternating them per packet)
-template <class C, int U, bool NTL, bool NTS, bool AIN = true, bool GRP = MPIX_REDOP_GROUPED_LOADS>
-__global__ void __launch_bounds__(1024)
-k_contig(const typename C::unit *__restrict__ in, typename C::unit *__restrict__ io,
-         uint64_t head, uint64_t npk, uint64_t tail_start, uint32_t ntail, Params prm)
+// The body of one contiguous combine as block `bid` of `nblk` (k_contig: the
+// launch's own block; k_batch: a block of its segment).
+template <class C, int U, bool NTL, bool NTS, bool AIN, bool GRP>
+__device__ __forceinline__ void
+contig_body(const typename C::unit *__restrict__ in, typename C::unit *__restrict__ io,
+            uint64_t head, uint64_t npk, uint64_t tail_start, uint32_t ntail, const Params &prm,
+            uint64_t bid, uint64_t nblk)
 {
     const v4u *__restrict__ vin = reinterpret_cast<const v4u *>(in + head);
     const char *__restrict__ cin = reinterpret_cast<const char *>(in + head);
     v4u *__restrict__ vio = reinterpret_cast<v4u *>(io + head);
     const uint64_t nt = blockDim.x;
     const uint64_t tile = nt * U;
-    const uint64_t stride = (uint64_t) gridDim.x * tile;
+    const uint64_t stride = nblk * tile;
     auto ldin = [&](uint64_t k) -> v4u {
         if constexpr (AIN)
             return ld16<NTL>(vin + k);
@@ -198,7 +201,7 @@ k_contig(const typename C::unit *__restrict__ in, typename C::unit *__restrict__
     };
     const bool wt = wt_block(prm);
     auto st = [&](v4u *p, v4u v) { st16_pol<NTS>(p, v, wt); };
-    for (uint64_t i = (uint64_t) blockIdx.x * tile + threadIdx.x; i < npk; i += stride) {
+    for (uint64_t i = bid * tile + threadIdx.x; i < npk; i += stride) {
         if (i + (U - 1) * nt < npk) {
             v4u a[U], b[U];
             if constexpr (GRP) {
@@ -254,12 +257,21 @@ k_contig(const typename C::unit *__restrict__ in, typename C::unit *__restrict__
             }
         }
     }
-    if (blockIdx.x == 0) {
+    if (bid == 0) {
         for (uint64_t t = threadIdx.x; t < head; t += nt)
             io[t] = C::apply(io[t], in[t], prm);
         for (uint64_t t = threadIdx.x; t < ntail; t += nt)
             io[tail_start + t] = C::apply(io[tail_start + t], in[tail_start + t], prm);
     }
+}
+
+template <class C, int U, bool NTL, bool NTS, bool AIN = true, bool GRP = MPIX_REDOP_GROUPED_LOADS>
+__global__ void __launch_bounds__(1024)
+k_contig(const typename C::unit *__restrict__ in, typename C::unit *__restrict__ io,
+         uint64_t head, uint64_t npk, uint64_t tail_start, uint32_t ntail, Params prm)
+{
+    contig_body<C, U, NTL, NTS, AIN, GRP>(in, io, head, npk, tail_start, ntail, prm, blockIdx.x,
+                                          gridDim.x);
     if (prm.done) {     // small synchronous call (launch_contig sets it)
         __threadfence();            // every wave: its stores complete
         __syncthreads();
@@ -277,6 +289,46 @@ k_contig(const typename C::unit *__restrict__ in, typename C::unit *__restrict__
             }
         }
     }
+}
+
+// Batch of independent contiguous combines in one launch
+// (MPIX_Reduce_local_batch_async): segment s owns blocks [blk0, blk0 + nblk)
+// of the grid, one tile each, laid out exactly as a k_contig launch of that
+// segment alone would lay them out (same head / packets / tail split, same
+// per-element combine), so the bits are those of one call per segment.
+constexpr int kMaxBatch = kMaxBatchSegs;
+struct BatchSeg {
+    const void *in;
+    void *io;
+    uint64_t npk;
+    uint32_t blk0;      // first block of the segment
+    uint8_t head, ntail, ain, pad;
+};
+struct BatchTab {
+    BatchSeg s[kMaxBatch];
+};
+
+template <class C, int U, bool NTL, bool NTS>
+__global__ void __launch_bounds__(1024)
+k_batch(BatchTab tab, int nseg, Params prm)
+{
+    using T = typename C::unit;
+    constexpr uint64_t E = 16 / sizeof(T);
+    const uint32_t b = blockIdx.x;
+    int q = 0;      // the segment of this block: the last with blk0 <= b (uniform)
+    while (q + 1 < nseg && tab.s[q + 1].blk0 <= b)
+        ++q;
+    const BatchSeg &g = tab.s[q];
+    const uint32_t next = q + 1 < nseg ? tab.s[q + 1].blk0 : gridDim.x;
+    const T *in = static_cast<const T *>(g.in);
+    T *io = static_cast<T *>(g.io);
+    const uint64_t tail_start = g.head + g.npk * E;
+    if (g.ain)
+        contig_body<C, U, NTL, NTS, true, MPIX_REDOP_GROUPED_LOADS>(
+            in, io, g.head, g.npk, tail_start, g.ntail, prm, b - g.blk0, next - g.blk0);
+    else
+        contig_body<C, U, NTL, NTS, false, MPIX_REDOP_GROUPED_LOADS>(
+            in, io, g.head, g.npk, tail_start, g.ntail, prm, b - g.blk0, next - g.blk0);
 }
 
 // Multi-input combine: inout = OP(...OP(OP(inout, in[0]), in[1])..., in[k-1]),
@@ -829,10 +881,80 @@ hipError_t launch_iov(const void *in, void *io, const int64_t *d_seg_off, const 
     return hipGetLastError();
 }
 
+// k independent contiguous combines (no operand range of one overlapping a
+// target of another; the caller checked) in one k_batch launch; segments of
+// zero count are skipped, segments whose operands are not element-aligned go
+// to launch_contig's element-wise kernel, as do all of a 32-byte unit type
+template <class C>
+hipError_t launch_batch(const void *const *ins, void *const *ios, const uint64_t *counts, int k,
+                        const Params &prm, const LaunchCfg &cfg, hipStream_t s)
+{
+    using T = typename C::unit;
+    Params p = prm;
+    p.done = nullptr;
+    if constexpr (sizeof(T) > 16) {
+        for (int i = 0; i < k; ++i)
+            if (counts[i]) {
+                hipError_t e = launch_contig<C>(ins[i], ios[i], counts[i], p, cfg, s);
+                if (e != hipSuccess)
+                    return e;
+            }
+        return hipSuccess;
+    } else {
+        constexpr uint64_t E = 16 / sizeof(T);
+        const uint64_t tile = (uint64_t) cfg.block * MPIX_REDOP_UNROLL;
+        BatchTab tab;
+        int n = 0;
+        uint64_t blocks = 0;
+        auto flush = [&]() -> hipError_t {
+            if (!n)
+                return hipSuccess;
+            Params q = p;
+            set_store_policy(q, cfg, (unsigned) blocks);
+            hipLaunchKernelGGL((k_batch<C, MPIX_REDOP_UNROLL, MPIX_REDOP_NT_LOAD, MPIX_REDOP_NT_STORE>),
+                               dim3((unsigned) blocks), dim3(cfg.block), 0, s, tab, n, q);
+            n = 0;
+            blocks = 0;
+            return hipGetLastError();
+        };
+        for (int i = 0; i < k; ++i) {
+            const uint64_t count = counts[i];
+            if (!count)
+                continue;
+            const uintptr_t ai = reinterpret_cast<uintptr_t>(ins[i]);
+            const uintptr_t ao = reinterpret_cast<uintptr_t>(ios[i]);
+            if ((ai % sizeof(T)) || (ao % sizeof(T))) {
+                hipError_t e = launch_contig<C>(ins[i], ios[i], count, p, cfg, s);
+                if (e != hipSuccess)
+                    return e;
+                continue;
+            }
+            uint64_t head = ((16 - (ao & 15)) & 15) / sizeof(T);
+            if (head > count)
+                head = count;
+            const uint64_t npk = (count - head) / E;
+            const uint64_t ntail = count - head - npk * E;
+            uint64_t nb = (npk + tile - 1) / tile;
+            if (nb == 0)
+                nb = 1;         // a segment of head / tail elements only
+            if (blocks + nb > 0x7fffffffull) {
+                hipError_t e = flush();
+                if (e != hipSuccess)
+                    return e;
+            }
+            tab.s[n] = BatchSeg{ins[i], ios[i], npk, (uint32_t) blocks, (uint8_t) head,
+                                (uint8_t) ntail, (uint8_t) ((ai & 15) == (ao & 15)), 0};
+            blocks += nb;
+            ++n;
+        }
+        return flush();
+    }
+}
+
 template <class C> constexpr Entry entry()
 {
     return Entry{&launch_contig<C>, &launch_vector<C>, &launch_multi<C>, &launch_iov<C>,
-                 &launch_tree<C>};
+                 &launch_tree<C>, &launch_batch<C>};
 }
 
 }  // namespace mpix

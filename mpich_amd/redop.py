@@ -50,6 +50,8 @@ def lib():
                                               i32),
             'MPIX_Reduce_local_tree_async': ([ctypes.POINTER(vp), i32, vp, aint, i32, i32, vp],
                                              i32),
+            'MPIX_Reduce_local_batch_async': ([ctypes.POINTER(vp), ctypes.POINTER(vp),
+                                               ctypes.POINTER(aint), i32, i32, i32, vp], i32),
             'MPIX_Reduce_local_iov_async': ([vp, vp, aint, ctypes.POINTER(aint),
                                              ctypes.POINTER(aint), i32, i32, vp], i32),
             'MPIX_Reduce_local_iovec_async': ([vp, vp, aint, ctypes.POINTER(aint),
@@ -280,6 +282,25 @@ def reduce_local_tree_async(inbufs, outbuf, count, datatype, op, stream=None):
     return lib().MPIX_Reduce_local_tree_async(arr, len(inbufs), _addr(outbuf), count,
                                               H.as_c_int(datatype), H.as_c_int(op),
                                               _stream_ptr(stream))
+
+
+BATCH_MAX = 64
+
+
+def reduce_local_batch_async(inbufs, inoutbufs, counts, datatype, op, stream=None):
+    """k independent combines inoutbufs[i] OP= inbufs[i] (counts[i] elements
+    each) in one launch on `stream` -- the same bits as k reduce_local_async
+    calls; no target may overlap another triple's source or target."""
+    k = len(counts)
+    if len(inbufs) != k or len(inoutbufs) != k:
+        raise ValueError('inbufs, inoutbufs and counts must have one entry per triple')
+    for b, o, c in zip(inbufs, inoutbufs, counts):
+        _span_check(c, datatype, op, b, o)
+    ins = (ctypes.c_void_p * max(k, 1))(*[_addr(b) for b in inbufs])
+    ios = (ctypes.c_void_p * max(k, 1))(*[_addr(b) for b in inoutbufs])
+    cnt = (ctypes.c_ssize_t * max(k, 1))(*counts)
+    return lib().MPIX_Reduce_local_batch_async(ins, ios, cnt, k, H.as_c_int(datatype),
+                                               H.as_c_int(op), _stream_ptr(stream))
 
 
 IPC_HANDLE_BYTES = 64

@@ -98,6 +98,12 @@ def test_queries_and_knobs_make_no_hip_call(shim):
         'L.MPIX_Reduce_local.argtypes = [vp, vp, a, i, i]',
         'assert L.MPIX_Reduce_local(None, None, 0, FLOAT, SUM) == 0     # count 0',
         'assert L.MPIX_Reduce_local(None, None, -1, FLOAT, SUM) != 0    # bad count',
+        # batch: argument and overlap errors are found before any HIP call
+        'P = ctypes.c_void_p * 2; C = ctypes.c_ssize_t * 2',
+        'assert L.MPIX_Reduce_local_batch_async(P(1 << 20, 2 << 20), P(4096, 4100), C(4, 4), 2,'
+        ' FLOAT, SUM, None) == 1      # MPI_ERR_BUFFER',
+        'assert L.MPIX_Reduce_local_batch_async(P(1 << 20, 2 << 20), P(4096, 8192), C(0, 0), 2,'
+        ' FLOAT, SUM, None) == 0      # nothing to do',
     ])
     hits, last = _probe(shim, calls)
     assert hits == 0, 'HIP entered through %s' % last
