@@ -380,6 +380,10 @@ def cpu_baseline(seconds, count, crossover_rows):
 
 
 def load_pmc(path, count):
+    """(HBM bytes per launch, the file they come from): the PMC summary of a
+    separate rocprofv3 FETCH_SIZE / WRITE_SIZE pass over the same command
+    (tools/gpu_evidence.sh, tools/pmc_summary.py) -- quoted, not measured in
+    this process, so the line names its source"""
     for p in (path, os.path.join(ROOT, 'profiles', 'r01_pmc_summary.json')):
         try:
             with open(p) as f:
@@ -388,8 +392,8 @@ def load_pmc(path, count):
             continue
         k = d.get('kernels', {}).get('reduce_local_fp32_sum')
         if k and k.get('count') == count:
-            return k.get('hbm_bytes_per_launch')
-    return None
+            return k.get('hbm_bytes_per_launch'), os.path.relpath(p, ROOT)
+    return None, None
 
 
 # ------------------------------------------------------------------ N = 1
@@ -444,6 +448,7 @@ def single_gpu(args, dev):
     leg = reduce_local_leg(args, 1, 0, dev)
     inb, inout, stream, kreps = leg['inb'], leg['inout'], leg['stream'], leg['kreps']
     achieved = nbytes_alg / (leg['k_avg'] * 1e-3) / 1e9
+    traffic, traffic_src = load_pmc(args.pmc, n)
     result = {
         'metric': METRIC,
         'value': round(nbytes_alg * args.steps / leg['t'] / GIB, 2),
@@ -467,7 +472,10 @@ def single_gpu(args, dev):
         'roofline': {
             'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
             'frac': round(achieved / HBM_PEAK_GBS, 4),
-            'traffic': load_pmc(args.pmc, n),
+            'traffic': traffic,
+            'traffic_source': ('quoted from %s (a separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE '
+                               'pass of the same command, gfx950-corrected)' % traffic_src)
+                              if traffic_src else None,
             'kernel_ms_avg': round(leg['k_avg'], 4), 'kernel_ms_median_batch': round(leg['k_med'], 4),
             'kernel_ms_min_batch': round(leg['k_min'], 4), 'kernel_launches_timed': 3 * kreps,
             'algorithmic_bytes_per_launch': nbytes_alg,

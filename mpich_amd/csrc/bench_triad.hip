@@ -390,3 +390,24 @@ extern "C" int mpix_bench_chunked_batch(void *fn, const void *in, void *io, int6
     *total_s = std::chrono::duration<double>(c - a).count();
     return 0;
 }
+
+// A copy kernel of `blocks` workgroups (grid-stride, 16-byte packets): HBM
+// traffic at a chosen fraction of the device's rate -- the stand-in for
+// RCCL's point-to-point kernels (a few channels' worth of CUs writing what
+// arrives over xGMI into HBM) next to a combine (tools/policy_concurrent.py).
+__global__ void k_trickle(f4 *__restrict__ dst, const f4 *__restrict__ src, uint64_t n)
+{
+    const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        dst[i] = src[i];
+}
+
+extern "C" int mpix_bench_trickle_copy(void *dst, const void *src, uint64_t bytes, int blocks,
+                                       void *stream)
+{
+    if (!dst || !src || blocks < 1 || (bytes & 15) || ((uintptr_t) dst & 15) || ((uintptr_t) src & 15))
+        return 12;
+    hipLaunchKernelGGL(k_trickle, dim3(blocks), dim3(256), 0, (hipStream_t) stream, (f4 *) dst,
+                       (const f4 *) src, bytes / 16);
+    return hipGetLastError() == hipSuccess ? 0 : 15;
+}

@@ -1152,7 +1152,12 @@ int pipelined(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ex
     return err.load();
 }
 
-// Spin barrier for the wave workers (sense reversal; yields while waiting).
+// Spin barrier for the wave workers (sense reversal).  Waiters spin with
+// `pause` and give the CPU up only after 20 ms: a yielding waiter on a CPU
+// shared with other runnable tasks can be left off it for a whole scheduler
+// slice, and every step of the wave waits for the last worker to leave the
+// barrier -- one such stall took a 256 MiB call from 12.6 to 21 ms
+// (profiles/r04_pageable_swing.json, the slowest trace's step 7).
 struct SpinBarrier {
     std::atomic<int> left;
     std::atomic<int> gen{0};
@@ -1166,8 +1171,13 @@ struct SpinBarrier {
             gen.fetch_add(1, std::memory_order_release);
             return;
         }
-        while (gen.load(std::memory_order_acquire) == g)
-            std::this_thread::yield();
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint32_t spins = 1; gen.load(std::memory_order_acquire) == g; ++spins) {
+            _mm_pause();
+            if ((spins & 0x3ff) == 0 &&
+                std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20))
+                std::this_thread::yield();
+        }
     }
 };
 

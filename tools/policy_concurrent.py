@@ -43,7 +43,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--reps', type=int, default=10)
     ap.add_argument('--rounds', type=int, default=4)
+    ap.add_argument('--traffic', default='full,16,64',
+                    help="concurrent copy kinds: 'full' (torch D2D copy, the device's rate) "
+                         "and/or workgroup counts of the throttled copy kernel")
     a = ap.parse_args()
+    import ctypes
+    B = ctypes.CDLL(os.path.join(ROOT, 'mpich_amd', 'libmpix_bench.so'))
+    B.mpix_bench_trickle_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                          ctypes.c_int, ctypes.c_void_p]
     assert redop.lib().MPIX_Redop_init() == 0
     dev = torch.device('cuda', 0)
     n = 1 << 28                                  # 1 GiB fp32
@@ -65,15 +72,24 @@ def main():
         'multi7_fp32_sum_256MiB': (lambda: redop.check(redop.reduce_local_multi_async(
             ins, acc, m, H.MPI_FLOAT, H.MPI_SUM, ks)), 9 * m * 4),
     }
-    # the copy stream's own rate, alone
-    copy_ms = timed(lambda: cdst.copy_(csrc), 10, torch.cuda.current_stream())
-    res = dict(copy_alone_ms=round(copy_ms, 4),
-               copy_alone_GBs=round(2 * n * 4 / (copy_ms * 1e-3) / 1e9, 1), rows=[])
+    def copier(kind):
+        if kind == 'full':
+            return lambda: cdst.copy_(csrc)
+        nb = int(kind)
+        return lambda: B.mpix_bench_trickle_copy(cdst.data_ptr(), csrc.data_ptr(), n * 4, nb,
+                                                 ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    kinds = ['none'] + a.traffic.split(',')
+    # each copier's own rate, alone
+    alone = {}
+    for kind in kinds[1:]:
+        cms = timed(copier(kind), 5, torch.cuda.current_stream())
+        alone[kind] = dict(ms=round(cms, 4), GBs=round(2 * n * 4 / (cms * 1e-3) / 1e9, 1))
+    res = dict(copy_alone=alone, rows=[])
     default = redop.get_store_policy()
     try:
         for rnd in range(a.rounds):
             for kname, (fn, nbytes) in kernels.items():
-                for copy_on in (False, True):
+                for copy_on in kinds:
                     pols = (0, 0x88) if rnd % 2 == 0 else (0x88, 0)
                     for pol in pols:
                         redop.check(redop.set_store_policy(pol, 0, 0, 0))
@@ -84,15 +100,17 @@ def main():
                         t0.record(torch.cuda.current_stream())
                         ks.wait_stream(torch.cuda.current_stream())
                         cs.wait_stream(torch.cuda.current_stream())
-                        if copy_on:
+                        if copy_on != 'none':
                             # enough copies to outlast the timed launches
-                            ncopies = max(8, int(3 * a.reps * nbytes / (2 * n * 4)) + 8)
+                            per = alone[copy_on]['ms']
+                            ncopies = max(4, int(3 * a.reps * nbytes / 6.5e9 / per) + 4)
                             c0 = torch.cuda.Event(enable_timing=True)
                             c1 = torch.cuda.Event(enable_timing=True)
+                            cp = copier(copy_on)
                             with torch.cuda.stream(cs):
                                 c0.record(cs)
                                 for _ in range(ncopies):
-                                    cdst.copy_(csrc)
+                                    cp()
                                 c1.record(cs)
                         k0 = torch.cuda.Event(enable_timing=True)
                         k1 = torch.cuda.Event(enable_timing=True)
@@ -106,7 +124,7 @@ def main():
                                    kernel_GBs=round(nbytes / (ms * 1e-3) / 1e9, 1))
                         row['kernels_span_ms'] = [round(t0.elapsed_time(k0), 3),
                                                   round(t0.elapsed_time(k1), 3)]
-                        if copy_on:
+                        if copy_on != 'none':
                             cms = c0.elapsed_time(c1) / ncopies
                             row['copy_ms_each'] = round(cms, 4)
                             # both windows on one clock: the kernels must sit
@@ -126,12 +144,16 @@ def main():
         summ.setdefault((r['kernel'], r['concurrent_copy'], r['xcd_mask']), []).append(r['kernel_ms'])
     out = []
     for kname in kernels:
-        for copy_on in (False, True):
+        for copy_on in kinds:
             off = sorted(summ[(kname, copy_on, 0)])
             on = sorted(summ[(kname, copy_on, 0x88)])
             mo, mn = off[len(off) // 2], on[len(on) // 2]
+            cps = [r['copy_ms_each'] for r in res['rows']
+                   if r['kernel'] == kname and r['concurrent_copy'] == copy_on and 'copy_ms_each' in r]
             out.append(dict(kernel=kname, concurrent_copy=copy_on, policy_off_ms=mo,
-                            policy_0x88_ms=mn, gain=round(mo / mn - 1, 4)))
+                            policy_0x88_ms=mn, gain=round(mo / mn - 1, 4),
+                            copy_GBs_during=round(2 * n * 4 / (sorted(cps)[len(cps) // 2] * 1e-3)
+                                                  / 1e9, 1) if cps else None))
     res['summary'] = out
     print(json.dumps(res), flush=True)
 
