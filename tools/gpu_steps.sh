@@ -37,6 +37,10 @@ for step in "$@"; do
         swing) run swing_default 300 python3 tools/pageable_swing.py --label default || exit $?
                run swing_gpuaff 300 env MPIX_REDOP_PAGEABLE_AFFINITY=gpu python3 \
                    tools/pageable_swing.py --label gpu_affinity || exit $? ;;
+        swingchunk) run swing_c16 300 python3 tools/pageable_swing.py --label chunk16 --chunk 16 \
+                        --sizes 32,48,64,128 || exit $?
+                    run swing_c8 300 python3 tools/pageable_swing.py --label chunk8 --chunk 8 \
+                        --sizes 16,24,32,64 || exit $? ;;
         floor) run floor 200 python3 tools/call_floor.py || exit $? ;;
         policy) run policy 300 python3 tools/policy_concurrent.py || exit $? ;;
         bench) run bench 600 python3 bench.py || exit $? ;;
