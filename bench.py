@@ -184,12 +184,14 @@ def sync_call_latency(B, dev, counts=(1, 4096, 1 << 20), reps=2000):
     return out
 
 
-CROSSOVER_BYTES = (4 << 10, 16 << 10, 64 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20,
-                   64 << 20, 256 << 20, 1 << 30)
+CROSSOVER_BYTES = (4 << 10, 16 << 10, 64 << 10, 256 << 10, 1 << 20, 4 << 20, 8 << 20, 16 << 20,
+                   64 << 20, 128 << 20, 256 << 20, 512 << 20, 1 << 30)
 
 
 def _reps_for(nbytes):
-    return max(3, min(2000, (256 << 20) // max(nbytes, 1)))
+    """calls per crossover point (median): at least 7, so one call that a
+    busy host stalls cannot set the median (profiles/r04_pageable_swing.json)"""
+    return max(7, min(2000, (256 << 20) // max(nbytes, 1)))
 
 
 def host_crossover_gpu(B):

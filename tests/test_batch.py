@@ -110,9 +110,21 @@ def test_batch_matches_oracle_and_single_calls(R, oracle, dtname, opname, odd, k
     assert rc == 0
     s.synchronize()
     got = d.cpu().numpy()
+
+    def same(x, y):
+        # fp16 results compare NaN-equivalent: the odd offsets cut random bit
+        # patterns, and fp16 NaN payloads differ between gfx950 and the x86
+        # loop when both operands are NaN
+        if dtname != 'MPIX_C_FLOAT16' or np.array_equal(x, y):
+            return np.array_equal(x, y)
+        fx, fy = x.view(np.float16), y.view(np.float16)
+        return bool(np.all((x.view(np.uint16) == y.view(np.uint16)) | (np.isnan(fx) & np.isnan(fy))))
     for q, (i_off, o_off, c) in enumerate(trip):
-        assert np.array_equal(got[o_off:o_off + c * ext], want[o_off:o_off + c * ext]), (q, c)
-    assert np.array_equal(got, want)            # nothing outside the targets moved
+        assert same(got[o_off:o_off + c * ext], want[o_off:o_off + c * ext]), (q, c)
+    outside = np.ones(len(got), bool)
+    for _, o_off, c in trip:
+        outside[o_off:o_off + c * ext] = False
+    assert np.array_equal(got[outside], want[outside])      # nothing outside the targets moved
     # the same triples as separate stream-ordered calls: identical bits
     d2 = torch.from_numpy(pool.copy()).cuda()
     torch.cuda.synchronize()
@@ -120,7 +132,7 @@ def test_batch_matches_oracle_and_single_calls(R, oracle, dtname, opname, odd, k
     for i_off, o_off, c in trip:
         assert R.reduce_local_async(b2 + i_off, b2 + o_off, c, dt, op, s) == 0
     s.synchronize()
-    assert np.array_equal(d2.cpu().numpy(), got)
+    assert np.array_equal(d2.cpu().numpy(), got)            # bit for bit, NaNs included
 
 
 @pytest.mark.gpu
