@@ -29,13 +29,26 @@ const Entry *cplx_half_ops(int opi)
 }
 
 // MPI_LONG_DOUBLE (x87 in 16 bytes) and MPI_REAL16 (binary128): MAX / MIN
-// only -- compare and select (redop_ops.h); SUM / PROD stay with the caller's
-// CPU op table (MPIX_Redop_is_supported answers 0 for them)
-template <class Max, class Min>
-const Entry *select_ops(int opi)
+// compare and select in integer arithmetic (redop_ops.h), SUM / PROD in
+// software extended / quad arithmetic (redop_soft.h)
+template <class Max, class Min, class Sum, class Prod>
+const Entry *soft_ops(int opi)
 {
-    static const Entry tab[2] = { entry<Max>(), entry<Min>() };
-    return (opi == 1 || opi == 2) ? &tab[opi - 1] : nullptr;
+    static const Entry tab[4] = { entry<Max>(), entry<Min>(), entry<Sum>(), entry<Prod>() };
+    return (opi >= 1 && opi <= 4) ? &tab[opi - 1] : nullptr;
+}
+
+// their complex forms: binary128 struct complex SUM / PROD, x87 C complex SUM / PROD
+const Entry *quadc_ops(int opi)
+{
+    static const Entry tab[2] = { entry<QuadCSum>(), entry<QuadCProd>() };
+    return (opi == 3 || opi == 4) ? &tab[opi - 3] : nullptr;
+}
+
+const Entry *x87c_ops(int opi)
+{
+    static const Entry tab[2] = { entry<X87CSum>(), entry<X87CProd>() };
+    return (opi == 3 || opi == 4) ? &tab[opi - 3] : nullptr;
 }
 
 const Entry *bf16_ops(int opi)
@@ -56,8 +69,10 @@ const Entry *lookup_fp(int raw, int opi)
         case 0x4c840800u: return cplx_ops<float>(opi);
         case 0x4c841000u: return cplx_ops<double>(opi);
         case 0x4c850200u: return bf16_ops(opi);
-        case 0x4c851000u: return select_ops<X87Max, X87Min>(opi);
-        case 0x4c831000u: return select_ops<QuadMax, QuadMin>(opi);
+        case 0x4c851000u: return soft_ops<X87Max, X87Min, X87Sum, X87Prod>(opi);
+        case 0x4c831000u: return soft_ops<QuadMax, QuadMin, QuadSum, QuadProd>(opi);
+        case 0x4c842000u: return quadc_ops(opi);
+        case 0x4c862000u: return x87c_ops(opi);
         default: return nullptr;
     }
 }

@@ -17,6 +17,7 @@
 #include <stdint.h>
 
 #include "redop_dispatch.h"
+#include "redop_soft.h"     // X87 / Quad units and their SUM / PROD
 
 namespace mpix {
 
@@ -346,11 +347,6 @@ template <typename P, bool IsMax> struct Loc {
 // value (both are m * 2^(1 - 16383 - 63)); zeros of either sign are equal.
 enum { kCmpLt = 0, kCmpEq = 1, kCmpGt = 2, kCmpUn = 3 };
 
-struct alignas(16) X87 {
-    uint64_t m;     // significand, J = bit 63
-    uint64_t se;    // bits 0-14 exponent, bit 15 sign, bits 16-63 padding
-};
-
 MPIX_DEV int sign_mag_cmp(bool sa, bool sb, int mag, bool both_zero)
 {
     if (both_zero)
@@ -398,10 +394,6 @@ struct X87Min {
     {
         return x87_cmp(a, b) == kCmpLt ? a : x87_store(a, b);
     }
-};
-
-struct alignas(16) Quad {
-    uint64_t lo, hi;    // hi: sign, 15-bit exponent, top 48 fraction bits
 };
 
 MPIX_DEV int quad_cmp(const Quad &a, const Quad &b)

@@ -1,0 +1,493 @@
+// redop_soft.h -- x87 extended and IEEE binary128 SUM / PROD in integer
+// arithmetic on gfx950 (no hardware for either format).
+//
+// MPI_LONG_DOUBLE on x86-64 is the x87 80-bit format in a 16-byte slot
+// (MPIR_ALT_FLOAT128, mpir_datatype.h:82); MPI_REAL16 is binary128
+// (MPIR_FLOAT128).  op_fns.c's `a[i] = a[i] + b[i]` / `a[i] * b[i]` on them
+// is, as gcc builds MPICH on x86-64: fldt a; fldt b; faddp / fmulp; fstpt a
+// (x87, precision control extended, round to nearest even) and
+// __addtf3(a, b) / __multf3(a, b) (libgcc soft-fp, round to nearest even).
+// Restated here bit for bit, checked against the oracle's gcc-built loops
+// (tests/test_soft_fp_gpu.py):
+//   * x87: an operand in an unsupported encoding (exponent != 0 with the
+//     explicit integer bit J clear: unnormals, pseudo-infinities, pseudo-
+//     NaNs) makes the result the "real indefinite" QNaN (sign 1, exponent
+//     0x7fff, significand 0xC000...), NaN operands or not; of two NaNs the
+//     one with the larger significand (a QNaN's is always the larger), on a
+//     tie the positive one; a NaN result is quieted (bit 62); inf - inf and
+//     0 * inf are the indefinite too.  Pseudo-denormals (exponent 0, J set)
+//     are operands of exponent 1; results are normalised, denormal results
+//     denormalised then rounded; `fstpt` stores 10 bytes, so the slot's
+//     padding keeps inout's.
+//   * binary128 (libgcc/config/i386/sfp-machine.h _FP_CHOOSENAN): of two
+//     NaNs the larger fraction, on a tie the first operand (inout) for + and
+//     *, the second for -; quieted; invalid results are the default NaN
+//     (sign 1, quiet bit only).
+// Both: exact result, then one rounding (RNE, gradual underflow).  These
+// combiners are not on any hot path: each element costs ~100 VALU, still
+// far under the HBM time of its 48 bytes at 8 TB/s per CU share.
+#pragma once
+
+#include <stdint.h>
+
+#include "redop_dispatch.h"
+
+// MPIX_SOFT_HOST: the same functions as plain host C++, for the CPU test that
+// checks them against the oracle on millions of pairs without a GPU
+// (tests/c/soft_check.cpp, tests/test_soft_fp.py)
+#ifdef MPIX_SOFT_HOST
+#define MPIX_SDEV inline
+#else
+#include <hip/hip_runtime.h>
+#define MPIX_SDEV __device__ __forceinline__
+#endif
+
+namespace mpix {
+
+typedef unsigned __int128 u128;
+
+// x87 extended in a 16-byte slot
+struct alignas(16) X87 {
+    uint64_t m;     // significand, J = bit 63
+    uint64_t se;    // bits 0-14 exponent, bit 15 sign, bits 16-63 padding
+};
+
+// IEEE binary128
+struct alignas(16) Quad {
+    uint64_t lo, hi;    // hi: sign, 15-bit exponent, top 48 fraction bits
+};
+
+// result classes (x87_class / quad_class); the compare-and-select combiners
+// of redop_ops.h use kCmp* instead
+enum SoftClass { kX87Bad = 0, kX87Nan, kX87Inf, kX87Zero, kX87Fin };
+
+MPIX_SDEV int clz128(u128 x)
+{
+    const uint64_t hi = (uint64_t) (x >> 64), lo = (uint64_t) x;
+    return hi ? __builtin_clzll(hi) : 64 + (lo ? __builtin_clzll(lo) : 64);
+}
+
+// Round the exact value S * 2^(E0 - 16383 - 126) (S != 0) to a significand of
+// `bits` bits (64 for x87 with its explicit J bit, 113 for binary128 with the
+// implicit one), round to nearest even, gradual underflow.  Out: *m the
+// significand (leading bit at bits - 1 for a normal), *e the biased exponent
+// (0: denormal or zero; 0x7fff: overflow to infinity, *m = the leading bit).
+MPIX_SDEV void round_exact(u128 S, int64_t E0, int bits, u128 *m, int64_t *e)
+{
+    const int p = 127 - clz128(S);      // leading one of S
+    int64_t E = E0 + p - 126;
+    int64_t sh = p - (bits - 1);        // bits of S below the significand
+    if (E < 1) {                        // denormal: the scale of exponent 1
+        sh += 1 - E;
+        E = 0;
+    }
+    u128 r;
+    if (sh <= 0) {
+        r = S << (int) (-sh);
+    } else if (sh > 128) {
+        r = 0;                          // below half of the smallest denormal
+    } else if (sh == 128) {
+        const u128 half = (u128) 1 << 127;
+        r = S > half ? 1 : 0;           // a tie rounds to the even 0
+    } else {
+        r = S >> (int) sh;
+        const u128 rest = S & (((u128) 1 << (int) sh) - 1);
+        const u128 half = (u128) 1 << (int) (sh - 1);
+        if (rest > half || (rest == half && (r & 1)))
+            r += 1;
+    }
+    const u128 lead = (u128) 1 << (bits - 1);
+    if (r >> bits) {                    // rounding carried out of the significand
+        r >>= 1;
+        E += 1;
+    }
+    if (E == 0 && (r & lead))           // a denormal rounded up into the normals
+        E = 1;
+    if (E >= 0x7fff) {
+        r = lead;
+        E = 0x7fff;
+    }
+    *m = r;
+    *e = E;
+}
+
+// ---------------------------------------------------------------- x87
+
+MPIX_SDEV int x87_class(uint64_t m, uint32_t e)
+{
+    const bool j = (m >> 63) != 0;
+    if (e != 0 && !j)
+        return kX87Bad;                 // unnormal, pseudo-infinity, pseudo-NaN
+    if (e == 0x7fff)
+        return (m << 1) ? kX87Nan : kX87Inf;
+    if (e == 0 && m == 0)
+        return kX87Zero;
+    return kX87Fin;                     // normal, denormal, pseudo-denormal
+}
+
+// the 10 value bytes of a result, the slot's padding taken from `pad`
+MPIX_SDEV X87 x87_make(const X87 &pad, bool s, uint32_t e, uint64_t m)
+{
+    X87 r;
+    r.m = m;
+    r.se = (pad.se & ~(uint64_t) 0xffff) | ((uint64_t) s << 15) | e;
+    return r;
+}
+
+MPIX_SDEV X87 x87_indefinite(const X87 &pad)
+{
+    return x87_make(pad, true, 0x7fff, 0xC000000000000000ull);
+}
+
+// NaN result of a, b (at least one a NaN, neither unsupported)
+MPIX_SDEV X87 x87_nan(const X87 &a, bool a_nan, const X87 &b, bool b_nan)
+{
+    const bool sa = (a.se >> 15) & 1, sb = (b.se >> 15) & 1;
+    bool pick_a;
+    if (a_nan && b_nan)
+        pick_a = a.m != b.m ? a.m > b.m : !sa;
+    else
+        pick_a = a_nan;
+    const X87 &n = pick_a ? a : b;
+    return x87_make(a, pick_a ? sa : sb, 0x7fff, n.m | (1ull << 62));
+}
+
+MPIX_SDEV X87 x87_from_round(const X87 &pad, bool s, u128 S, int64_t E0)
+{
+    u128 m;
+    int64_t e;
+    round_exact(S, E0, 64, &m, &e);
+    return x87_make(pad, s, (uint32_t) e, (uint64_t) m);
+}
+
+// a + b (sub: a - b), as fldt a; fldt b; faddp (fsubp); the result keeps a's padding
+MPIX_SDEV X87 x87_add(const X87 &a, const X87 &b, bool sub)
+{
+    const uint32_t ea = (uint32_t) a.se & 0x7fff, eb = (uint32_t) b.se & 0x7fff;
+    const int ca = x87_class(a.m, ea), cb = x87_class(b.m, eb);
+    if (ca == kX87Bad || cb == kX87Bad)
+        return x87_indefinite(a);
+    if (ca == kX87Nan || cb == kX87Nan)
+        return x87_nan(a, ca == kX87Nan, b, cb == kX87Nan);
+    bool sa = (a.se >> 15) & 1, sb = ((b.se >> 15) & 1) ^ (sub ? 1 : 0);
+    if (ca == kX87Inf || cb == kX87Inf) {
+        if (ca == kX87Inf && cb == kX87Inf && sa != sb)
+            return x87_indefinite(a);
+        return x87_make(a, ca == kX87Inf ? sa : sb, 0x7fff, 1ull << 63);
+    }
+    if (ca == kX87Zero && cb == kX87Zero)
+        return x87_make(a, sa && sb, 0, 0);
+    uint64_t ma = a.m, mb = b.m;
+    int64_t xa = ea ? ea : 1, xb = eb ? eb : 1;
+    if (xa < xb || (xa == xb && ma < mb)) {     // |a| >= |b|
+        uint64_t t = ma; ma = mb; mb = t;
+        int64_t u = xa; xa = xb; xb = u;
+        bool v = sa; sa = sb; sb = v;
+    }
+    const u128 A = (u128) ma << 63;
+    const int64_t d = xa - xb;
+    u128 B = 0;
+    if (d < 128) {
+        const u128 full = (u128) mb << 63;
+        B = full >> (int) d;
+        if (d > 0 && (full & (((u128) 1 << (int) d) - 1)))
+            B |= 1;                     // sticky
+    } else if (mb) {
+        B = 1;
+    }
+    const u128 S = sa == sb ? A + B : A - B;
+    if (S == 0)
+        return x87_make(a, false, 0, 0);        // exact cancellation: +0
+    return x87_from_round(a, sa, S, xa);
+}
+
+MPIX_SDEV X87 x87_mul(const X87 &a, const X87 &b)
+{
+    const uint32_t ea = (uint32_t) a.se & 0x7fff, eb = (uint32_t) b.se & 0x7fff;
+    const int ca = x87_class(a.m, ea), cb = x87_class(b.m, eb);
+    if (ca == kX87Bad || cb == kX87Bad)
+        return x87_indefinite(a);
+    if (ca == kX87Nan || cb == kX87Nan)
+        return x87_nan(a, ca == kX87Nan, b, cb == kX87Nan);
+    const bool s = ((a.se ^ b.se) >> 15) & 1;
+    if (ca == kX87Inf || cb == kX87Inf) {
+        if (ca == kX87Zero || cb == kX87Zero)
+            return x87_indefinite(a);
+        return x87_make(a, s, 0x7fff, 1ull << 63);
+    }
+    if (ca == kX87Zero || cb == kX87Zero)
+        return x87_make(a, s, 0, 0);
+    const int64_t xa = ea ? ea : 1, xb = eb ? eb : 1;
+    // value = ma * mb * 2^(xa + xb - 2*16383 - 126) = S * 2^(E0 - 16383 - 126)
+    return x87_from_round(a, s, (u128) a.m * b.m, xa + xb - 16383);
+}
+
+struct X87Sum {
+    using unit = X87;
+    static MPIX_SDEV X87 apply(X87 a, X87 b, const Params &) { return x87_add(a, b, false); }
+};
+struct X87Prod {
+    using unit = X87;
+    static MPIX_SDEV X87 apply(X87 a, X87 b, const Params &) { return x87_mul(a, b); }
+};
+
+// ----------------------------------------------------------- binary128
+MPIX_SDEV int quad_class(const Quad &q)
+{
+    const uint32_t e = (uint32_t) (q.hi >> 48) & 0x7fff;
+    const uint64_t fh = q.hi & 0xffffffffffffull;
+    if (e == 0x7fff)
+        return (fh | q.lo) ? kX87Nan : kX87Inf;
+    if (e == 0 && !(fh | q.lo))
+        return kX87Zero;
+    return kX87Fin;
+}
+
+MPIX_SDEV Quad quad_make(bool s, uint32_t e, u128 frac)
+{
+    Quad r;
+    r.lo = (uint64_t) frac;
+    r.hi = ((uint64_t) s << 63) | ((uint64_t) e << 48) | ((uint64_t) (frac >> 64) & 0xffffffffffffull);
+    return r;
+}
+
+// _FP_CHOOSENAN (i386): the larger fraction; a tie goes to x for + and *
+// (x_on_tie), to y for -; the result quieted
+MPIX_SDEV Quad quad_nan(const Quad &x, bool x_nan, const Quad &y, bool y_nan, bool x_on_tie)
+{
+    const u128 fx = ((u128) (x.hi & 0xffffffffffffull) << 64) | x.lo;
+    const u128 fy = ((u128) (y.hi & 0xffffffffffffull) << 64) | y.lo;
+    bool pick_x;
+    if (x_nan && y_nan)
+        pick_x = fx != fy ? fx > fy : x_on_tie;
+    else
+        pick_x = x_nan;
+    const Quad &n = pick_x ? x : y;
+    Quad r = n;
+    r.hi |= 1ull << 47;
+    return r;
+}
+
+MPIX_SDEV Quad quad_default_nan() { return quad_make(true, 0x7fff, (u128) 1 << 111); }
+
+MPIX_SDEV void quad_parts(const Quad &q, bool *s, int64_t *x, u128 *m)
+{
+    const uint32_t e = (uint32_t) (q.hi >> 48) & 0x7fff;
+    *s = q.hi >> 63;
+    *x = e ? e : 1;
+    *m = ((u128) (q.hi & 0xffffffffffffull) << 64) | q.lo;
+    if (e)
+        *m |= (u128) 1 << 112;
+}
+
+MPIX_SDEV Quad quad_from_round(bool s, u128 S, int64_t E0)
+{
+    u128 m;
+    int64_t e;
+    round_exact(S, E0, 113, &m, &e);
+    return quad_make(s, (uint32_t) e, m & (((u128) 1 << 112) - 1));
+}
+
+// x + y (sub: x - y): __addtf3 / __subtf3
+MPIX_SDEV Quad quad_add(const Quad &x, const Quad &y, bool sub)
+{
+    const int cx = quad_class(x), cy = quad_class(y);
+    if (cx == kX87Nan || cy == kX87Nan)
+        return quad_nan(x, cx == kX87Nan, y, cy == kX87Nan, !sub);
+    bool sa, sb;
+    int64_t xa, xb;
+    u128 ma, mb;
+    quad_parts(x, &sa, &xa, &ma);
+    quad_parts(y, &sb, &xb, &mb);
+    sb ^= sub;
+    if (cx == kX87Inf || cy == kX87Inf) {
+        if (cx == kX87Inf && cy == kX87Inf && sa != sb)
+            return quad_default_nan();
+        return quad_make(cx == kX87Inf ? sa : sb, 0x7fff, 0);
+    }
+    if (cx == kX87Zero && cy == kX87Zero)
+        return quad_make(sa && sb, 0, 0);
+    if (xa < xb || (xa == xb && ma < mb)) {
+        u128 t = ma; ma = mb; mb = t;
+        int64_t u = xa; xa = xb; xb = u;
+        bool v = sa; sa = sb; sb = v;
+    }
+    const u128 A = ma << 14;            // leading bit at 126, 14 guard bits
+    const int64_t d = xa - xb;
+    u128 B = 0;
+    if (d < 128) {
+        const u128 full = mb << 14;
+        B = full >> (int) d;
+        if (d > 0 && (full & (((u128) 1 << (int) d) - 1)))
+            B |= 1;
+    } else if (mb) {
+        B = 1;
+    }
+    const u128 S = sa == sb ? A + B : A - B;
+    if (S == 0)
+        return quad_make(false, 0, 0);
+    return quad_from_round(sa, S, xa);
+}
+
+// x * y: __multf3 (the 226-bit product folded to 128 bits plus a sticky bit)
+MPIX_SDEV Quad quad_mul(const Quad &x, const Quad &y)
+{
+    const int cx = quad_class(x), cy = quad_class(y);
+    if (cx == kX87Nan || cy == kX87Nan)
+        return quad_nan(x, cx == kX87Nan, y, cy == kX87Nan, true);
+    bool sa, sb;
+    int64_t xa, xb;
+    u128 ma, mb;
+    quad_parts(x, &sa, &xa, &ma);
+    quad_parts(y, &sb, &xb, &mb);
+    const bool s = sa ^ sb;
+    if (cx == kX87Inf || cy == kX87Inf) {
+        if (cx == kX87Zero || cy == kX87Zero)
+            return quad_default_nan();
+        return quad_make(s, 0x7fff, 0);
+    }
+    if (cx == kX87Zero || cy == kX87Zero)
+        return quad_make(s, 0, 0);
+    // 256-bit product of two 113-bit significands, limbs of 64 bits
+    const uint64_t a0 = (uint64_t) ma, a1 = (uint64_t) (ma >> 64);
+    const uint64_t b0 = (uint64_t) mb, b1 = (uint64_t) (mb >> 64);
+    const u128 p00 = (u128) a0 * b0, p01 = (u128) a0 * b1, p10 = (u128) a1 * b0;
+    const u128 p11 = (u128) a1 * b1;
+    const u128 mid = p01 + p10;         // a1, b1 < 2^49: no carry out
+    u128 lo = p00 + (mid << 64);
+    u128 hi = p11 + (mid >> 64) + (lo < p00 ? 1 : 0);
+    // normalise: the leading one to bit 254 of (hi, lo), then fold
+    const int lead = hi ? 255 - clz128(hi) : 127 - clz128(lo);
+    const int k = 254 - lead;           // left shift, >= 0 (a product < 2^226)
+    if (k >= 128) {
+        hi = lo << (k - 128);
+        lo = 0;
+    } else if (k > 0) {
+        hi = (hi << k) | (lo >> (128 - k));
+        lo <<= k;
+    }
+    const u128 S = hi | (lo ? 1 : 0);
+    // value = product * 2^(xa + xb - 2*16383 - 224), product = S * 2^(lead - 126)
+    return quad_from_round(s, S, lead + xa + xb - 16383 - 224);
+}
+
+struct QuadSum {
+    using unit = Quad;
+    static MPIX_SDEV Quad apply(Quad a, Quad b, const Params &) { return quad_add(a, b, false); }
+};
+struct QuadProd {
+    using unit = Quad;
+    static MPIX_SDEV Quad apply(Quad a, Quad b, const Params &) { return quad_mul(a, b); }
+};
+
+// ------------------------------------------------------------ complex
+// MPI_COMPLEX32 (MPIR_COMPLEX128): Fortran struct complex of binary128 parts,
+// MPIR_OP_TYPE_GROUP(COMPLEX) (op_fns.c:26-42 component sums; :74-85
+// re = c.re*b.re - c.im*b.im, im = c.im*b.re + c.re*b.im, each op soft-fp
+// rounded).  MPI_C_LONG_DOUBLE_COMPLEX (MPIR_ALT_COMPLEX128): component
+// sums of x87 parts, and the C99 product below.  32-byte units.
+struct alignas(16) QuadC {
+    Quad re, im;
+};
+struct QuadCSum {
+    using unit = QuadC;
+    static MPIX_SDEV QuadC apply(QuadC a, QuadC b, const Params &)
+    {
+        QuadC r;
+        r.re = quad_add(a.re, b.re, false);
+        r.im = quad_add(a.im, b.im, false);
+        return r;
+    }
+};
+struct QuadCProd {
+    using unit = QuadC;
+    static MPIX_SDEV QuadC apply(QuadC c, QuadC b, const Params &)
+    {
+        QuadC r;
+        r.re = quad_add(quad_mul(c.re, b.re), quad_mul(c.im, b.im), true);
+        r.im = quad_add(quad_mul(c.im, b.re), quad_mul(c.re, b.im), false);
+        return r;
+    }
+};
+struct alignas(16) X87C {
+    X87 re, im;
+};
+
+// C `long double _Complex` product = libgcc's __mulxc3(a, b, c, d) (x = a+ib
+// inout, y = c+id in): four x87 products, x = ac - bd, y = ad + bc, and when
+// both come out NaN the C99 Annex G recovery of infinities (libgcc2.c), every
+// operation an x87 one.  isnan is an unordered self-compare (true for NaNs
+// and the unsupported encodings), isinf true for the infinity encoding only,
+// copysign a sign-bit copy.
+MPIX_SDEV bool x87_isnan(const X87 &v)
+{
+    const int c = x87_class(v.m, (uint32_t) v.se & 0x7fff);
+    return c == kX87Nan || c == kX87Bad;
+}
+MPIX_SDEV bool x87_isinf(const X87 &v) { return x87_class(v.m, (uint32_t) v.se & 0x7fff) == kX87Inf; }
+MPIX_SDEV X87 x87_signed(bool one, const X87 &sgn)      // copysign(one ? 1 : 0, sgn)
+{
+    X87 r;
+    r.m = one ? 1ull << 63 : 0;
+    r.se = (sgn.se & 0x8000) | (one ? 0x3fff : 0);
+    return r;
+}
+
+struct X87CProd {
+    using unit = X87C;
+    static MPIX_SDEV X87C apply(X87C x, X87C y, const Params &)
+    {
+        X87 a = x.re, b = x.im, c = y.re, d = y.im;
+        const X87 ac = x87_mul(a, c), bd = x87_mul(b, d), ad = x87_mul(a, d), bc = x87_mul(b, c);
+        X87 re = x87_add(ac, bd, true), im = x87_add(ad, bc, false);
+        if (x87_isnan(re) && x87_isnan(im)) {
+            bool recalc = false;
+            if (x87_isinf(a) || x87_isinf(b)) {
+                a = x87_signed(x87_isinf(a), a);
+                b = x87_signed(x87_isinf(b), b);
+                if (x87_isnan(c)) c = x87_signed(false, c);
+                if (x87_isnan(d)) d = x87_signed(false, d);
+                recalc = true;
+            }
+            if (x87_isinf(c) || x87_isinf(d)) {
+                c = x87_signed(x87_isinf(c), c);
+                d = x87_signed(x87_isinf(d), d);
+                if (x87_isnan(a)) a = x87_signed(false, a);
+                if (x87_isnan(b)) b = x87_signed(false, b);
+                recalc = true;
+            }
+            if (!recalc && (x87_isinf(ac) || x87_isinf(bd) || x87_isinf(ad) || x87_isinf(bc))) {
+                if (x87_isnan(a)) a = x87_signed(false, a);
+                if (x87_isnan(b)) b = x87_signed(false, b);
+                if (x87_isnan(c)) c = x87_signed(false, c);
+                if (x87_isnan(d)) d = x87_signed(false, d);
+                recalc = true;
+            }
+            if (recalc) {
+                X87 inf;
+                inf.m = 1ull << 63;
+                inf.se = 0x7fff;
+                re = x87_mul(inf, x87_add(x87_mul(a, c), x87_mul(b, d), true));
+                im = x87_mul(inf, x87_add(x87_mul(a, d), x87_mul(b, c), false));
+            }
+        }
+        X87C r;     // stored with fstpt: each part keeps inout's padding
+        r.re = x87_make(x.re, (re.se >> 15) & 1, (uint32_t) re.se & 0x7fff, re.m);
+        r.im = x87_make(x.im, (im.se >> 15) & 1, (uint32_t) im.se & 0x7fff, im.m);
+        return r;
+    }
+};
+struct X87CSum {
+    using unit = X87C;
+    static MPIX_SDEV X87C apply(X87C a, X87C b, const Params &)
+    {
+        X87C r;
+        r.re = x87_add(a.re, b.re, false);
+        r.im = x87_add(a.im, b.im, false);
+        return r;
+    }
+};
+
+#undef MPIX_SDEV
+
+}  // namespace mpix

@@ -441,7 +441,7 @@ def test_errors_on_gpu(R, H):
     y = torch.zeros(1 << 16, device='cuda')
     assert R.MPI_Reduce_local(x, x, 1024, H.MPI_FLOAT, H.MPI_SUM) == H.MPI_ERR_BUFFER
     assert R.MPI_Reduce_local(-1, y, 1024, H.MPI_FLOAT, H.MPI_SUM) == H.MPI_ERR_BUFFER
-    assert R.MPI_Reduce_local(x, y, 1024, H.MPI_LONG_DOUBLE, H.MPI_SUM) == H.MPI_ERR_TYPE
+    assert R.MPI_Reduce_local(x, y, 1024, H.MPIX_BFLOAT16, H.MPI_MIN) == H.MPI_ERR_TYPE
     assert R.MPI_Reduce_local(x, y, 1024, H.MPIX_BFLOAT16, H.MPI_MAX) == H.MPI_ERR_TYPE
     assert R.MPI_Reduce_local(x, y, 10, H.MPI_FLOAT, H.MPI_LXOR) == H.MPI_ERR_OP
     assert R.MPI_Reduce_local(x, y, 0, H.MPI_FLOAT, H.MPI_SUM) == H.MPI_SUCCESS

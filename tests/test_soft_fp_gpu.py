@@ -1,0 +1,101 @@
+"""x87 extended and IEEE binary128 SUM / PROD (and their complex forms) on
+gfx950 (mpich_amd/csrc/redop_soft.h) against the oracle's gcc-built loops,
+every byte compared (padding included): the specials tables and random
+values of tests/test_soft_fp.py (which checks the same code built for the
+host on millions of pairs), here through the synchronous kernel path, the
+stream-ordered one, the multi-input fold and a host (pageable) operand.
+Reference: op_fns.c:19-91 over mpir_op_util.h:211-236."""
+import numpy as np
+import pytest
+import torch
+
+from tests import test_soft_fp as S
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def R():
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    from mpich_amd import redop
+    assert redop.lib().MPIX_Redop_init() == 0
+    return redop
+
+
+def dev(a):
+    t = torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1).copy()).cuda()
+    torch.cuda.synchronize()
+    return t
+
+
+def _gpu_vs_oracle(R, oracle, dt, op, a, b, ext):
+    n = len(a.reshape(-1)) // ext
+    want = a.reshape(-1).copy()
+    assert oracle.reduce_local(b.reshape(-1).copy(), want, n, dt, op) == 0
+    da, db = dev(a), dev(b)
+    assert R.MPI_Reduce_local(db, da, n, dt, op) == 0
+    got = da.cpu().numpy()
+    bad = np.flatnonzero((got.reshape(n, ext) != want.reshape(n, ext)).any(1))
+    assert bad.size == 0, ('%d of %d differ' % (bad.size, n), bad[:4])
+    return want
+
+
+CASES = [('x87 SUM', S.LD, S.MPI_SUM), ('x87 PROD', S.LD, S.MPI_PROD),
+         ('quad SUM', S.REAL16, S.MPI_SUM), ('quad PROD', S.REAL16, S.MPI_PROD)]
+
+
+@pytest.mark.parametrize('name,dt,op', CASES, ids=[c[0] for c in CASES])
+def test_specials_and_random(R, oracle, name, dt, op):
+    rng = np.random.default_rng(0x5EED0900 + op + dt)
+    if name.startswith('x87'):
+        a, b = S.all_pairs(S.x87_specials(), rng, 10)
+        ra, rb = S.x87_random(rng, 300000, True), S.x87_random(rng, 300000, False)
+    else:
+        a, b = S.all_pairs(S.quad_specials(), rng, 16)
+        ra, rb = S.quad_random(rng, 300000, tiny=True), S.quad_random(rng, 300000, close=True)
+    _gpu_vs_oracle(R, oracle, dt, op, a, b, 16)
+    _gpu_vs_oracle(R, oracle, dt, op, ra, rb, 16)
+
+
+@pytest.mark.parametrize('dt,op', [(S.COMPLEX32, S.MPI_SUM), (S.COMPLEX32, S.MPI_PROD),
+                                   (S.C_LD_COMPLEX, S.MPI_SUM), (S.C_LD_COMPLEX, S.MPI_PROD)])
+def test_complex(R, oracle, dt, op):
+    rng = np.random.default_rng(0x5EED0910 + op + dt)
+    n = 100000
+    x87 = dt == S.C_LD_COMPLEX
+    gen = (lambda: S.x87_random(rng, n, True)) if x87 else (lambda: S.quad_random(rng, n, True))
+    sp = np.stack(S.x87_specials() if x87 else S.quad_specials())
+    parts = [gen() for _ in range(4)]
+    for p in parts:
+        p[::9] = sp[rng.integers(0, len(sp), len(p[::9]))]
+    a = np.concatenate(parts[:2], axis=1)
+    b = np.concatenate(parts[2:], axis=1)
+    _gpu_vs_oracle(R, oracle, dt, op, a, b, 32)
+
+
+def test_entry_points(R, oracle):
+    """x87 SUM (16-byte packets) through the stream-ordered call, a 3-input
+    fold in one pass, and a pageable host inout"""
+    rng = np.random.default_rng(0x5EED0920)
+    n = 50001
+    a = S.x87_random(rng, n, True)
+    bs = [S.x87_random(rng, n, True) for _ in range(3)]
+
+    def orc(b, inout):
+        assert oracle.reduce_local(b.reshape(-1).copy(), inout.reshape(-1), n, S.LD, S.MPI_SUM) == 0
+        return inout
+    da = dev(a)
+    assert R.reduce_local_async(dev(bs[0]), da, n, S.LD, S.MPI_SUM) == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(da.cpu().numpy().reshape(n, 16), orc(bs[0], a.copy()))
+    want = a.copy()
+    for b in bs:
+        orc(b, want)
+    da = dev(a)
+    R.check(R.reduce_local_multi_async([dev(b) for b in bs], da, n, S.LD, S.MPI_SUM))
+    torch.cuda.synchronize()
+    assert np.array_equal(da.cpu().numpy().reshape(n, 16), want)
+    h = a.copy()
+    assert R.MPI_Reduce_local(bs[0].copy(), h, n, S.LD, S.MPI_SUM) == 0
+    assert np.array_equal(h, orc(bs[0], a.copy()))

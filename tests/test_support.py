@@ -6,7 +6,8 @@ at the boundary (no GPU compute calls):
     MPIX_REDOP_THRESHOLD declines count > 0 whose packed size exceeds it;
   * MPIX_Redop_is_supported_buffers declines host-resident operands below the
     floor of their memory kind (here: pageable numpy buffers);
-  * an MPIX_Op_table entry on a type no kernel covers (MPI_LONG_DOUBLE)
+  * an MPIX_Op_table entry on a pair no kernel covers (MAX on MPIX_BFLOAT16,
+    which the reference's MPIR_MAXF asserts on too)
     aborts like op_fns.c:51-53's MPIR_Assert(0), or only records the error
     with MPIX_REDOP_OPFN_ABORT=0;
   * libmpix_coll declines such a type on every rank before any exchange, and
@@ -84,7 +85,7 @@ def test_buffer_predicate_host_floor(knobs, H):
     R.check(R.set_support(enable=True, threshold_bytes=-1, host_floor_bytes=0))
     assert R.is_supported_buffers(H.MPI_SUM, H.MPI_FLOAT, 1, a, b)
     # unsupported pairs stay unsupported whatever the buffers
-    assert not R.is_supported_buffers(H.MPI_SUM, H.MPI_LONG_DOUBLE, 16, a, b)
+    assert not R.is_supported_buffers(H.MPI_MAX, H.MPIX_BFLOAT16, 16, a, b)
     R.check(R.set_support(enable=False))
     assert not R.is_supported_buffers(H.MPI_SUM, H.MPI_FLOAT, 1 << 20, a, b)
 
@@ -101,32 +102,32 @@ def test_env_knobs_read_at_first_use(H):
     subprocess.run([sys.executable, '-c', code], check=True, env=env, timeout=120)
 
 
-def _op_table_long_double(env_extra):
+def _op_table_unsupported(env_extra):
     code = ('import ctypes, sys; sys.path.insert(0, %r)\n'
             'from mpich_amd import redop as R, handles as H\n'
             'L = R.lib()\n'
             'tab = (ctypes.c_void_p * 16).in_dll(L, "MPIX_Op_table")\n'
             'fn = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p,\n'
             '                      ctypes.POINTER(ctypes.c_ssize_t), ctypes.POINTER(ctypes.c_int))'
-            '(tab[H.MPI_SUM & 0xf])\n'
+            '(tab[H.MPI_MAX & 0xf])\n'
             'a = (ctypes.c_char * 64)(); b = (ctypes.c_char * 64)()\n'
-            'n = ctypes.c_ssize_t(4); t = ctypes.c_int(H.as_c_int(H.MPI_LONG_DOUBLE))\n'
+            'n = ctypes.c_ssize_t(4); t = ctypes.c_int(H.as_c_int(H.MPIX_BFLOAT16))\n'
             'fn(a, b, ctypes.byref(n), ctypes.byref(t))\n'
             'print("returned", L.MPIX_Redop_last_error(), bytes(b) == bytes(64))\n' % ROOT)
     return subprocess.run([sys.executable, '-c', code], capture_output=True, text=True,
                           env=dict(os.environ, **env_extra), timeout=120)
 
 
-def test_op_table_unsupported_type_aborts():
+def test_op_table_unsupported_type_aborts(H):
     """op_fns.c:51-53: MPIR_Assert(0) on a type the op function does not cover"""
-    p = _op_table_long_double({})
+    p = _op_table_unsupported({})
     assert p.returncode == -6, (p.returncode, p.stdout, p.stderr)
-    assert 'MPIX_SUM_fn' in p.stderr and '0x4c00100c' in p.stderr, p.stderr
+    assert 'MPIX_MAXF' in p.stderr and '0x%08x' % H.MPIX_BFLOAT16 in p.stderr, p.stderr
     assert 'returned' not in p.stdout
 
 
 def test_op_table_unsupported_type_recorded_without_abort():
-    p = _op_table_long_double({'MPIX_REDOP_OPFN_ABORT': '0'})
+    p = _op_table_unsupported({'MPIX_REDOP_OPFN_ABORT': '0'})
     assert p.returncode == 0, p.stderr
     assert p.stdout.split() == ['returned', '3', 'True'], p.stdout   # MPI_ERR_TYPE, untouched
 
@@ -143,20 +144,20 @@ def _run_threads(n, fn):
 
 
 def test_collectives_decline_unsupported_type_on_every_rank(H):
-    """MPI_LONG_DOUBLE has no kernel: every rank returns MPI_ERR_TYPE before
+    """MAX on MPIX_BFLOAT16 has no kernel: every rank returns MPI_ERR_TYPE before
     any exchange (no rank is left waiting on a peer), buffers untouched"""
     from mpich_amd import ccl
     P = 3
     comms = ccl.comm_create_local(P)        # host transport, no combine installed
     try:
-        send = [np.arange(P * 8 * 16, dtype=np.uint8) for _ in range(P)]   # extent 16
-        recv = [np.full(8 * 16, 0xAB, np.uint8) for _ in range(P)]
+        send = [np.arange(P * 8 * 2, dtype=np.uint8) for _ in range(P)]    # extent 2
+        recv = [np.full(8 * 2, 0xAB, np.uint8) for _ in range(P)]
         rcs = _run_threads(P, lambda r: ccl.reduce_scatter_block(
-            send[r], recv[r], 8, H.MPI_LONG_DOUBLE, H.MPI_SUM, comms[r], 'recursive_halving'))
+            send[r], recv[r], 8, H.MPIX_BFLOAT16, H.MPI_MAX, comms[r], 'recursive_halving'))
         assert rcs == [H.MPI_ERR_TYPE] * P
         assert all((x == 0xAB).all() for x in recv)
         rcs = _run_threads(P, lambda r: ccl.allreduce(
-            send[r], recv[r], 8, H.MPI_LONG_DOUBLE, H.MPI_SUM, comms[r], 'ring'))
+            send[r], recv[r], 8, H.MPIX_BFLOAT16, H.MPI_MAX, comms[r], 'ring'))
         assert rcs == [H.MPI_ERR_TYPE] * P
     finally:
         for c in comms:
