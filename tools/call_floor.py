@@ -58,6 +58,28 @@ def main():
         rows.append(dict(count=count, sync_median_us=round(med.value, 2),
                          **{k: round(v, 3) for k, v in zip(keys, o)}))
     out['rows'] = rows
+    # steady state: n back-to-back 64 KiB calls (the bench's chunked_async_c
+    # loop) for growing n -- where the per-call time leaves the burst figure,
+    # the host is waiting for room in the stream's queue
+    B.mpix_bench_chunked_async.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
+                                           ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                           ctypes.POINTER(ctypes.c_double),
+                                           ctypes.POINTER(ctypes.c_double)]
+    m = 16384
+    x = torch.ones(m * 16384, dtype=torch.float32, device='cuda')
+    y = torch.zeros(m * 16384, dtype=torch.float32, device='cuda')
+    torch.cuda.synchronize()
+    steady = []
+    for ncalls in (64, 256, 1024, 4096, 16384):
+        issue, total = ctypes.c_double(), ctypes.c_double()
+        rc = B.mpix_bench_chunked_async(fa, x.data_ptr(), y.data_ptr(), m * ncalls, m, 4,
+                                        H.MPI_FLOAT, H.MPI_SUM, ctypes.c_void_p(s.cuda_stream),
+                                        ctypes.byref(issue), ctypes.byref(total))
+        assert rc == 0, rc
+        steady.append(dict(calls=ncalls, issue_us_per_call=round(1e6 * issue.value / ncalls, 3),
+                           us_per_call=round(1e6 * total.value / ncalls, 3)))
+    out['steady_64KiB'] = steady
     print(json.dumps(out), flush=True)
 
 
