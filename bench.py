@@ -568,6 +568,22 @@ def other_configs(inb, inout, n, stream):
             rows.append((round(3 * m * ext / (avg * 1e-3) / 1e9, 1), tn, on))
     rows.sort()
     gbs = [r[0] for r in rows]
+    # beyond config 3's types: the x87 / binary128 families (software
+    # arithmetic for SUM / PROD, integer compare-and-select for the rest)
+    soft = []
+    for tn in ('MPI_LONG_DOUBLE', 'MPI_REAL16', 'MPI_C_LONG_DOUBLE_COMPLEX', 'MPI_COMPLEX32',
+               'MPI_LONG_DOUBLE_INT'):
+        dt = getattr(H, tn)
+        ext = redop.datatype_extent(dt)
+        m = nbytes // ext
+        for on, op in H.OPS.items():
+            if op in (H.MPI_REPLACE, H.MPI_NO_OP) or not redop.is_supported(op, dt):
+                continue
+            redop.check(redop.reduce_local_async(b8, a8, m, dt, op, stream))
+            avg, _, _ = event_time_per_launch(
+                lambda: redop.check(redop.reduce_local_async(b8, a8, m, dt, op, stream)), 3, stream,
+                rounds=2)
+            soft.append(dict(type=tn, op=on, GBs=round(3 * m * ext / (avg * 1e-3) / 1e9, 1)))
     cnt = 1 << 26
     src = inb.view(torch.float64)[:cnt]
     dst = inout.view(torch.float64)[:2 * cnt]
@@ -582,6 +598,7 @@ def other_configs(inb, inout, n, stream):
         config3_per_pair_1GiB=dict(pairs=len(rows), min_GBs=gbs[0], median_GBs=gbs[len(gbs) // 2],
                                    max_GBs=gbs[-1], min_frac=round(gbs[0] / HBM_PEAK_GBS, 4),
                                    slowest=[dict(GBs=g, type=t, op=o) for g, t, o in rows[:3]]),
+        x87_binary128_1GiB=soft,
         config5_vector=dict(kernel_ms=round(vavg, 4),
                             GBs_algorithmic=round(3 * cnt * 8 / (vavg * 1e-3) / 1e9, 1),
                             GBs_physical=round(2.5 * GIB / (vavg * 1e-3) / 1e9, 1),

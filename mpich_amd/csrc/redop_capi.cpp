@@ -310,12 +310,14 @@ std::atomic<int> g_pipe_wave{1};
 // the PCIe round trip (crossover measured by bench.py's host_crossover leg).
 std::atomic<bool> g_enable{true};
 std::atomic<long long> g_threshold{-1};
-// defaults from bench.py's host_crossover on MI355X + EPYC 9575F (profiles/
-// r02_host_crossover.json): one core wins below 16 MiB per pageable operand
-// and below 4 MiB per page-locked one; from there on the GPU path is faster or
-// within 5 % at every measured size
-std::atomic<long long> g_host_floor{(long long) 16 << 20};
-std::atomic<long long> g_pinned_floor{(long long) 4 << 20};
+// defaults from the crossover on MI355X + EPYC 9575F boxes, including the
+// driver's (BENCH_r03 host_crossover, profiles/r04_pageable_swing.json): one
+// core matches the pageable path up to 64 MiB per operand (the staged form at
+// 1.00-1.05 x its time) and loses to it from 128 MiB on (0.4-0.8 x); it beats
+// the page-locked zero-copy call at 4 MiB (236 vs 216 us on the driver's box)
+// and loses from 16 MiB on.  Below the floors MPICH keeps its op_fns.c loop.
+std::atomic<long long> g_host_floor{(long long) 128 << 20};
+std::atomic<long long> g_pinned_floor{(long long) 16 << 20};
 // MPIX_Op_table entries return void, like MPIR_op_function: a call the GPU
 // path declines aborts by default, as op_fns.c's MPIR_Assert(0) does
 // (op_fns.c:51-53); MPIX_REDOP_OPFN_ABORT=0 only records the error
