@@ -10,6 +10,7 @@
 #   floor                   tools/call_floor.py
 #   policy                  tools/policy_concurrent.py
 #   bench                   the default bench.py line
+#   evidence                tools/gpu_evidence.sh (R=r04): rocprofv3 stats + PMC passes + bench
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -44,6 +45,7 @@ for step in "$@"; do
         floor) run floor 200 python3 tools/call_floor.py || exit $? ;;
         policy) run policy 300 python3 tools/policy_concurrent.py || exit $? ;;
         bench) run bench 600 python3 bench.py || exit $? ;;
+        evidence) run evidence 1100 env R=${R:-r04} bash tools/gpu_evidence.sh || exit $? ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done
