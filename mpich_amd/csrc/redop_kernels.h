@@ -301,12 +301,13 @@ struct BatchSeg {
     const void *in;
     void *io;
     uint64_t npk;
-    uint32_t blk0;      // first block of the segment
-    uint8_t head, ntail, ain, pad;
+    uint8_t head, ntail, ain, pad[5];
 };
 struct BatchTab {
+    uint32_t blk0[kMaxBatch];   // first block of each segment, ascending, blk0[0] = 0
     BatchSeg s[kMaxBatch];
 };
+static_assert(kMaxBatch <= 64, "one wave looks the segment up");
 
 template <class C, int U, bool NTL, bool NTS>
 __global__ void __launch_bounds__(1024)
@@ -315,20 +316,23 @@ k_batch(BatchTab tab, int nseg, Params prm)
     using T = typename C::unit;
     constexpr uint64_t E = 16 / sizeof(T);
     const uint32_t b = blockIdx.x;
-    int q = 0;      // the segment of this block: the last with blk0 <= b (uniform)
-    while (q + 1 < nseg && tab.s[q + 1].blk0 <= b)
-        ++q;
+    // the segment of this block, the last with blk0 <= b: lane i of every
+    // wave reads blk0[i], one ballot counts them (no serial scan of the table)
+    const uint32_t lane = threadIdx.x & 63;
+    const bool le = lane < (uint32_t) nseg && tab.blk0[lane] <= b;
+    const int q = __popcll(__ballot(le)) - 1;
     const BatchSeg &g = tab.s[q];
-    const uint32_t next = q + 1 < nseg ? tab.s[q + 1].blk0 : gridDim.x;
+    const uint32_t first = tab.blk0[q];
+    const uint32_t next = q + 1 < nseg ? tab.blk0[q + 1] : gridDim.x;
     const T *in = static_cast<const T *>(g.in);
     T *io = static_cast<T *>(g.io);
     const uint64_t tail_start = g.head + g.npk * E;
     if (g.ain)
         contig_body<C, U, NTL, NTS, true, MPIX_REDOP_GROUPED_LOADS>(
-            in, io, g.head, g.npk, tail_start, g.ntail, prm, b - g.blk0, next - g.blk0);
+            in, io, g.head, g.npk, tail_start, g.ntail, prm, b - first, next - first);
     else
         contig_body<C, U, NTL, NTS, false, MPIX_REDOP_GROUPED_LOADS>(
-            in, io, g.head, g.npk, tail_start, g.ntail, prm, b - g.blk0, next - g.blk0);
+            in, io, g.head, g.npk, tail_start, g.ntail, prm, b - first, next - first);
 }
 
 // Multi-input combine: inout = OP(...OP(OP(inout, in[0]), in[1])..., in[k-1]),
@@ -942,8 +946,9 @@ hipError_t launch_batch(const void *const *ins, void *const *ios, const uint64_t
                 if (e != hipSuccess)
                     return e;
             }
-            tab.s[n] = BatchSeg{ins[i], ios[i], npk, (uint32_t) blocks, (uint8_t) head,
-                                (uint8_t) ntail, (uint8_t) ((ai & 15) == (ao & 15)), 0};
+            tab.blk0[n] = (uint32_t) blocks;
+            tab.s[n] = BatchSeg{ins[i], ios[i], npk, (uint8_t) head, (uint8_t) ntail,
+                                (uint8_t) ((ai & 15) == (ao & 15)), {0, 0, 0, 0, 0}};
             blocks += nb;
             ++n;
         }
