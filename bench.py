@@ -74,7 +74,7 @@ def parse(argv=None):
                    help='watchdog (s) over the N>1 secondary collective figures and teardown')
     p.add_argument('--value-timeout', type=float, default=600.0,
                    help='watchdog (s) over the N>1 value leg (bootstrap, parity check, timed steps)')
-    p.add_argument('--pmc', default=os.path.join(ROOT, 'profiles', 'r03_pmc_summary.json'),
+    p.add_argument('--pmc', default=os.path.join(ROOT, 'profiles', 'r04_pmc_summary.json'),
                    help='PMC traffic summary (from tools/pmc_summary.py) to quote as traffic')
     return p.parse_args(argv)
 
@@ -562,10 +562,13 @@ def other_configs(inb, inout, n, stream):
             if op in (H.MPI_REPLACE, H.MPI_NO_OP) or not redop.is_supported(op, dt):
                 continue
             redop.check(redop.reduce_local_async(b8, a8, m, dt, op, stream))
-            avg, _, _ = event_time_per_launch(
+            # median of three batches of five: one disturbed batch (seen once
+            # at 0.62 of the row's rate, profiles/r04_bench_n1.json) does not
+            # set the row
+            _, med, _ = event_time_per_launch(
                 lambda: redop.check(redop.reduce_local_async(b8, a8, m, dt, op, stream)), 5, stream,
-                rounds=2)
-            rows.append((round(3 * m * ext / (avg * 1e-3) / 1e9, 1), tn, on))
+                rounds=3)
+            rows.append((round(3 * m * ext / (med * 1e-3) / 1e9, 1), tn, on))
     rows.sort()
     gbs = [r[0] for r in rows]
     # beyond config 3's types: the x87 / binary128 families (software
@@ -580,10 +583,10 @@ def other_configs(inb, inout, n, stream):
             if op in (H.MPI_REPLACE, H.MPI_NO_OP) or not redop.is_supported(op, dt):
                 continue
             redop.check(redop.reduce_local_async(b8, a8, m, dt, op, stream))
-            avg, _, _ = event_time_per_launch(
+            _, med, _ = event_time_per_launch(
                 lambda: redop.check(redop.reduce_local_async(b8, a8, m, dt, op, stream)), 3, stream,
-                rounds=2)
-            soft.append(dict(type=tn, op=on, GBs=round(3 * m * ext / (avg * 1e-3) / 1e9, 1)))
+                rounds=3)
+            soft.append(dict(type=tn, op=on, GBs=round(3 * m * ext / (med * 1e-3) / 1e9, 1)))
     cnt = 1 << 26
     src = inb.view(torch.float64)[:cnt]
     dst = inout.view(torch.float64)[:2 * cnt]
@@ -823,7 +826,8 @@ def multi_gpu(args, world, rank, dev):
     from mpich_amd import ccl
     result = {'metric': METRIC_RSB, 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
               'unit': 'GB/s', 'higher_is_better': True, 'scaling': 'strong', 'vs_baseline': None,
-              'dtype': 'f32', 'data': 'synthetic (uniform [-1,1), seeded per rank)'}
+              'dtype': 'f32', 'data': 'synthetic (uniform [-1,1), seeded per rank)',
+              'launcher': 'bench.py' if os.environ.get('MPIX_BENCH_LAUNCHED') else 'external'}
     # the round-1 figure, kept as an extra: N independent 1 GiB local reductions
     leg = reduce_local_leg(args, world, rank, dev)
     n = args.count

@@ -197,3 +197,16 @@ def test_collectives_refuse_split_equal(oracle, H):
     finally:
         for c in comms:
             c.free()
+
+
+def test_default_host_floors():
+    """the floors MPIX_Redop_is_supported_buffers applies by default: the
+    measured crossover (128 MiB pageable, 16 MiB page-locked
+    per operand), in a fresh process with no MPIX_REDOP_* in the environment"""
+    code = ('import sys; sys.path.insert(0, %r)\n'
+            'from mpich_amd import redop as R\n'
+            's = R.get_support()\n'
+            'assert s == dict(enable=True, threshold_bytes=-1, host_floor_bytes=128 << 20, '
+            'pinned_floor_bytes=16 << 20), s\n' % ROOT)
+    env = {k: v for k, v in os.environ.items() if not k.startswith('MPIX_REDOP_')}
+    subprocess.run([sys.executable, '-c', code], check=True, env=env, timeout=120)
