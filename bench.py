@@ -102,7 +102,59 @@ def bench_lib():
                                            ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                            ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                            ctypes.POINTER(ctypes.c_double)]
+    L.mpix_bench_issue_burst.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                         ctypes.POINTER(ctypes.c_double)]
+    L.mpix_bench_issue_noargs.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+    L.mpix_bench_issue_noargs.restype = ctypes.c_double
+    L.mpix_bench_query_us.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                      ctypes.POINTER(ctypes.c_double)]
+    L.mpix_bench_issue_hidden.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                          ctypes.POINTER(ctypes.c_double)]
     return L
+
+
+def call_floor_parts(B, inb, inout, stream, count=16384, burst=64, rounds=100):
+    """where the host time of one stream-ordered MPIX_Reduce_local_async goes
+    (64 KiB fp32 SUM), measured in bursts of `burst` calls so issue separates
+    from the GPU: the launch with no kernel arguments (HIP's floor), the
+    argument upload (an empty one-argument kernel minus that), the library's
+    own host work (the reduce call minus the empty kernel)"""
+    fa = ctypes.cast(redop.lib().MPIX_Reduce_local_async, ctypes.c_void_p).value
+    o = (ctypes.c_double * 10)()
+    rc = B.mpix_bench_issue_burst(fa, inb.data_ptr(), inout.data_ptr(), count,
+                                  H.as_c_int(H.MPI_FLOAT), H.as_c_int(H.MPI_SUM),
+                                  stream.cuda_stream, burst, rounds, o)
+    if rc:
+        raise RuntimeError('issue burst loop failed: MPI error class %d' % rc)
+    none = B.mpix_bench_issue_noargs(stream.cuda_stream, burst, rounds)
+    if none < 0:
+        raise RuntimeError('no-argument issue loop failed')
+    q = (ctypes.c_double * 3)()
+    rc = B.mpix_bench_query_us(inout.data_ptr(), stream.cuda_stream, 20000, q)
+    if rc:
+        raise RuntimeError('HIP query loop failed (%d)' % rc)
+    hid = (ctypes.c_double * 2)()
+    rc = B.mpix_bench_issue_hidden(stream.cuda_stream, burst, rounds, hid)
+    if rc:
+        raise RuntimeError('hidden-argument issue loop failed (%d)' % rc)
+    lib = o[0] - o[2]
+    queries = 2 * q[0] + q[1] + q[2]
+    return dict(count=count, burst=burst, rounds=rounds,
+                launch_noargs_us=round(none, 3),
+                argument_upload_us=round(o[2] - none, 3),
+                library_host_us=round(lib, 3),
+                library_hip_queries_us=dict(pointer_attributes_x2=round(2 * q[0], 3),
+                                            stream_device=round(q[1], 3),
+                                            last_error=round(q[2], 3)),
+                library_own_code_us=round(lib - queries, 3),
+                empty_issue_args104_us=round(hid[0], 3),
+                empty_issue_args104_hidden_us=round(hid[1], 3),
+                call_issue_us=round(o[0], 3), call_burst_us=round(o[1], 3),
+                note='host us per call; launch_noargs + argument_upload + library_host = '
+                     'call_issue; library_host = the HIP queries it makes (timed alone, '
+                     'warm) + its own code; call_burst includes the drain of each burst')
 
 
 def c_call_median_us(B, fn_addr, inp, io, n, reps):
@@ -508,12 +560,23 @@ def single_gpu(args, dev):
             result['roofline']['frac_of_triad_store_policy'] = round(achieved / trx, 4)
         del a3
         result['sync_call_latency'] = sync_call_latency(B, dev)
+        # the chunk loops run on a created stream, as a collective engine's
+        # combine stream is; the same 64 KiB loop on torch's current (legacy
+        # null) stream is reported beside it, since every launch there pays
+        # the implicit synchronisation with the other blocking streams
+        cs = torch.cuda.Stream(device=dev)
+        torch.cuda.synchronize()
         result['chunked_async_c'] = chunked_async_c(
-            B, inb, inout, n, stream,
+            B, inb, inout, n, cs,
             (64 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20, 64 << 20) if args.sweep
             else (64 << 10, 1 << 20, 16 << 20))
-        result['chunked_batch_c'] = chunked_batch_c(B, inb, inout, n, stream,
+        result['chunked_batch_c'] = chunked_batch_c(B, inb, inout, n, cs,
                                                     (64 << 10, 1 << 20))
+        result['chunked_async_c_null_stream'] = chunked_async_c(
+            B, inb, inout, n, stream, (64 << 10,))
+        torch.cuda.synchronize()
+        result['call_floor_parts'] = call_floor_parts(B, inb, inout, cs)
+        torch.cuda.synchronize()
         end_to_end(result, n, dev)
         crossover = host_crossover_gpu(B)
         result['configs_3_and_5'] = other_configs(inb, inout, n, stream)

@@ -307,6 +307,95 @@ static double issue_args_us(hipStream_t s, int burst, int rounds)
     return tot / ((double) burst * rounds);
 }
 
+// An empty kernel with no kernel arguments at all: HIP skips the argument
+// upload (the write to device memory and its visibility flush), so its issue
+// time is the launch's own floor; issue of k_empty minus this = the upload.
+__global__ void k_none() {}
+
+extern "C" double mpix_bench_issue_noargs(void *stream, int burst, int rounds)
+{
+    hipStream_t s = (hipStream_t) stream;
+    double tot = 0;
+    for (int r = 0; r < rounds + 1; ++r) {      // round 0 warms up
+        if (hipStreamSynchronize(s) != hipSuccess)
+            return -1;
+        auto a = std::chrono::steady_clock::now();
+        for (int i = 0; i < burst; ++i)
+            hipLaunchKernelGGL(k_none, dim3(1), dim3(64), 0, s);
+        if (r)
+            tot += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - a).count();
+    }
+    if (hipStreamSynchronize(s) != hipSuccess)
+        return -1;
+    return tot / ((double) burst * rounds);
+}
+
+// An empty kernel with k_contig's explicit argument size (104 B) that reads
+// gridDim / blockDim, so its segment carries the hidden arguments too (360 B,
+// as k_contig's does).
+__global__ void k_empty_hidden(ArgBlock<104> g, int *p)
+{
+    if (p && gridDim.x == 12345u && g.w[0] == 1)
+        p[0] = (int) blockDim.x;
+}
+
+// out[0]: host us to issue an empty kernel with a 104-B argument block and no
+// hidden arguments; out[1]: the same with the hidden arguments (360 B).
+extern "C" int mpix_bench_issue_hidden(void *stream, int burst, int rounds, double *out)
+{
+    if (burst < 1 || rounds < 1 || !out)
+        return 12;
+    hipStream_t s = (hipStream_t) stream;
+    out[0] = issue_args_us<104>(s, burst, rounds);
+    ArgBlock<104> g{};
+    double tot = 0;
+    for (int r = 0; r < rounds; ++r) {
+        if (hipStreamSynchronize(s) != hipSuccess)
+            return 15;
+        auto a = std::chrono::steady_clock::now();
+        for (int i = 0; i < burst; ++i)
+            hipLaunchKernelGGL(k_empty_hidden, dim3(1), dim3(64), 0, s, g, (int *) nullptr);
+        tot += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - a).count();
+    }
+    if (hipStreamSynchronize(s) != hipSuccess)
+        return 15;
+    out[1] = tot / ((double) burst * rounds);
+    return out[0] < 0 ? 15 : 0;
+}
+
+// Host us per call of the HIP queries a stream-ordered reduce makes before
+// its launch (redop_capi.cpp reachable()): out[0] hipPointerGetAttributes
+// (made twice per call, once per operand), out[1] hipStreamGetDevice,
+// out[2] hipGetLastError (once after the launch).
+extern "C" int mpix_bench_query_us(const void *p, void *stream, int reps, double *out)
+{
+    if (!p || reps < 1 || !out)
+        return 12;
+    using clk = std::chrono::steady_clock;
+    hipStream_t s = (hipStream_t) stream;
+    hipPointerAttribute_t a;
+    auto t0 = clk::now();
+    for (int i = 0; i < reps; ++i)
+        if (hipPointerGetAttributes(&a, p) != hipSuccess)
+            return 15;
+    auto t1 = clk::now();
+    hipDevice_t d;
+    for (int i = 0; i < reps; ++i)
+        if (hipStreamGetDevice(s, &d) != hipSuccess)
+            return 15;
+    auto t2 = clk::now();
+    int acc = 0;
+    for (int i = 0; i < reps; ++i)
+        acc |= (int) hipGetLastError();
+    auto t3 = clk::now();
+    if (acc)
+        return 15;
+    out[0] = std::chrono::duration<double, std::micro>(t1 - t0).count() / reps;
+    out[1] = std::chrono::duration<double, std::micro>(t2 - t1).count() / reps;
+    out[2] = std::chrono::duration<double, std::micro>(t3 - t2).count() / reps;
+    return 0;
+}
+
 extern "C" int mpix_bench_issue_burst(void *fn, const void *in, void *io, int64_t count, int dt,
                                       int op, void *stream, int burst, int rounds, double *out)
 {

@@ -37,6 +37,12 @@ def main():
     fa = ctypes.cast(L.MPIX_Reduce_local_async, ctypes.c_void_p).value
     fs = ctypes.cast(L.MPIX_Reduce_local, ctypes.c_void_p).value
     s = torch.cuda.Stream()
+    # bench.py's decomposition first, in a process that has done nothing else
+    import bench
+    xb = torch.ones(1 << 20, dtype=torch.float32, device='cuda')
+    yb = torch.zeros(1 << 20, dtype=torch.float32, device='cuda')
+    torch.cuda.synchronize()
+    parts_fresh = bench.call_floor_parts(bench.bench_lib(), xb, yb, s)
     keys = ['reduce_issue_us', 'reduce_burst_us', 'empty_issue_us', 'empty_burst_us',
             'empty_args8_issue_us', 'empty_args64_issue_us', 'empty_args128_issue_us',
             'empty_args256_issue_us', 'empty_args1024_issue_us', 'empty_args2048_issue_us']
@@ -80,6 +86,8 @@ def main():
         steady.append(dict(calls=ncalls, issue_us_per_call=round(1e6 * issue.value / ncalls, 3),
                            us_per_call=round(1e6 * total.value / ncalls, 3)))
     out['steady_64KiB'] = steady
+    out['parts_fresh'] = parts_fresh
+    out['parts_after'] = bench.call_floor_parts(bench.bench_lib(), xb, yb, s)
     print(json.dumps(out), flush=True)
 
 
