@@ -111,6 +111,7 @@ def bench_lib():
     L.mpix_bench_query_us.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                       ctypes.POINTER(ctypes.c_double)]
     L.mpix_bench_issue_hidden.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.POINTER(ctypes.c_double)]
     return L
 
@@ -135,8 +136,9 @@ def call_floor_parts(B, inb, inout, stream, count=16384, burst=64, rounds=100):
     rc = B.mpix_bench_query_us(inout.data_ptr(), stream.cuda_stream, 20000, q)
     if rc:
         raise RuntimeError('HIP query loop failed (%d)' % rc)
-    hid = (ctypes.c_double * 2)()
-    rc = B.mpix_bench_issue_hidden(stream.cuda_stream, burst, rounds, hid)
+    hid = (ctypes.c_double * 3)()
+    rc = B.mpix_bench_issue_hidden(stream.cuda_stream, burst, rounds, inb.data_ptr(),
+                                   inout.data_ptr(), hid)
     if rc:
         raise RuntimeError('hidden-argument issue loop failed (%d)' % rc)
     lib = o[0] - o[2]
@@ -151,6 +153,7 @@ def call_floor_parts(B, inb, inout, stream, count=16384, burst=64, rounds=100):
                 library_own_code_us=round(lib - queries, 3),
                 empty_issue_args104_us=round(hid[0], 3),
                 empty_issue_args104_hidden_us=round(hid[1], 3),
+                empty_issue_two_device_pointers_us=round(hid[2], 3),
                 call_issue_us=round(o[0], 3), call_burst_us=round(o[1], 3),
                 note='host us per call; launch_noargs + argument_upload + library_host = '
                      'call_issue; library_host = the HIP queries it makes (timed alone, '

@@ -339,11 +339,21 @@ __global__ void k_empty_hidden(ArgBlock<104> g, int *p)
         p[0] = (int) blockDim.x;
 }
 
-// out[0]: host us to issue an empty kernel with a 104-B argument block and no
-// hidden arguments; out[1]: the same with the hidden arguments (360 B).
-extern "C" int mpix_bench_issue_hidden(void *stream, int burst, int rounds, double *out)
+// Two device pointers as plain kernel arguments, as the reduce kernels take
+// their operands.
+__global__ void k_empty_ptrs(const float *a, float *b)
 {
-    if (burst < 1 || rounds < 1 || !out)
+    if (a == b && threadIdx.x == 0)
+        b[0] = 0.f;
+}
+
+// out[0]: host us to issue an empty kernel with a 104-B argument block and no
+// hidden arguments; out[1]: the same with the hidden arguments (360 B);
+// out[2]: an empty kernel given the two device pointers p, q.
+extern "C" int mpix_bench_issue_hidden(void *stream, int burst, int rounds, const void *p,
+                                       void *q, double *out)
+{
+    if (burst < 1 || rounds < 1 || !out || !p || !q || p == q)
         return 12;
     hipStream_t s = (hipStream_t) stream;
     out[0] = issue_args_us<104>(s, burst, rounds);
@@ -360,6 +370,18 @@ extern "C" int mpix_bench_issue_hidden(void *stream, int burst, int rounds, doub
     if (hipStreamSynchronize(s) != hipSuccess)
         return 15;
     out[1] = tot / ((double) burst * rounds);
+    tot = 0;
+    for (int r = 0; r < rounds; ++r) {
+        if (hipStreamSynchronize(s) != hipSuccess)
+            return 15;
+        auto a = std::chrono::steady_clock::now();
+        for (int i = 0; i < burst; ++i)
+            hipLaunchKernelGGL(k_empty_ptrs, dim3(1), dim3(64), 0, s, (const float *) p, (float *) q);
+        tot += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - a).count();
+    }
+    if (hipStreamSynchronize(s) != hipSuccess)
+        return 15;
+    out[2] = tot / ((double) burst * rounds);
     return out[0] < 0 ? 15 : 0;
 }
 
