@@ -651,6 +651,130 @@ int check_args(MPIX_Comm c, const void *recvbuf, MPIX_Aint count, MPIX_Datatype 
 }
 
 // ------------------------------------------------------------ schedules
+// The communicator's second stream and its hand-off events (pipelined
+// schedules): at least `nev` events.
+int ensure_aux(MPIX_Comm c, size_t nev)
+{
+    if (!c->aux)
+        HTRY(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+    while (c->pipe_ev.size() < nev) {
+        hipEvent_t e;
+        HTRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        c->pipe_ev.push_back(e);
+    }
+    return MPIX_REDOP_SUCCESS;
+}
+
+// Smallest half-step (bytes) whose combine recursive halving moves onto the
+// second stream (rs_recursive_halving_overlap); 0 = never.  MPIX_COLL_RH_OVERLAP
+// overrides: 0 switches the overlap off, N > 0 sets the bytes.
+size_t rh_overlap_min()
+{
+    const char *e = getenv("MPIX_COLL_RH_OVERLAP");
+    if (!e || !*e)
+        return size_t(1) << 20;
+    char *end = nullptr;
+    unsigned long long v = strtoull(e, &end, 10);
+    return (end && *end == '\0') ? (size_t) v : size_t(1) << 20;
+}
+
+// The overlapped form applies to P a power of two >= 4 with equal blocks on a
+// device communicator combining with the library's kernels (a custom combine
+// is called on the collective's stream only).
+bool rh_overlap_applies(MPIX_Comm c, const std::vector<size_t> &cnts, size_t ext)
+{
+    const int P = c->size;
+    if (c->host() || c->combine || P < 4 || (P & (P - 1)))
+        return false;
+    for (size_t n : cnts)
+        if (n != cnts[0])
+            return false;
+    const size_t min = rh_overlap_min();
+    // the first step's kept quarter is the largest half-step that can split
+    return min && (size_t) (P / 4) * cnts[0] * ext >= min;
+}
+
+// rs_recursive_halving with communication and computation overlapped
+// (SURVEY.md §7 step 5), P = 2^k >= 4, equal blocks of rc elements.  A step's
+// combine is cut in two along the next step's split: the half the next step
+// sends is combined first on the collective's stream s -- the next exchange
+// waits for it -- and the half it keeps on the communicator's second stream,
+// where it runs under the next exchange.  The next step receives into the
+// part of this step's receive buffer the sent half was just read from (dead
+// by then; the same size with equal blocks), so the kept half's combine and
+// the next receive touch disjoint bytes; s waits for the second stream before
+// the next combine reads the kept half.  Every element is still combined
+// once per step with the same two operands in the same roles: same bits.
+// Half-steps under rh_overlap_min() are combined whole on s.
+int rs_recursive_halving_overlap(const char *sb, char *rb, size_t rc, MPIX_Datatype dt,
+                                 MPIX_Op op, MPIX_Comm c, char *ws, hipStream_t s, size_t ext)
+{
+    const int rank = c->rank, size = c->size;
+    const size_t total = rc * (size_t) size, blk = rc * ext, min = rh_overlap_min();
+    char *tmp_results = ws;
+    char *tmp_recvbuf = ws + round256(total * ext);
+    TRY(ensure_aux(c, 2));
+    hipEvent_t ev_in = c->pipe_ev[0], ev_kept = c->pipe_ev[1];
+    TRY(mark(c, "start", s));
+    int mask = size >> 1, send_idx = 0, recv_idx = 0;
+    bool in_rb = false, kept_pending = false;
+    char *rbuf = nullptr;       // where this step's partner half lands
+    while (mask > 0) {
+        const int dst = rank ^ mask;
+        if (rank < dst)
+            send_idx = recv_idx + mask;
+        else
+            recv_idx = send_idx + mask;
+        const bool first = mask == size >> 1;
+        const char *cur = first ? sb : tmp_results;
+        if (first)
+            rbuf = tmp_recvbuf + (size_t) recv_idx * blk;
+        const size_t n = (size_t) mask * rc;
+        TRY(exchange(c, {snd(dst, cur + (size_t) send_idx * blk, n * ext), rcv(dst, rbuf, n * ext)},
+                     s));
+        TRY(mark(c, "exchange", s));
+        const char *own = cur + (size_t) recv_idx * blk;
+        char *out = tmp_results + (size_t) recv_idx * blk;
+        if (mask == 1 && recv_idx == rank && (own == rb || own + blk <= rb || rb + blk <= own)) {
+            out = rb;
+            in_rb = true;
+        }
+        if (kept_pending) {     // `own` is the half the second stream combined last step
+            HTRY(hipStreamWaitEvent(s, ev_kept, 0));
+            kept_pending = false;
+        }
+        const int half = mask >> 1;
+        if (half && (size_t) half * blk >= min) {
+            // the next step keeps the lower half iff this rank is the lower of
+            // its next pair; the other half is what it sends
+            const bool keep_low = rank < (rank ^ half);
+            const size_t k_off = keep_low ? 0 : (size_t) half * blk;
+            const size_t s_off = keep_low ? (size_t) half * blk : 0;
+            HTRY(hipEventRecord(ev_in, s));
+            HTRY(hipStreamWaitEvent(c->aux, ev_in, 0));
+            TRY(combine_to(c, own + k_off, rbuf + k_off, out + k_off, (MPIX_Aint) half * rc, dt,
+                           op, c->aux, ext));
+            HTRY(hipEventRecord(ev_kept, c->aux));
+            kept_pending = true;
+            TRY(combine_to(c, own + s_off, rbuf + s_off, out + s_off, (MPIX_Aint) half * rc, dt,
+                           op, s, ext));
+            TRY(mark(c, "combine (sent half)", s));
+            rbuf += s_off;      // the next partner half lands where the sent half was
+        } else {
+            TRY(combine_to(c, own, rbuf, out, (MPIX_Aint) n, dt, op, s, ext));
+            TRY(mark(c, "combine", s));
+        }
+        send_idx = recv_idx;
+        mask >>= 1;
+    }
+    if (kept_pending)
+        HTRY(hipStreamWaitEvent(s, ev_kept, 0));
+    if (!in_rb)
+        TRY(copy(c, rb, tmp_results + (size_t) rank * blk, blk, s));         // :232-240
+    TRY(mark(c, "epilogue", s));
+    return MPIX_REDOP_SUCCESS;
+}
+
 // MPIR_Reduce_scatter_intra_recursive_halving
 // (reduce_scatter_intra_recursive_halving.c:38-260; the _block variant,
 // reduce_scatter_block_intra_recursive_halving.c:38-260, is the case of
@@ -666,6 +790,8 @@ int rs_recursive_halving(const char *sb, char *rb, const std::vector<size_t> &cn
     const size_t total = disps[size - 1] + cnts[size - 1];
     if (!total)
         return MPIX_REDOP_SUCCESS;
+    if (rh_overlap_applies(c, cnts, ext))
+        return rs_recursive_halving_overlap(sb, rb, cnts[0], dt, op, c, ws, s, ext);
     char *tmp_results = ws;
     char *tmp_recvbuf = ws + round256(total * ext);
     const int pof2 = pof2_of(size), rem = size - pof2;
@@ -971,13 +1097,7 @@ int rs_pairwise_pipelined(const char *sb, char *rb, const std::vector<size_t> &c
     size_t nch = maxblk >> 22;
     if (nch > kPipeChunks)
         nch = kPipeChunks;
-    if (!c->aux)
-        HTRY(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
-    while (c->pipe_ev.size() < nch + 1) {
-        hipEvent_t e;
-        HTRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        c->pipe_ev.push_back(e);
-    }
+    TRY(ensure_aux(c, nch + 1));
     std::vector<size_t> disps(size, 0);
     for (int i = 1; i < size; ++i)
         disps[i] = disps[i - 1] + cnts[i - 1];

@@ -580,6 +580,71 @@ def test_rsb_recursive_halving_pull_matches_oracle(oracle, P, dt, op, in_place):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('overlap', ['1', '0', 'default'])
+@pytest.mark.parametrize('in_place', [False, True])
+@pytest.mark.parametrize('dt,op', [(MPI_FLOAT, MPI_SUM), (MPI_DOUBLE, MPI_MAX),
+                                   (MPI_2INT, MPI_MAXLOC)])
+@pytest.mark.parametrize('P', [4, 8, 16])
+def test_rsb_recursive_halving_overlap_matches_oracle(oracle, monkeypatch, P, dt, op, in_place,
+                                                      overlap):
+    """recursive halving with each step's kept half combined on the second
+    stream under the next exchange (MPIX_COLL_RH_OVERLAP=1: every half-step
+    splits; 0: none; default: half-steps of >= 1 MiB) is bit-identical to the
+    oracle's simulation of reduce_scatter_block_intra_recursive_halving.c --
+    NaN payloads and +-0 (double MAX) and MAXLOC ties show the operand roles;
+    the step labels show which combines ran split"""
+    import torch
+    from mpich_amd import ccl
+    if overlap == 'default':
+        monkeypatch.delenv('MPIX_COLL_RH_OVERLAP', raising=False)
+        recvcount = (1 << 20) // oracle.extent(dt) + 5      # one block > 1 MiB
+    else:
+        monkeypatch.setenv('MPIX_COLL_RH_OVERLAP', overlap)
+        recvcount = 4099
+    if P == 16 and overlap == 'default':
+        recvcount //= 4
+    ext = oracle.extent(dt)
+    rng = np.random.default_rng(0x5EED0900 + P)
+    if dt == MPI_2INT:
+        sends = [rng.integers(0, 3, (P * recvcount, 2)).astype(np.int32) for _ in range(P)]
+    elif dt == MPI_DOUBLE:
+        sends = _special_doubles(P, P * recvcount, P)
+    else:
+        sends = float_sends(P, P * recvcount, 0x5EED0901)
+    raw = [np.ascontiguousarray(s).view(np.uint8).reshape(-1) for s in sends]
+    dsend = [torch.from_numpy(r.copy()).cuda() for r in raw]
+    drecv = dsend if in_place else [torch.zeros(recvcount * ext, dtype=torch.uint8, device='cuda')
+                                    for _ in range(P)]
+    torch.cuda.synchronize()
+    comms = _dev_comms(P)
+
+    def body(r, c):
+        c.set_step_timing(True)
+        rc = ccl.reduce_scatter_block(None if in_place else dsend[r], drecv[r], recvcount, dt, op,
+                                      c, 'recursive_halving')
+        c.set_step_timing(False)
+        torch.cuda.synchronize()
+        return rc, [s['phase'] for s in c.step_times()]
+    out = run_ranks(comms, body)
+    free_all(comms)
+    assert [o[0] for o in out] == [0] * P, out
+    steps = P.bit_length() - 1
+    for rc, phases in out:
+        split = phases.count('combine (sent half)')
+        assert split + phases.count('combine') == steps, phases
+        if overlap == '0':
+            assert split == 0, phases
+        elif overlap == '1':
+            assert split == steps - 1, phases
+        else:       # the first step's kept quarter is >= 1 MiB: at least it splits
+            assert split >= 1, phases
+    exp = oracle.rsb_recursive_halving(raw, recvcount, dt, op)
+    for r in range(P):
+        got = drecv[r].cpu().numpy()[:recvcount * ext]
+        assert got.tobytes() == exp[r].tobytes(), r
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize('dt,op', [(MPI_INT, MPI_PROD), (MPI_DOUBLE, MPI_MAX),
                                    (MPI_INT, MPI_BXOR), (MPI_2INT, MPI_MAXLOC)])
 @pytest.mark.parametrize('algo', ['recursive_halving', 'pairwise'])
