@@ -959,11 +959,19 @@ def multi_gpu(args, world, rank, dev):
     while pof2 * 2 <= world:
         pof2 *= 2
     link_bytes = (pof2 - 1) / pof2 * total * 4      # received over one link across the steps
-    # per-step breakdown on rank 0's stream
+    # per-step breakdown on rank 0's stream, of one extra
+    # call with the combine overlap off (every combine whole on the collective's
+    # stream, so its marks bracket the combine kernel alone; same bits)
+    overlap_env = os.environ.get('MPIX_COLL_RH_OVERLAP')
+    os.environ['MPIX_COLL_RH_OVERLAP'] = '0'
     cc.set_step_timing(True)
     step()
     torch.cuda.synchronize()
     cc.set_step_timing(False)
+    if overlap_env is None:
+        del os.environ['MPIX_COLL_RH_OVERLAP']
+    else:
+        os.environ['MPIX_COLL_RH_OVERLAP'] = overlap_env
     steps = cc.step_times()
     comb_ms = sum(s['ms'] for s in steps if s['phase'] == 'combine')
     exch_ms = sum(s['ms'] for s in steps if s['phase'] == 'exchange')
@@ -979,6 +987,10 @@ def multi_gpu(args, world, rank, dev):
         parity=dict(checked=True, recvcount=rc_small, bit_exact_all_ranks=True,
                     against='numpy restatement of the recursive-halving association'),
         schedule_ran=sched['schedule_ran'],
+        combine_overlap=('off' if os.environ.get('MPIX_COLL_RH_OVERLAP') == '0' else
+                         'each step\'s kept half combined on a second stream under the next '
+                         'exchange (half-steps >= %s B); the step breakdown is of one call '
+                         'with it off' % os.environ.get('MPIX_COLL_RH_OVERLAP', str(1 << 20))),
         roofline={'bound': 'hbm', 'unit': 'GB/s',
                   'achieved': round(comb_gbs, 1) if comb_gbs else None, 'peak': HBM_PEAK_GBS,
                   'frac': round(comb_gbs / HBM_PEAK_GBS, 4) if comb_gbs else None,
