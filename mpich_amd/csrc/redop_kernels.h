@@ -548,6 +548,89 @@ k_elem(const typename C::unit *__restrict__ in, typename C::unit *__restrict__ i
         io[i] = C::apply(io[i], in[i], prm);
 }
 
+// 32-byte units (long double / binary128 pairs and complex), both operands
+// 16-byte aligned.  Loads and stores stay k_contig's: lane l of a wave reads
+// packets l and 64 + l of the wave's 128-packet (64-unit) run, so every
+// instruction moves 1 KiB of whole lines (a unit per lane, its two packets 32
+// bytes apart, would move half lines per instruction).  Adjacent lanes then
+// swap one packet (DPP, no LDS): the even lane of a pair holds unit m of the
+// run, the odd lane unit 32 + m; after the combine the same swap restores the
+// packet layout for the stores.  U runs per lane per operand in flight, all
+// loads of the tile before the first combine, the store policy per block.
+// Full tiles only; the last partial tile goes a unit per lane.
+struct alignas(16) Pk32 {
+    v4u lo, hi;
+};
+
+// v from the other lane of each adjacent pair (quad_perm [1,0,3,2])
+__device__ __forceinline__ v4u swap_pair(v4u v)
+{
+    v4u r;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+        r[e] = (unsigned) __builtin_amdgcn_mov_dpp((int) v[e], 0xB1, 0xF, 0xF, false);
+    return r;
+}
+
+template <class C, int U, bool NTL, bool NTS>
+__global__ void __launch_bounds__(256)
+k_contig32(const typename C::unit *__restrict__ in, typename C::unit *__restrict__ io, uint64_t n,
+           Params prm)
+{
+    using T = typename C::unit;
+    static_assert(sizeof(T) == 32, "32-byte units");
+    const v4u *__restrict__ vin = reinterpret_cast<const v4u *>(in);
+    v4u *__restrict__ vio = reinterpret_cast<v4u *>(io);
+    const bool wt = wt_block(prm);
+    auto f = [&](const Pk32 &a, const Pk32 &b) {
+        return __builtin_bit_cast(Pk32, C::apply(__builtin_bit_cast(T, a),
+                                                 __builtin_bit_cast(T, b), prm));
+    };
+    const uint64_t nt = blockDim.x, tile = nt * U;       // units per tile
+    const uint64_t nfull = n / tile;
+    const unsigned lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const bool odd = lane & 1;
+    // the unit a lane holds after the swap: run unit lane/2 (even) or 32 + lane/2 (odd)
+    auto gather = [&](v4u p0, v4u p1) {
+        const v4u y = swap_pair(odd ? p0 : p1);
+        return odd ? Pk32{y, p1} : Pk32{p0, y};
+    };
+    for (uint64_t t = blockIdx.x; t < nfull; t += gridDim.x) {
+        v4u a0[U], a1[U], b0[U], b1[U];
+        // run u of this wave: units [t*tile + u*nt + wave*64, +64) = packets from q
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t q = 2 * (t * tile + u * nt + wave * 64) + lane;
+            a0[u] = ld16<NTL>(vio + q);
+            a1[u] = ld16<NTL>(vio + q + 64);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t q = 2 * (t * tile + u * nt + wave * 64) + lane;
+            b0[u] = ld16<NTL>(vin + q);
+            b1[u] = ld16<NTL>(vin + q + 64);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const Pk32 r = f(gather(a0[u], a1[u]), gather(b0[u], b1[u]));
+            const v4u y = swap_pair(odd ? r.lo : r.hi);
+            const uint64_t q = 2 * (t * tile + u * nt + wave * 64) + lane;
+            st16_pol<NTS>(vio + q, odd ? y : r.lo, wt);
+            st16_pol<NTS>(vio + q + 64, odd ? r.hi : y, wt);
+        }
+    }
+    // the last partial tile, a unit per lane
+    if (blockIdx.x == nfull % gridDim.x) {
+        for (uint64_t k = nfull * tile + threadIdx.x; k < n; k += nt) {
+            const Pk32 r = f(Pk32{ld16<NTL>(vio + 2 * k), ld16<NTL>(vio + 2 * k + 1)},
+                             Pk32{ld16<NTL>(vin + 2 * k), ld16<NTL>(vin + 2 * k + 1)});
+            st16_pol<NTS>(vio + 2 * k, r.lo, wt);
+            st16_pol<NTS>(vio + 2 * k + 1, r.hi, wt);
+        }
+    }
+}
+
 // Vector target (typerep_op.c:115-150 for MPI_Type_vector(count, bl, stride)):
 // packed source element j = b*bl + k lands on target element b*stride + k.
 // Thread per source element: the source stream is fully coalesced, the
@@ -707,6 +790,9 @@ inline void set_store_policy(Params &p, const LaunchCfg &cfg, unsigned grid)
     p.wt_xcd = (unsigned) cfg.wt_xcd & 0xffu;
 }
 
+// k_contig32's block (its __launch_bounds__)
+constexpr unsigned kContig32Block = 256;
+
 // Contiguous launcher: chooses the packet or the element-wise kernel.
 template <class C>
 hipError_t launch_contig(const void *in, void *io, uint64_t count, const Params &prm,
@@ -719,10 +805,23 @@ hipError_t launch_contig(const void *in, void *io, uint64_t count, const Params 
     bool signalled = false;
     uintptr_t ai = reinterpret_cast<uintptr_t>(in), ao = reinterpret_cast<uintptr_t>(io);
     if constexpr (sizeof(T) > 16) {
-        // 32-byte units (the long double / binary128 pairs): one element per
-        // lane, two 16-byte loads per operand, no packet form
-        unsigned grid = grid_for((uint64_t) cfg.block * 4, count, cfg.max_grid);
-        hipLaunchKernelGGL((k_elem<C>), dim3(grid), dim3(cfg.block), 0, s, tin, tio, count, prm);
+        // 32-byte units (the long double / binary128 pairs and complex): two
+        // units of two 16-byte packets per lane and operand, as many bytes in
+        // flight as k_contig's four packets; operands off the 16-byte grid go
+        // element-wise
+        if (((ai | ao) & 15) == 0) {
+            constexpr int U32 = 2;
+            unsigned grid = grid_for((uint64_t) kContig32Block * U32, count, cfg.max_grid);
+            Params p = prm;
+            p.done = nullptr;
+            set_store_policy(p, cfg, grid);
+            hipLaunchKernelGGL((k_contig32<C, U32, MPIX_REDOP_NT_LOAD, MPIX_REDOP_NT_STORE>),
+                               dim3(grid), dim3(kContig32Block), 0, s, tin, tio, count, p);
+        } else {
+            unsigned grid = grid_for((uint64_t) cfg.block * 4, count, cfg.max_grid);
+            hipLaunchKernelGGL((k_elem<C>), dim3(grid), dim3(cfg.block), 0, s, tin, tio, count,
+                               prm);
+        }
     } else if ((ao % sizeof(T)) == 0 && (ai % sizeof(T)) == 0) {
         uint64_t head = ((16 - (ao & 15)) & 15) / sizeof(T);
         if (head > count)
