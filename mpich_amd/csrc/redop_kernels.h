@@ -185,12 +185,11 @@ template <class C, int U, bool NTL, bool NTS, bool AIN, bool GRP>
 __device__ __forceinline__ void
 contig_body(const typename C::unit *__restrict__ in, typename C::unit *__restrict__ io,
             uint64_t head, uint64_t npk, uint64_t tail_start, uint32_t ntail, const Params &prm,
-            uint64_t bid, uint64_t nblk)
+            uint64_t bid, uint64_t nblk, uint64_t nt)
 {
     const v4u *__restrict__ vin = reinterpret_cast<const v4u *>(in + head);
     const char *__restrict__ cin = reinterpret_cast<const char *>(in + head);
     v4u *__restrict__ vio = reinterpret_cast<v4u *>(io + head);
-    const uint64_t nt = blockDim.x;
     const uint64_t tile = nt * U;
     const uint64_t stride = nblk * tile;
     auto ldin = [&](uint64_t k) -> v4u {
@@ -265,20 +264,25 @@ contig_body(const typename C::unit *__restrict__ in, typename C::unit *__restric
     }
 }
 
+// The grid and block sizes come in as arguments (nblk, nt): a kernel that
+// reads gridDim / blockDim gets the runtime's hidden-argument block appended
+// to its kernel arguments (360 instead of 112 bytes here), which the host
+// writes on every launch.
 template <class C, int U, bool NTL, bool NTS, bool AIN = true, bool GRP = MPIX_REDOP_GROUPED_LOADS>
 __global__ void __launch_bounds__(1024)
 k_contig(const typename C::unit *__restrict__ in, typename C::unit *__restrict__ io,
-         uint64_t head, uint64_t npk, uint64_t tail_start, uint32_t ntail, Params prm)
+         uint64_t head, uint64_t npk, uint64_t tail_start, uint32_t ntail, Params prm,
+         uint32_t nblk, uint32_t nt)
 {
     contig_body<C, U, NTL, NTS, AIN, GRP>(in, io, head, npk, tail_start, ntail, prm, blockIdx.x,
-                                          gridDim.x);
+                                          nblk, nt);
     if (prm.done) {     // small synchronous call (launch_contig sets it)
         __threadfence();            // every wave: its stores complete
         __syncthreads();
         if (threadIdx.x == 0) {
             bool last = true;
-            if (gridDim.x > 1) {    // the last workgroup to arrive signals
-                last = atomicAdd(prm.done_ctr, 1u) == gridDim.x - 1;
+            if (nblk > 1) {         // the last workgroup to arrive signals
+                last = atomicAdd(prm.done_ctr, 1u) == nblk - 1;
                 if (last)
                     *prm.done_ctr = 0;
             }
@@ -329,10 +333,10 @@ k_batch(BatchTab tab, int nseg, Params prm)
     const uint64_t tail_start = g.head + g.npk * E;
     if (g.ain)
         contig_body<C, U, NTL, NTS, true, MPIX_REDOP_GROUPED_LOADS>(
-            in, io, g.head, g.npk, tail_start, g.ntail, prm, b - first, next - first);
+            in, io, g.head, g.npk, tail_start, g.ntail, prm, b - first, next - first, blockDim.x);
     else
         contig_body<C, U, NTL, NTS, false, MPIX_REDOP_GROUPED_LOADS>(
-            in, io, g.head, g.npk, tail_start, g.ntail, prm, b - first, next - first);
+            in, io, g.head, g.npk, tail_start, g.ntail, prm, b - first, next - first, blockDim.x);
 }
 
 // Multi-input combine: inout = OP(...OP(OP(inout, in[0]), in[1])..., in[k-1]),
@@ -841,11 +845,13 @@ hipError_t launch_contig(const void *in, void *io, uint64_t count, const Params 
         if ((ai & 15) == (ao & 15))
             hipLaunchKernelGGL(
                 (k_contig<C, MPIX_REDOP_UNROLL, MPIX_REDOP_NT_LOAD, MPIX_REDOP_NT_STORE, true>),
-                dim3(grid), dim3(cfg.block), 0, s, tin, tio, head, npk, tail_start, ntail, p);
+                dim3(grid), dim3(cfg.block), 0, s, tin, tio, head, npk, tail_start, ntail, p,
+                grid, (uint32_t) cfg.block);
         else
             hipLaunchKernelGGL(
                 (k_contig<C, MPIX_REDOP_UNROLL, MPIX_REDOP_NT_LOAD, MPIX_REDOP_NT_STORE, false>),
-                dim3(grid), dim3(cfg.block), 0, s, tin, tio, head, npk, tail_start, ntail, p);
+                dim3(grid), dim3(cfg.block), 0, s, tin, tio, head, npk, tail_start, ntail, p,
+                grid, (uint32_t) cfg.block);
     } else {
         unsigned grid = grid_for((uint64_t) cfg.block * 4, count, cfg.max_grid);
         hipLaunchKernelGGL((k_elem<C>), dim3(grid), dim3(cfg.block), 0, s, tin, tio, count, prm);

@@ -30,23 +30,28 @@ static void launch(int v, const float *in, float *io, uint64_t n, hipStream_t s)
     switch (v) {
         case 0:
             hipLaunchKernelGGL((k_contig<C, 4, true, true, true, false>), dim3((unsigned) (npk / 1024)),
-                               dim3(256), 0, s, in, io, 0, npk, npk * 4, 0u, prm);
+                               dim3(256), 0, s, in, io, 0, npk, npk * 4, 0u, prm,
+                               (uint32_t) (npk / 1024), 256u);
             break;
         case 2:
             hipLaunchKernelGGL((k_contig<C, 8, true, true, true, true>), dim3((unsigned) (npk / 2048)),
-                               dim3(256), 0, s, in, io, 0, npk, npk * 4, 0u, prm);
+                               dim3(256), 0, s, in, io, 0, npk, npk * 4, 0u, prm,
+                               (uint32_t) (npk / 2048), 256u);
             break;
         case 3:
             hipLaunchKernelGGL((k_contig<C, 2, true, true, true, true>), dim3((unsigned) (npk / 512)),
-                               dim3(256), 0, s, in, io, 0, npk, npk * 4, 0u, prm);
+                               dim3(256), 0, s, in, io, 0, npk, npk * 4, 0u, prm,
+                               (uint32_t) (npk / 512), 256u);
             break;
         case 4:
             hipLaunchKernelGGL((k_contig<C, 4, true, true, true, true>), dim3((unsigned) (npk / 2048)),
-                               dim3(512), 0, s, in, io, 0, npk, npk * 4, 0u, prm);
+                               dim3(512), 0, s, in, io, 0, npk, npk * 4, 0u, prm,
+                               (uint32_t) (npk / 2048), 512u);
             break;
         default:
             hipLaunchKernelGGL((k_contig<C, 4, true, true, true, true>), dim3((unsigned) (npk / 1024)),
-                               dim3(256), 0, s, in, io, 0, npk, npk * 4, 0u, prm);
+                               dim3(256), 0, s, in, io, 0, npk, npk * 4, 0u, prm,
+                               (uint32_t) (npk / 1024), 256u);
     }
 }
 

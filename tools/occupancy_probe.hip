@@ -62,7 +62,7 @@ static void launch(int v, const void *in, void *io, uint64_t bytes, hipStream_t 
     if (v == 0)
         hipLaunchKernelGGL((k_contig<C, U, true, true, true, true>), dim3((unsigned) tiles), dim3(256),
                            0, s, static_cast<const T *>(in), static_cast<T *>(io), 0, npk,
-                           npk * (16 / sizeof(T)), 0u, prm);
+                           npk * (16 / sizeof(T)), 0u, prm, (uint32_t) tiles, 256u);
     else if (v == 1)
         hipLaunchKernelGGL(k_plain<C>, dim3((unsigned) tiles), dim3(256), 0, s, vin, vio, prm);
     else
