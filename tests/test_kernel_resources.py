@@ -23,7 +23,8 @@ READELF = '/opt/rocm/lib/llvm/bin/llvm-readelf'
 
 
 def _kernels(obj):
-    """[(name, vgpr_count, private_segment_fixed_size)] of the gfx950 code object in obj"""
+    """[(name, vgpr_count, private_segment_fixed_size, kernarg_segment_size)] of the gfx950
+    code object in obj"""
     with tempfile.TemporaryDirectory() as d:
         src = os.path.join(d, os.path.basename(obj))
         shutil.copy(obj, src)
@@ -37,8 +38,9 @@ def _kernels(obj):
         m = re.search(r'\.name:\s+(\S+)', b)
         v = re.search(r'\.vgpr_count:\s+(\d+)', b)
         p = re.search(r'\.private_segment_fixed_size:\s+(\d+)', b)
-        if m and v and p:
-            out.append((m.group(1), int(v.group(1)), int(p.group(1))))
+        k = re.search(r'\.kernarg_segment_size:\s+(\d+)', b)
+        if m and v and p and k:
+            out.append((m.group(1), int(v.group(1)), int(p.group(1)), int(k.group(1))))
     return out
 
 
@@ -57,12 +59,22 @@ def kernels():
 
 def test_no_kernel_uses_scratch(kernels):
     assert len(kernels) > 1000
-    spilled = [(n, v, p) for n, v, p in kernels if p]
+    spilled = [(n, v, p) for n, v, p, _ in kernels if p]
     assert not spilled, spilled[:5]
 
 
 def test_contiguous_kernels_under_the_vgpr_cap(kernels):
-    contig = [(n, v) for n, v, _ in kernels if n.startswith('_ZN4mpix8k_contig')]
+    contig = [(n, v) for n, v, _, _ in kernels if n.startswith('_ZN4mpix8k_contig')]
     assert len(contig) >= 200
     worst = max(contig, key=lambda x: x[1])
     assert worst[1] <= 96, worst
+
+
+def test_contiguous_kernels_carry_no_hidden_arguments(kernels):
+    """k_contig (every single stream-ordered call) gets its grid and block
+    sizes as arguments: reading gridDim / blockDim would append the runtime's
+    hidden-argument block (360 instead of 112 bytes), written by the host on
+    every launch (bench.py call_floor_parts: up to 1 us per call)"""
+    contig = [(n, k) for n, _, _, k in kernels if n.startswith('_ZN4mpix8k_contig')]
+    assert len(contig) >= 200
+    assert max(k for _, k in contig) <= 128, max(contig, key=lambda x: x[1])
