@@ -315,7 +315,7 @@ static_assert(kMaxBatch <= 64, "one wave looks the segment up");
 
 template <class C, int U, bool NTL, bool NTS>
 __global__ void __launch_bounds__(1024)
-k_batch(BatchTab tab, int nseg, Params prm)
+k_batch(BatchTab tab, int nseg, Params prm, uint32_t nblk, uint32_t nt)
 {
     using T = typename C::unit;
     constexpr uint64_t E = 16 / sizeof(T);
@@ -327,16 +327,16 @@ k_batch(BatchTab tab, int nseg, Params prm)
     const int q = __popcll(__ballot(le)) - 1;
     const BatchSeg &g = tab.s[q];
     const uint32_t first = tab.blk0[q];
-    const uint32_t next = q + 1 < nseg ? tab.blk0[q + 1] : gridDim.x;
+    const uint32_t next = q + 1 < nseg ? tab.blk0[q + 1] : nblk;
     const T *in = static_cast<const T *>(g.in);
     T *io = static_cast<T *>(g.io);
     const uint64_t tail_start = g.head + g.npk * E;
     if (g.ain)
         contig_body<C, U, NTL, NTS, true, MPIX_REDOP_GROUPED_LOADS>(
-            in, io, g.head, g.npk, tail_start, g.ntail, prm, b - first, next - first, blockDim.x);
+            in, io, g.head, g.npk, tail_start, g.ntail, prm, b - first, next - first, nt);
     else
         contig_body<C, U, NTL, NTS, false, MPIX_REDOP_GROUPED_LOADS>(
-            in, io, g.head, g.npk, tail_start, g.ntail, prm, b - first, next - first, blockDim.x);
+            in, io, g.head, g.npk, tail_start, g.ntail, prm, b - first, next - first, nt);
 }
 
 // Multi-input combine: inout = OP(...OP(OP(inout, in[0]), in[1])..., in[k-1]),
@@ -1021,7 +1021,8 @@ hipError_t launch_batch(const void *const *ins, void *const *ios, const uint64_t
             Params q = p;
             set_store_policy(q, cfg, (unsigned) blocks);
             hipLaunchKernelGGL((k_batch<C, MPIX_REDOP_UNROLL, MPIX_REDOP_NT_LOAD, MPIX_REDOP_NT_STORE>),
-                               dim3((unsigned) blocks), dim3(cfg.block), 0, s, tab, n, q);
+                               dim3((unsigned) blocks), dim3(cfg.block), 0, s, tab, n, q,
+                               (uint32_t) blocks, (uint32_t) cfg.block);
             n = 0;
             blocks = 0;
             return hipGetLastError();
