@@ -569,6 +569,7 @@ def single_gpu(args, dev):
         # the implicit synchronisation with the other blocking streams
         cs = torch.cuda.Stream(device=dev)
         torch.cuda.synchronize()
+        chunked_async_c(B, inb, inout, n, cs, (64 << 10,))     # untimed warm-up of the loop
         result['chunked_async_c'] = chunked_async_c(
             B, inb, inout, n, cs,
             (64 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20, 64 << 20) if args.sweep
