@@ -916,22 +916,36 @@ def multi_gpu(args, world, rank, dev):
     recvcount = total // world
     # parity before timing: fp32 SUM at a reduced size, bit for bit against
     # the schedule's association restated in numpy on every rank
+    # checked twice: with every half-step's combine split onto the second
+    # stream (MPIX_COLL_RH_OVERLAP=1, the form the timed 4 GiB calls take at
+    # P = 2^k >= 4) and with none split
     rc_small = (1 << 16) + 3
     sends = [rsb_inputs_host(r, world, rc_small) for r in range(world)]
     ds = torch.from_numpy(sends[rank]).to(dev)
     dr = torch.empty(rc_small, dtype=torch.float32, device=dev)
-    redop.check(ccl.reduce_scatter_block(ds, dr, rc_small, H.MPI_FLOAT, H.MPI_SUM, cc,
-                                         'recursive_halving'), 'MPIX_Reduce_scatter_block')
-    sched = schedule_ran(cc, 'recursive_halving')
-    if 'error' in sched:
-        raise RuntimeError('value leg: recursive halving requested, ' + sched['error'])
-    got = dr.cpu().numpy()
-    ok = got.tobytes() == rh_expected_block(sends, rank, rc_small).tobytes()
-    ok_all = allreduce_scalar(1.0 if ok else 0.0, dist.ReduceOp.MIN, dev) == 1.0
+    expected = rh_expected_block(sends, rank, rc_small).tobytes()
+    overlap_env = os.environ.get('MPIX_COLL_RH_OVERLAP')
+    try:
+        for mode in ('1', '0'):
+            os.environ['MPIX_COLL_RH_OVERLAP'] = mode
+            dr.fill_(float('nan'))
+            redop.check(ccl.reduce_scatter_block(ds, dr, rc_small, H.MPI_FLOAT, H.MPI_SUM, cc,
+                                                 'recursive_halving'), 'MPIX_Reduce_scatter_block')
+            sched = schedule_ran(cc, 'recursive_halving')
+            if 'error' in sched:
+                raise RuntimeError('value leg: recursive halving requested, ' + sched['error'])
+            ok = dr.cpu().numpy().tobytes() == expected
+            ok_all = allreduce_scalar(1.0 if ok else 0.0, dist.ReduceOp.MIN, dev) == 1.0
+            if not ok_all:
+                raise RuntimeError('recursive-halving RSB over RCCL differs from the reference '
+                                   'association (fp32 SUM, recvcount %d, overlap %s) on some rank'
+                                   % (rc_small, 'on' if mode == '1' else 'off'))
+    finally:
+        if overlap_env is None:
+            os.environ.pop('MPIX_COLL_RH_OVERLAP', None)
+        else:
+            os.environ['MPIX_COLL_RH_OVERLAP'] = overlap_env
     del ds, dr, sends
-    if not ok_all:
-        raise RuntimeError('recursive-halving RSB over RCCL differs from the reference association '
-                           '(fp32 SUM, recvcount %d) on some rank' % rc_small)
 
     send = torch.empty(total, dtype=torch.float32, device=dev)
     fill_uniform(send, 0x5EED0100 + rank)
@@ -986,6 +1000,7 @@ def multi_gpu(args, world, rank, dev):
                 'vector_bytes_per_rank': total * 4, 'recvcount': recvcount,
                 'parallelism': 'rsb%d (one rank per GPU, libmpix_coll over RCCL)' % world},
         parity=dict(checked=True, recvcount=rc_small, bit_exact_all_ranks=True,
+                    combine_overlap_checked=['every half-step split', 'none split'],
                     against='numpy restatement of the recursive-halving association'),
         schedule_ran=sched['schedule_ran'],
         combine_overlap=('off' if os.environ.get('MPIX_COLL_RH_OVERLAP') == '0' else
