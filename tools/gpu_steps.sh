@@ -10,6 +10,7 @@
 #   floor                   tools/call_floor.py
 #   policy                  tools/policy_concurrent.py
 #   bench                   the default bench.py line
+#   pmcwide                 tools/pmc_wide.py: FETCH/WRITE passes over the 32-byte-unit kernels
 #   evidence                tools/gpu_evidence.sh (R=r04): rocprofv3 stats + PMC passes + bench
 set -o pipefail
 cd $GRAFT_REPO_ROOT
@@ -45,6 +46,16 @@ for step in "$@"; do
         floor) run floor 200 python3 tools/call_floor.py || exit $? ;;
         policy) run policy 300 python3 tools/policy_concurrent.py || exit $? ;;
         bench) run bench 600 python3 bench.py || exit $? ;;
+        pmcwide) run pmcwide_run 120 python3 tools/pmc_wide.py || exit $?
+                 run pmcwide_fetch 120 rocprofv3 --pmc FETCH_SIZE -T -d $O/pw_fetch -o f \
+                     --output-format csv -- python3 tools/pmc_wide.py || exit $?
+                 run pmcwide_write 120 rocprofv3 --pmc WRITE_SIZE -T -d $O/pw_write -o w \
+                     --output-format csv -- python3 tools/pmc_wide.py || exit $?
+                 tail -n 1 $O/pmcwide_run.out > $O/pmcwide_run.json
+                 run pmcwide_sum 60 python3 tools/pmc_wide.py --summarise \
+                     "$(find $O/pw_fetch -name '*counter_collection.csv' | head -n 1)" \
+                     "$(find $O/pw_write -name '*counter_collection.csv' | head -n 1)" \
+                     $O/r04_pmc_wide.json $O/pmcwide_run.json || exit $? ;;
         evidence) run evidence 1100 env R=${R:-r04} bash tools/gpu_evidence.sh || exit $? ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
