@@ -231,3 +231,33 @@ def test_long_double_int_other_entry_points(R, H, oracle):
     ha = a.copy()
     assert R.MPI_Reduce_local(bs[0].copy(), ha, n, dt, op) == 0
     assert np.array_equal(ha, orc(bs[0], a.copy()))
+
+
+@pytest.mark.parametrize('n', [1, 63, 64, 511, 512, 513, 3 * 512 + 7, 20011])
+@pytest.mark.parametrize('offs', [(0, 0), (16, 0), (0, 16), (16, 16), (8, 8)])
+def test_contig32_tiles_and_offsets(R, H, oracle, n, offs):
+    """k_contig32 (32-byte units, whole-line packet loads plus an adjacent-lane
+    swap; 512-unit tiles of 256 lanes x 2 runs) across the tile boundaries and
+    the last partial tile, with in / inout at 16-byte offsets that keep the
+    packet path (0, 16: units on or off the 32-byte grid) and both 8 bytes off
+    the 16-byte grid (the element-wise kernel); MAXLOC on MPI_LONG_DOUBLE_INT
+    specials, bit for bit with the padding"""
+    rng = np.random.default_rng(0x5EED0610 + n)
+    dt, op = H.MPI_LONG_DOUBLE_INT, H.MPI_MAXLOC
+    spec = np.stack(x87_specials())
+    A, B = loc_records(spec[rng.integers(0, len(spec), n)], spec[rng.integers(0, len(spec), n)],
+                       rng, 16)
+    exp = A.reshape(-1).copy()
+    assert oracle.reduce_local(B.reshape(-1).copy(), exp, n, dt, op) == 0
+    oi, oo = offs
+    bi = torch.zeros(n * 32 + 64, dtype=torch.uint8, device='cuda')
+    bo = torch.zeros(n * 32 + 64, dtype=torch.uint8, device='cuda')
+    bi[oi:oi + n * 32] = torch.from_numpy(B.reshape(-1).copy()).cuda()
+    bo[oo:oo + n * 32] = torch.from_numpy(A.reshape(-1).copy()).cuda()
+    guard = bo.cpu().numpy().copy()
+    assert R.MPI_Reduce_local(bi[oi:], bo[oo:], n, dt, op) == 0
+    got = host(bo)
+    assert np.array_equal(got[oo:oo + n * 32], exp)
+    # nothing outside the target span is written
+    assert np.array_equal(got[:oo], guard[:oo]) and np.array_equal(got[oo + n * 32:],
+                                                                   guard[oo + n * 32:])
