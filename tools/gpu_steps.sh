@@ -9,6 +9,7 @@
 #   swing                   tools/pageable_swing.py, default and GPU-node worker affinity
 #   floor                   tools/call_floor.py
 #   policy                  tools/policy_concurrent.py
+#   pgrid                   tools/pinned_grid.py: zero-copy calls against the grid cap
 #   bench                   the default bench.py line
 #   pmcwide                 tools/pmc_wide.py: FETCH/WRITE passes over the 32-byte-unit kernels
 #   evidence                tools/gpu_evidence.sh (R=r04): rocprofv3 stats + PMC passes + bench
@@ -45,6 +46,7 @@ for step in "$@"; do
                         --sizes 16,24,32,64 || exit $? ;;
         floor) run floor 200 python3 tools/call_floor.py || exit $? ;;
         policy) run policy 300 python3 tools/policy_concurrent.py || exit $? ;;
+        pgrid) run pgrid 300 python3 tools/pinned_grid.py || exit $? ;;
         bench) run bench 600 python3 bench.py || exit $? ;;
         pmcwide) run pmcwide_run 120 python3 tools/pmc_wide.py || exit $?
                  run pmcwide_fetch 120 rocprofv3 --pmc FETCH_SIZE -T -d $O/pw_fetch -o f \
