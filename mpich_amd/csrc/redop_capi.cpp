@@ -240,6 +240,14 @@ const Entry *gpu_entry(uint32_t opi, uint32_t it)
 // ---------------------------------------------------------------- state
 std::atomic<long long> g_ftrue{1}, g_ffalse{0};
 std::atomic<int> g_block{256}, g_max_grid{0};
+// Grid cap of kernels reading page-locked host memory over PCIe (zero-copy):
+// with one tile per block every block loads its whole tile (host to device)
+// before it stores (device to host), and a grid of a few hundred blocks is
+// one round, so the two link directions take turns.  32 looping blocks keep
+// both busy: 4 MiB 235 -> 186 us, 16 MiB 780 -> 655 us, 1 GiB 39.2 -> 38.1 ms
+// (tools/pinned_grid.py, profiles/r04_pinned_grid.json; 32-64 equal, 16 and
+// 8 lose).  MPIX_REDOP_ZC_GRID overrides (0: uncapped).
+std::atomic<int> g_zc_grid{32};
 // Store policy of the contiguous and multi-input kernels and the two-slot tree
 // (MPIX_Redop_set_store_policy): the blocks running on the XCDs of g_wt_xcd
 // store write-through (sc0 sc1), the others non-temporally.  Two XCDs of eight
@@ -343,6 +351,8 @@ void read_env()
         g_wt_xcd = (int) (strtol(s, nullptr, 0) & 0xff);
     if (const char *s = getenv("MPIX_REDOP_MAXGRID"))
         g_max_grid = atoi(s) > 0 ? atoi(s) : 0;
+    if (const char *s = getenv("MPIX_REDOP_ZC_GRID"))
+        g_zc_grid = atoi(s) > 0 ? atoi(s) : 0;
     if (const char *s = getenv("MPIX_REDOP_SYNC"))
         g_sync = strcmp(s, "block") == 0 ? 0
                : strcmp(s, "flag") == 0  ? 2
@@ -555,6 +565,16 @@ LaunchCfg launch_cfg()
                      g_wt_phase.load(), wt};
 }
 
+// ... of one whose operand(s) include page-locked host memory (g_zc_grid)
+LaunchCfg launch_cfg(bool zero_copy)
+{
+    LaunchCfg c = launch_cfg();
+    const int z = g_zc_grid.load();
+    if (zero_copy && z > 0 && (c.max_grid <= 0 || c.max_grid > z))
+        c.max_grid = z;
+    return c;
+}
+
 Params params() { return Params{g_ftrue.load(), g_ffalse.load()}; }
 
 // Spin until the pinned completion word holds `seq`.  The stream is queried
@@ -675,7 +695,7 @@ int validate(const void *in, const void *io, MPIX_Aint count, uint32_t dt, uint3
 // workgroup counter, NULL = one workgroup only).
 int enqueue(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext, uint32_t op,
             hipStream_t s, uint32_t *done = nullptr, uint32_t *ctr = nullptr, uint32_t seq = 0,
-            bool *signalled = nullptr)
+            bool *signalled = nullptr, bool zero_copy = false)
 {
     if (signalled)
         *signalled = false;
@@ -694,7 +714,7 @@ int enqueue(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext,
     prm.done = done;
     prm.done_ctr = ctr;
     prm.done_seq = seq;
-    int rc = hip_err(e->contig(in, io, count, prm, launch_cfg(), s));
+    int rc = hip_err(e->contig(in, io, count, prm, launch_cfg(zero_copy), s));
     if (signalled)
         *signalled = done && rc == MPIX_REDOP_SUCCESS;
     return rc;
@@ -707,20 +727,20 @@ int enqueue(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext,
 // profiles/r01_sync_latency.txt); other ops and the other wait modes go
 // through wait_stream.
 int run_sync(DevState *d, const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext,
-             uint32_t op)
+             uint32_t op, bool zero_copy = false)
 {
     launch_cfg();       // environment read before g_sync is consulted
     if (g_sync.load() == 2 && d->flag) {
         const uint32_t seq = ++d->seq;
         bool signalled = false;
         int rc = enqueue(in, io, count, it, ext, op, d->s[0], (uint32_t *) d->flag, d->flag_ctr,
-                         seq, &signalled);
+                         seq, &signalled, zero_copy);
         if (signalled)      // the kernel stores the word itself
             return spin_on_flag(d, d->s[0], seq);
         int rc2 = wait_stream(d, d->s[0]);
         return rc ? rc : rc2;
     }
-    int rc = enqueue(in, io, count, it, ext, op, d->s[0]);
+    int rc = enqueue(in, io, count, it, ext, op, d->s[0], nullptr, nullptr, 0, nullptr, zero_copy);
     int rc2 = wait_stream(d, d->s[0]);
     return rc ? rc : rc2;
 }
@@ -869,7 +889,7 @@ int bounced(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext,
         memcpy(d->bounce + d->bounce_half, io, bytes);
         kio = d->bounce_dev + d->bounce_half;
     }
-    int rc = run_sync(d, kin, kio, count, it, ext, op);
+    int rc = run_sync(d, kin, kio, count, it, ext, op, true);
     if (rc == MPIX_REDOP_SUCCESS && io_host)
         memcpy(io, d->bounce + d->bounce_half, bytes);
     return rc;
@@ -1091,7 +1111,7 @@ int pipelined(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ex
             pipe_mark(tr, w, k, 1);
             const void *kin = in_pg ? (const void *) dbuf[b] : (const char *) in + off * ext;
             void *kio = io_pg ? (void *) (dbuf[b] + half) : (char *) io + off * ext;
-            int rc = enqueue(kin, kio, n, it, ext, op, sl.s);
+            int rc = enqueue(kin, kio, n, it, ext, op, sl.s, nullptr, nullptr, 0, nullptr, true);
             return rc ? rc : hip_err(hipEventRecord(sl.ev[b], sl.s));
         };
         // chunk k's kernel done: its result back to the pageable inout
@@ -1312,7 +1332,8 @@ int waved(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext, u
                 // (profiles/r03_pageable_split_rejected.jsonl): the copy
                 // engine and the CUs' PCIe reads share the link badly, as the
                 // SDMA-only duplex pattern does (56 ms, bench.py pcie)
-                int rc = enqueue(kin, kio, cnt, it, ext, op, P.ring_s);
+                int rc = enqueue(kin, kio, cnt, it, ext, op, P.ring_s, nullptr, nullptr, 0, nullptr,
+                                 true);
                 if (rc == MPIX_REDOP_SUCCESS)
                     rc = hip_err(hipEventRecord(P.ring_ev[b], P.ring_s));
                 if (rc)
@@ -1477,14 +1498,18 @@ int stream_device(hipStream_t s)
 // another device's memory is reachable only with peer access (enabled here at
 // first use), else refused too.  `launch` caches the stream's device (-2 = not
 // looked up yet).
-bool reachable(const void *p, hipStream_t s, int *launch, const void **devptr)
+bool reachable(const void *p, hipStream_t s, int *launch, const void **devptr,
+               bool *pinned = nullptr)
 {
     int owner = -1;
     const Where w = classify(p, &owner, devptr);
     if (w == Where::Pageable)
         return false;
-    if (w != Where::Device)
+    if (w != Where::Device) {
+        if (pinned)
+            *pinned = true;     // page-locked host memory, read through its mapping
         return true;
+    }
     if (*launch == -2)
         *launch = stream_device(s);
     return peer_state(*launch, owner) != kPeerNone;
@@ -1742,11 +1767,12 @@ int MPIX_Reduce_local_async(const void *inbuf, void *inoutbuf, MPIX_Aint count,
         return set_err(rc);
     const void *pin, *pio;
     int launch = -2;
-    if (!reachable(inbuf, (hipStream_t) stream, &launch, &pin) ||
-        !reachable(inoutbuf, (hipStream_t) stream, &launch, &pio))
+    bool zc = false;
+    if (!reachable(inbuf, (hipStream_t) stream, &launch, &pin, &zc) ||
+        !reachable(inoutbuf, (hipStream_t) stream, &launch, &pio, &zc))
         return set_err(MPIX_REDOP_ERR_BUFFER);
     return set_err(enqueue(pin, (void *) pio, (uint64_t) count, it, ext, (uint32_t) op,
-                           (hipStream_t) stream));
+                           (hipStream_t) stream, nullptr, nullptr, 0, nullptr, zc));
 }
 
 // Several ready chunks in one launch (include/mpix_redop.h).  Checks first,
@@ -1882,7 +1908,8 @@ int MPIX_Reduce_local(const void *inbuf, void *inoutbuf, MPIX_Aint count, MPIX_D
     DevState *d = dev_state(dev);
     if (!d)
         return set_err(MPIX_REDOP_ERR_OTHER);
-    return set_err(run_sync(d, pin, (void *) pio, (uint64_t) count, it, ext, (uint32_t) op));
+    return set_err(run_sync(d, pin, (void *) pio, (uint64_t) count, it, ext, (uint32_t) op,
+                            win == Where::Pinned || wio == Where::Pinned));
 }
 
 int MPIX_Reduce_local_vector_async(const void *inbuf, void *inoutbuf, MPIX_Aint count,
