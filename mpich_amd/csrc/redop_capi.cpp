@@ -321,11 +321,13 @@ std::atomic<long long> g_threshold{-1};
 // defaults from the crossover on MI355X + EPYC 9575F boxes, including the
 // driver's (BENCH_r03 host_crossover, profiles/r04_pageable_swing.json): one
 // core matches the pageable path up to 64 MiB per operand (the staged form at
-// 1.00-1.05 x its time) and loses to it from 128 MiB on (0.4-0.8 x); it beats
-// the page-locked zero-copy call at 4 MiB (236 vs 216 us on the driver's box)
-// and loses from 16 MiB on.  Below the floors MPICH keeps its op_fns.c loop.
+// 1.00-1.05 x its time) and loses to it from 128 MiB on (0.4-0.8 x).  The
+// page-locked zero-copy call lost to one core at 4 MiB (236 vs 216 us on the
+// driver's box) until its kernel was capped to looping blocks (g_zc_grid):
+// 169 vs 219 us at 4 MiB, even at 1 MiB (profiles/r04_bench_n1_zc.json).
+// Below the floors MPICH keeps its op_fns.c loop.
 std::atomic<long long> g_host_floor{(long long) 128 << 20};
-std::atomic<long long> g_pinned_floor{(long long) 16 << 20};
+std::atomic<long long> g_pinned_floor{(long long) 4 << 20};
 // MPIX_Op_table entries return void, like MPIR_op_function: a call the GPU
 // path declines aborts by default, as op_fns.c's MPIR_Assert(0) does
 // (op_fns.c:51-53); MPIX_REDOP_OPFN_ABORT=0 only records the error

@@ -207,6 +207,6 @@ def test_default_host_floors():
             'from mpich_amd import redop as R\n'
             's = R.get_support()\n'
             'assert s == dict(enable=True, threshold_bytes=-1, host_floor_bytes=128 << 20, '
-            'pinned_floor_bytes=16 << 20), s\n' % ROOT)
+            'pinned_floor_bytes=4 << 20), s\n' % ROOT)
     env = {k: v for k, v in os.environ.items() if not k.startswith('MPIX_REDOP_')}
     subprocess.run([sys.executable, '-c', code], check=True, env=env, timeout=120)
