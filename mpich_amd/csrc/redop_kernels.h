@@ -359,23 +359,34 @@ k_contig_multi(MultiIn<typename C::unit> ins, int k, typename C::unit *__restric
     const uint64_t tile = nt * U;
     const uint64_t stride = (uint64_t) gridDim.x * tile;
     const bool wt = wt_block(prm);
+    // input q + 1's packets are loaded before input q's are combined, so two
+    // inputs' worth stay in flight through the fold (one at a time: 5.86 TB/s
+    // at k = 7, tools/multi_probe.py)
+    auto load = [&](int q, v4u *b, uint64_t i) {
+        const v4u *__restrict__ vin = reinterpret_cast<const v4u *>(ins.p[q] + head);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (i + u * nt < npk)
+                b[u] = ld16<true>(vin + i + u * nt);
+    };
     for (uint64_t i = (uint64_t) blockIdx.x * tile + threadIdx.x; i < npk; i += stride) {
-        v4u acc[U];
+        v4u acc[U], b[U], nb[U];
 #pragma unroll
         for (int u = 0; u < U; ++u)
             if (i + u * nt < npk)
                 acc[u] = ld16<true>(vio + i + u * nt);
+        if (k > 0)
+            load(0, b, i);
         for (int q = 0; q < k; ++q) {
-            const v4u *__restrict__ vin = reinterpret_cast<const v4u *>(ins.p[q] + head);
-            v4u b[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (i + u * nt < npk)
-                    b[u] = ld16<true>(vin + i + u * nt);
+            if (q + 1 < k)
+                load(q + 1, nb, i);
 #pragma unroll
             for (int u = 0; u < U; ++u)
                 if (i + u * nt < npk)
                     acc[u] = combine16<C>(acc[u], b[u], prm);
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                b[u] = nb[u];
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -928,7 +939,7 @@ hipError_t launch_tree(const void *const *ins, int k, void *out, uint64_t count,
         uint64_t tail_start = head + npk * E;
         uint32_t ntail = (uint32_t) (count - tail_start);
         Params p = prm;
-        const unsigned grid = grid_for(k == 2 ? 256 * 4 : 256, npk, 0);
+        const unsigned grid = grid_for(k == 2 ? 256 * 4 : k <= 4 ? 256 * 2 : 256, npk, 0);
         // the store policy pays for the k = 2 form (+5 %); the 16-slot form
         // gains nothing at k = 4 / 8 / 16 (profiles/r03_tree_probe_policy.json)
         if (k == 2)
@@ -937,7 +948,10 @@ hipError_t launch_tree(const void *const *ins, int k, void *out, uint64_t count,
             if (k == 2)     // out = a OP b: the contiguous kernel's 4 packets per lane
                 hipLaunchKernelGGL((k_contig_tree<C, 2, 4>), dim3(grid), dim3(256), 0, s, mi, k,
                                    pres, tout, head, npk, tail_start, ntail, p);
-            else            // one 16-slot form for every k (an 8-slot form, more waves in
+            else if (k <= 4)    // 4 slots x 2 packets per lane: 8 loads in flight, as k_contig
+                hipLaunchKernelGGL((k_contig_tree<C, 4, 2>), dim3(grid), dim3(256), 0, s, mi, k,
+                                   pres, tout, head, npk, tail_start, ntail, p);
+            else            // one 16-slot form for k > 4 (an 8-slot form, more waves in
                             // flight, measured 4-9 % slower at k = 4 and 8)
                 hipLaunchKernelGGL((k_contig_tree<C, kMaxMulti, 1>), dim3(grid), dim3(256), 0, s,
                                    mi, k, pres, tout, head, npk, tail_start, ntail, p);
