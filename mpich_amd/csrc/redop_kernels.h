@@ -896,7 +896,7 @@ hipError_t launch_multi(const void *const *ins, int k, void *io, uint64_t count,
         uint64_t npk = (count - head) / E;
         uint64_t tail_start = head + npk * E;
         uint32_t ntail = (uint32_t) (count - tail_start);
-        constexpr int U = 2;
+        constexpr int U = 2;    // 4 measured no better (k = 1..15, tools/multi_probe.py)
         unsigned grid = grid_for((uint64_t) cfg.block * U, npk, cfg.max_grid);
         Params p = prm;
         set_store_policy(p, cfg, grid);
