@@ -328,8 +328,8 @@ int MPIX_Redop_set_fortran_booleans(int true_value, int false_value);
 /* ---- per-op function table, MPIR_op_function signature (mpir_op.h:206) ----
  * Synchronous; same pointer rules as MPIX_Reduce_local.  Only pairs that
  * MPIX_Redop_is_supported() accepts may be passed: the op functions return
- * void like the reference's, and a call that fails (a type no kernel covers,
- * e.g. MPI_LONG_DOUBLE, or a HIP error) prints the reason and abort()s, as
+ * void like the reference's, and a call that fails (a pair no kernel covers,
+ * e.g. MPI_MAX on MPIX_BFLOAT16, or a HIP error) prints the reason and abort()s, as
  * the reference's MPIR_Assert(0) does (op_fns.c:51-53).  With env
  * MPIX_REDOP_OPFN_ABORT=0 the failure is only recorded and can be read with
  * MPIX_Redop_last_error(). */
@@ -381,7 +381,10 @@ int MPIX_Reduce_local_batch_async(const void *const *inbufs, void *const *inoutb
  * threads per block and a cap on the grid (0 = one tile per block, no
  * grid-stride loop).  The packets-per-thread unroll is a compile-time
  * constant (MPIX_REDOP_UNROLL).  Env MPIX_REDOP_BLOCK / MPIX_REDOP_MAXGRID
- * override the defaults at first use. */
+ * override the defaults at first use.  Kernels that read page-locked host
+ * memory over PCIe (zero-copy) run at most 32 looping blocks unless max_grid
+ * is smaller, so loads and stores share the link both ways; env
+ * MPIX_REDOP_ZC_GRID sets that cap (0: none). */
 int MPIX_Redop_set_launch(int block_threads, int max_grid);
 int MPIX_Redop_get_launch(int *block_threads, int *unroll, int *max_grid);
 
