@@ -453,6 +453,18 @@ def load_pmc(path, count):
     return None, None
 
 
+def overlap_note(rccl):
+    """what the recursive-halving combine overlap does in this run
+    (libmpix_coll: on by default for RCCL communicators only)"""
+    env = os.environ.get('MPIX_COLL_RH_OVERLAP')
+    if env == '0' or (env is None and not rccl):
+        return 'off (%s)' % ('MPIX_COLL_RH_OVERLAP=0' if env == '0' else
+                             'the default of a non-RCCL communicator')
+    return ('each step\'s kept half combined on a second stream under the next exchange '
+            '(half-steps >= %s B); the step breakdown is of one call with it off'
+            % (env or str(1 << 20)))
+
+
 # ------------------------------------------------------------------ N = 1
 def reduce_local_leg(args, world, rank, dev):
     """the headline loop: synchronous MPIX_Reduce_local over 1 GiB operands,
@@ -1003,10 +1015,7 @@ def multi_gpu(args, world, rank, dev):
                     combine_overlap_checked=['every half-step split', 'none split'],
                     against='numpy restatement of the recursive-halving association'),
         schedule_ran=sched['schedule_ran'],
-        combine_overlap=('off' if os.environ.get('MPIX_COLL_RH_OVERLAP') == '0' else
-                         'each step\'s kept half combined on a second stream under the next '
-                         'exchange (half-steps >= %s B); the step breakdown is of one call '
-                         'with it off' % os.environ.get('MPIX_COLL_RH_OVERLAP', str(1 << 20))),
+        combine_overlap=overlap_note(os.environ.get('MPIX_BENCH_BACKEND', 'nccl') == 'nccl'),
         roofline={'bound': 'hbm', 'unit': 'GB/s',
                   'achieved': round(comb_gbs, 1) if comb_gbs else None, 'peak': HBM_PEAK_GBS,
                   'frac': round(comb_gbs / HBM_PEAK_GBS, 4) if comb_gbs else None,

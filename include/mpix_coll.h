@@ -115,13 +115,14 @@ int MPIX_Comm_free(MPIX_Comm comm);
  * (the communicator keeps a grow-only scratch) or at least
  * MPIX_Reduce_scatter_block_workspace() bytes of the buffers' memory kind. */
 #define MPIX_RSB_AUTO               0   /* generic.json: recursive halving < 512 KiB, else pairwise */
-#define MPIX_RSB_RECURSIVE_HALVING  1   /* on device communicators with P = 2^k >= 4 and
+#define MPIX_RSB_RECURSIVE_HALVING  1   /* on RCCL communicators with P = 2^k >= 4 and
                                            equal blocks, each step's combine is cut along
                                            the next step's split: the half sent next on the
                                            collective's stream, the half kept on a second
                                            stream under the next exchange (half-steps of
-                                           >= 1 MiB; MPIX_COLL_RH_OVERLAP=0 off, =N bytes);
-                                           same bits */
+                                           >= 1 MiB; env MPIX_COLL_RH_OVERLAP=N bytes sets
+                                           it for any device communicator, 0 off); same
+                                           bits */
 #define MPIX_RSB_PAIRWISE           2   /* the P-1 exchanges in ONE group + one multi-input combine */
 #define MPIX_RSB_PAIRWISE_SEQUENTIAL 3  /* the reference's loop: P-1 sendrecv + combine steps */
 #define MPIX_RSB_PAIRWISE_PIPELINED 4   /* PAIRWISE cut into 2..8 chunks (>= 4 MiB of the

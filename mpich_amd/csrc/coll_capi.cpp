@@ -666,16 +666,23 @@ int ensure_aux(MPIX_Comm c, size_t nev)
 }
 
 // Smallest half-step (bytes) whose combine recursive halving moves onto the
-// second stream (rs_recursive_halving_overlap); 0 = never.  MPIX_COLL_RH_OVERLAP
-// overrides: 0 switches the overlap off, N > 0 sets the bytes.
-size_t rh_overlap_min()
+// second stream (rs_recursive_halving_overlap); 0 = never.  By default 1 MiB
+// on RCCL communicators, where the exchange crosses xGMI links and the
+// combine has the HBM to itself, and off on the others: where the exchange is
+// a device copy on the same GPU (local communicators) the two compete for HBM
+// and the split only adds its launches and events -- 1.8 % (4 ranks) and
+// 5.8 % (8 ranks) slower on one GPU (tools/rh_overlap_probe.py,
+// profiles/r04_rh_overlap_probe.json).  MPIX_COLL_RH_OVERLAP overrides for
+// every communicator: 0 off, N > 0 the bytes.
+size_t rh_overlap_min(MPIX_Comm c)
 {
+    const size_t dflt = c->kind == K_CCL ? size_t(1) << 20 : 0;
     const char *e = getenv("MPIX_COLL_RH_OVERLAP");
     if (!e || !*e)
-        return size_t(1) << 20;
+        return dflt;
     char *end = nullptr;
     unsigned long long v = strtoull(e, &end, 10);
-    return (end && *end == '\0') ? (size_t) v : size_t(1) << 20;
+    return (end && *end == '\0') ? (size_t) v : dflt;
 }
 
 // The overlapped form applies to P a power of two >= 4 with equal blocks on a
@@ -689,7 +696,7 @@ bool rh_overlap_applies(MPIX_Comm c, const std::vector<size_t> &cnts, size_t ext
     for (size_t n : cnts)
         if (n != cnts[0])
             return false;
-    const size_t min = rh_overlap_min();
+    const size_t min = rh_overlap_min(c);
     // the first step's kept quarter is the largest half-step that can split
     return min && (size_t) (P / 4) * cnts[0] * ext >= min;
 }
@@ -710,7 +717,7 @@ int rs_recursive_halving_overlap(const char *sb, char *rb, size_t rc, MPIX_Datat
                                  MPIX_Op op, MPIX_Comm c, char *ws, hipStream_t s, size_t ext)
 {
     const int rank = c->rank, size = c->size;
-    const size_t total = rc * (size_t) size, blk = rc * ext, min = rh_overlap_min();
+    const size_t total = rc * (size_t) size, blk = rc * ext, min = rh_overlap_min(c);
     char *tmp_results = ws;
     char *tmp_recvbuf = ws + round256(total * ext);
     TRY(ensure_aux(c, 2));

@@ -580,7 +580,7 @@ def test_rsb_recursive_halving_pull_matches_oracle(oracle, P, dt, op, in_place):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('overlap', ['1', '0', 'default'])
+@pytest.mark.parametrize('overlap', ['1', '0', 'default', str(1 << 20)])
 @pytest.mark.parametrize('in_place', [False, True])
 @pytest.mark.parametrize('dt,op', [(MPI_FLOAT, MPI_SUM), (MPI_DOUBLE, MPI_MAX),
                                    (MPI_2INT, MPI_MAXLOC)])
@@ -589,20 +589,22 @@ def test_rsb_recursive_halving_overlap_matches_oracle(oracle, monkeypatch, P, dt
                                                       overlap):
     """recursive halving with each step's kept half combined on the second
     stream under the next exchange (MPIX_COLL_RH_OVERLAP=1: every half-step
-    splits; 0: none; default: half-steps of >= 1 MiB) is bit-identical to the
-    oracle's simulation of reduce_scatter_block_intra_recursive_halving.c --
-    NaN payloads and +-0 (double MAX) and MAXLOC ties show the operand roles;
-    the step labels show which combines ran split"""
+    splits; 2^20: half-steps of >= 1 MiB, the RCCL communicators' default; 0
+    and the default of these local communicators: none) is bit-identical to
+    the oracle's simulation of reduce_scatter_block_intra_recursive_halving.c
+    -- NaN payloads and +-0 (double MAX) and MAXLOC ties show the operand
+    roles; the step labels show which combines ran split"""
     import torch
     from mpich_amd import ccl
     if overlap == 'default':
         monkeypatch.delenv('MPIX_COLL_RH_OVERLAP', raising=False)
-        recvcount = (1 << 20) // oracle.extent(dt) + 5      # one block > 1 MiB
     else:
         monkeypatch.setenv('MPIX_COLL_RH_OVERLAP', overlap)
-        recvcount = 4099
-    if P == 16 and overlap == 'default':
-        recvcount //= 4
+    recvcount = 4099
+    if overlap == str(1 << 20):
+        recvcount = (1 << 20) // oracle.extent(dt) + 5      # one block > 1 MiB
+        if P == 16:
+            recvcount //= 4
     ext = oracle.extent(dt)
     rng = np.random.default_rng(0x5EED0900 + P)
     if dt == MPI_2INT:
@@ -632,7 +634,7 @@ def test_rsb_recursive_halving_overlap_matches_oracle(oracle, monkeypatch, P, dt
     for rc, phases in out:
         split = phases.count('combine (sent half)')
         assert split + phases.count('combine') == steps, phases
-        if overlap == '0':
+        if overlap in ('0', 'default'):
             assert split == 0, phases
         elif overlap == '1':
             assert split == steps - 1, phases
