@@ -589,13 +589,14 @@ __device__ __forceinline__ v4u swap_pair(v4u v)
 
 template <class C, int U, bool NTL, bool NTS>
 __global__ void __launch_bounds__(256)
-k_contig32(const typename C::unit *__restrict__ in, typename C::unit *__restrict__ io, uint64_t n,
+k_contig32(const typename C::unit *in, const typename C::unit *io, typename C::unit *out, uint64_t n,
            Params prm)
 {
     using T = typename C::unit;
     static_assert(sizeof(T) == 32, "32-byte units");
-    const v4u *__restrict__ vin = reinterpret_cast<const v4u *>(in);
-    v4u *__restrict__ vio = reinterpret_cast<v4u *>(io);
+    const v4u *vin = reinterpret_cast<const v4u *>(in);
+    const v4u *vio = reinterpret_cast<const v4u *>(io);     // the inout role (read)
+    v4u *vout = reinterpret_cast<v4u *>(out);               // io itself, or the tree's output
     const bool wt = wt_block(prm);
     auto f = [&](const Pk32 &a, const Pk32 &b) {
         return __builtin_bit_cast(Pk32, C::apply(__builtin_bit_cast(T, a),
@@ -631,8 +632,8 @@ k_contig32(const typename C::unit *__restrict__ in, typename C::unit *__restrict
             const Pk32 r = f(gather(a0[u], a1[u]), gather(b0[u], b1[u]));
             const v4u y = swap_pair(odd ? r.lo : r.hi);
             const uint64_t q = 2 * (t * tile + u * nt + wave * 64) + lane;
-            st16_pol<NTS>(vio + q, odd ? y : r.lo, wt);
-            st16_pol<NTS>(vio + q + 64, odd ? r.hi : y, wt);
+            st16_pol<NTS>(vout + q, odd ? y : r.lo, wt);
+            st16_pol<NTS>(vout + q + 64, odd ? r.hi : y, wt);
         }
     }
     // the last partial tile, a unit per lane
@@ -640,8 +641,8 @@ k_contig32(const typename C::unit *__restrict__ in, typename C::unit *__restrict
         for (uint64_t k = nfull * tile + threadIdx.x; k < n; k += nt) {
             const Pk32 r = f(Pk32{ld16<NTL>(vio + 2 * k), ld16<NTL>(vio + 2 * k + 1)},
                              Pk32{ld16<NTL>(vin + 2 * k), ld16<NTL>(vin + 2 * k + 1)});
-            st16_pol<NTS>(vio + 2 * k, r.lo, wt);
-            st16_pol<NTS>(vio + 2 * k + 1, r.hi, wt);
+            st16_pol<NTS>(vout + 2 * k, r.lo, wt);
+            st16_pol<NTS>(vout + 2 * k + 1, r.hi, wt);
         }
     }
 }
@@ -831,7 +832,7 @@ hipError_t launch_contig(const void *in, void *io, uint64_t count, const Params 
             p.done = nullptr;
             set_store_policy(p, cfg, grid);
             hipLaunchKernelGGL((k_contig32<C, U32, MPIX_REDOP_NT_LOAD, MPIX_REDOP_NT_STORE>),
-                               dim3(grid), dim3(kContig32Block), 0, s, tin, tio, count, p);
+                               dim3(grid), dim3(kContig32Block), 0, s, tin, tio, tio, count, p);
         } else {
             unsigned grid = grid_for((uint64_t) cfg.block * 4, count, cfg.max_grid);
             hipLaunchKernelGGL((k_elem<C>), dim3(grid), dim3(cfg.block), 0, s, tin, tio, count,
@@ -931,6 +932,24 @@ hipError_t launch_tree(const void *const *ins, int k, void *out, uint64_t count,
         aligned = aligned && ((reinterpret_cast<uintptr_t>(ins[q]) & 15) == (ao & 15));
     }
     T *tout = static_cast<T *>(out);
+    if constexpr (sizeof(T) > 16) {
+        // out = slot 0 OP slot 1 on 32-byte units, all three 16-byte aligned:
+        // k_contig32 with slot 0 in the inout role (recursive halving's
+        // combine_to); other shapes go element-wise below
+        if (k == 2 && pres == 3u &&
+            ((ao | reinterpret_cast<uintptr_t>(ins[0]) | reinterpret_cast<uintptr_t>(ins[1])) & 15) ==
+                0) {
+            constexpr int U32 = 2;
+            const unsigned grid = grid_for((uint64_t) kContig32Block * U32, count, cfg.max_grid);
+            Params p = prm;
+            p.done = nullptr;
+            set_store_policy(p, cfg, grid);
+            hipLaunchKernelGGL((k_contig32<C, U32, MPIX_REDOP_NT_LOAD, MPIX_REDOP_NT_STORE>),
+                               dim3(grid), dim3(kContig32Block), 0, s, mi.p[1], mi.p[0], tout, count,
+                               p);
+            return hipGetLastError();
+        }
+    }
     if (aligned) {
         uint64_t head = ((16 - (ao & 15)) & 15) / sizeof(T);
         if (head > count)

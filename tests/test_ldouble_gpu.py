@@ -261,3 +261,25 @@ def test_contig32_tiles_and_offsets(R, H, oracle, n, offs):
     # nothing outside the target span is written
     assert np.array_equal(got[:oo], guard[:oo]) and np.array_equal(got[oo + n * 32:],
                                                                    guard[oo + n * 32:])
+
+
+@pytest.mark.parametrize('n', [1, 511, 512, 1500, 20011])
+@pytest.mark.parametrize('target', ['separate', 'slot0', 'slot1'])
+def test_contig32_two_slot_tree(R, H, oracle, n, target):
+    """out = slot 0 OP slot 1 on MPI_LONG_DOUBLE_INT (recursive halving's
+    combine_to on 32-byte units): k_contig32 with slot 0 in the inout role,
+    into a separate output or in place over either slot; bit for bit with
+    the oracle's reduce_local(in = slot 1, inout = slot 0)"""
+    rng = np.random.default_rng(0x5EED0620 + n)
+    dt, op = H.MPI_LONG_DOUBLE_INT, H.MPI_MAXLOC
+    spec = np.stack(x87_specials())
+    A, B = loc_records(spec[rng.integers(0, len(spec), n)], spec[rng.integers(0, len(spec), n)],
+                       rng, 16)
+    exp = A.reshape(-1).copy()
+    assert oracle.reduce_local(B.reshape(-1).copy(), exp, n, dt, op) == 0
+    da, db = dev(A), dev(B)
+    out = {'separate': torch.zeros(n * 32, dtype=torch.uint8, device='cuda'), 'slot0': da,
+           'slot1': db}[target]
+    torch.cuda.synchronize()
+    assert R.reduce_local_tree_async([da, db], out, n, dt, op) == 0
+    assert np.array_equal(host(out), exp)
