@@ -12,6 +12,8 @@ ordering slip in a schedule changes the fp association or the MAXLOC winner.
 GPU: the same properties on the device transport with the HIP combine, P
 ranks as threads on cuda:0, counts large enough for the packet kernels.
 """
+import os
+
 import numpy as np
 import pytest
 from hypothesis import HealthCheck, given, settings
@@ -143,7 +145,8 @@ def test_scan_random(oracle, P, case, exclusive, count, in_place, seed):
         assert outs[r].tobytes() == exp[r].tobytes(), r
 
 
-GPU_SETTINGS = settings(max_examples=25, derandomize=True, deadline=None,
+GPU_SETTINGS = settings(max_examples=int(os.environ.get('MPIX_FUZZ_EXAMPLES_COLL', 25)),
+                        derandomize=True, deadline=None,
                         suppress_health_check=[HealthCheck.function_scoped_fixture,
                                                HealthCheck.too_slow])
 

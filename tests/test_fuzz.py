@@ -12,6 +12,8 @@ parity sweep, counts, byte offsets of both operands (packet, unaligned-load
 and element-wise kernels) and entry points (synchronous, stream-ordered,
 pinned and pageable host operands).
 """
+import os
+
 import numpy as np
 import pytest
 from hypothesis import HealthCheck, given, settings
@@ -111,7 +113,8 @@ def _sweep():
 
 
 @pytest.mark.gpu
-@settings(max_examples=300, derandomize=True, deadline=None,
+@settings(max_examples=int(os.environ.get('MPIX_FUZZ_EXAMPLES', 300)), derandomize=True,
+          deadline=None,
           suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
 @given(k=st.integers(0, 10 ** 6), n=st.one_of(st.integers(0, 2000), st.integers(2000, 70000)),
        off_io=st.integers(0, 3), off_in=st.integers(0, 3), sub=st.sampled_from([0, 0, 0, 1]),
