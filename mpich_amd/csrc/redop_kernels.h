@@ -590,7 +590,7 @@ __device__ __forceinline__ v4u swap_pair(v4u v)
 template <class C, int U, bool NTL, bool NTS>
 __global__ void __launch_bounds__(256)
 k_contig32(const typename C::unit *in, const typename C::unit *io, typename C::unit *out, uint64_t n,
-           Params prm)
+           Params prm, uint32_t nblk, uint32_t nthreads)
 {
     using T = typename C::unit;
     static_assert(sizeof(T) == 32, "32-byte units");
@@ -602,7 +602,7 @@ k_contig32(const typename C::unit *in, const typename C::unit *io, typename C::u
         return __builtin_bit_cast(Pk32, C::apply(__builtin_bit_cast(T, a),
                                                  __builtin_bit_cast(T, b), prm));
     };
-    const uint64_t nt = blockDim.x, tile = nt * U;       // units per tile
+    const uint64_t nt = nthreads, tile = nt * U;          // units per tile
     const uint64_t nfull = n / tile;
     const unsigned lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const bool odd = lane & 1;
@@ -611,7 +611,7 @@ k_contig32(const typename C::unit *in, const typename C::unit *io, typename C::u
         const v4u y = swap_pair(odd ? p0 : p1);
         return odd ? Pk32{y, p1} : Pk32{p0, y};
     };
-    for (uint64_t t = blockIdx.x; t < nfull; t += gridDim.x) {
+    for (uint64_t t = blockIdx.x; t < nfull; t += nblk) {
         v4u a0[U], a1[U], b0[U], b1[U];
         // run u of this wave: units [t*tile + u*nt + wave*64, +64) = packets from q
 #pragma unroll
@@ -637,7 +637,7 @@ k_contig32(const typename C::unit *in, const typename C::unit *io, typename C::u
         }
     }
     // the last partial tile, a unit per lane
-    if (blockIdx.x == nfull % gridDim.x) {
+    if (blockIdx.x == nfull % nblk) {
         for (uint64_t k = nfull * tile + threadIdx.x; k < n; k += nt) {
             const Pk32 r = f(Pk32{ld16<NTL>(vio + 2 * k), ld16<NTL>(vio + 2 * k + 1)},
                              Pk32{ld16<NTL>(vin + 2 * k), ld16<NTL>(vin + 2 * k + 1)});
@@ -832,7 +832,8 @@ hipError_t launch_contig(const void *in, void *io, uint64_t count, const Params 
             p.done = nullptr;
             set_store_policy(p, cfg, grid);
             hipLaunchKernelGGL((k_contig32<C, U32, MPIX_REDOP_NT_LOAD, MPIX_REDOP_NT_STORE>),
-                               dim3(grid), dim3(kContig32Block), 0, s, tin, tio, tio, count, p);
+                               dim3(grid), dim3(kContig32Block), 0, s, tin, tio, tio, count, p, grid,
+                               kContig32Block);
         } else {
             unsigned grid = grid_for((uint64_t) cfg.block * 4, count, cfg.max_grid);
             hipLaunchKernelGGL((k_elem<C>), dim3(grid), dim3(cfg.block), 0, s, tin, tio, count,
@@ -946,7 +947,7 @@ hipError_t launch_tree(const void *const *ins, int k, void *out, uint64_t count,
             set_store_policy(p, cfg, grid);
             hipLaunchKernelGGL((k_contig32<C, U32, MPIX_REDOP_NT_LOAD, MPIX_REDOP_NT_STORE>),
                                dim3(grid), dim3(kContig32Block), 0, s, mi.p[1], mi.p[0], tout, count,
-                               p);
+                               p, grid, kContig32Block);
             return hipGetLastError();
         }
     }

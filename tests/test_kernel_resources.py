@@ -23,8 +23,8 @@ READELF = '/opt/rocm/lib/llvm/bin/llvm-readelf'
 
 
 def _kernels(obj):
-    """[(name, vgpr_count, private_segment_fixed_size, kernarg_segment_size)] of the gfx950
-    code object in obj"""
+    """[(name, vgpr_count, private_segment_fixed_size, kernarg_segment_size or -1 when
+    the runtime's hidden arguments are part of it)] of the gfx950 code object in obj"""
     with tempfile.TemporaryDirectory() as d:
         src = os.path.join(d, os.path.basename(obj))
         shutil.copy(obj, src)
@@ -40,7 +40,8 @@ def _kernels(obj):
         p = re.search(r'\.private_segment_fixed_size:\s+(\d+)', b)
         k = re.search(r'\.kernarg_segment_size:\s+(\d+)', b)
         if m and v and p and k:
-            out.append((m.group(1), int(v.group(1)), int(p.group(1)), int(k.group(1))))
+            out.append((m.group(1), int(v.group(1)), int(p.group(1)),
+                        -1 if '.value_kind:     hidden_' in b else int(k.group(1))))
     return out
 
 
@@ -78,3 +79,8 @@ def test_contiguous_kernels_carry_no_hidden_arguments(kernels):
     contig = [(n, k) for n, _, _, k in kernels if n.startswith('_ZN4mpix8k_contig')]
     assert len(contig) >= 200
     assert max(k for _, k in contig) <= 128, max(contig, key=lambda x: x[1])
+    # -1: the metadata lists hidden_* arguments
+    for prefix in ('_ZN4mpix8k_contig', '_ZN4mpix10k_contig32', '_ZN4mpix7k_batch'):
+        ks = [(n, k) for n, _, _, k in kernels if n.startswith(prefix)]
+        assert ks, prefix
+        assert all(k >= 0 for _, k in ks), [n for n, k in ks if k < 0][:3]
