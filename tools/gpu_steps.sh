@@ -10,6 +10,7 @@
 #   floor                   tools/call_floor.py
 #   policy                  tools/policy_concurrent.py
 #   pgrid                   tools/pinned_grid.py: zero-copy calls against the grid cap
+#   pmcmulti                FETCH/WRITE passes over tools/multi_probe.py (multi-input and tree)
 #   bench                   the default bench.py line
 #   pmcwide                 tools/pmc_wide.py: FETCH/WRITE passes over the 32-byte-unit kernels
 #   evidence                tools/gpu_evidence.sh (R=r04): rocprofv3 stats + PMC passes + bench
@@ -47,6 +48,14 @@ for step in "$@"; do
         floor) run floor 200 python3 tools/call_floor.py || exit $? ;;
         policy) run policy 300 python3 tools/policy_concurrent.py || exit $? ;;
         pgrid) run pgrid 300 python3 tools/pinned_grid.py || exit $? ;;
+        pmcmulti) run pmcmulti_fetch 180 rocprofv3 --pmc FETCH_SIZE -T -d $O/pm_fetch -o f \
+                      --output-format csv -- python3 tools/multi_probe.py || exit $?
+                  run pmcmulti_write 180 rocprofv3 --pmc WRITE_SIZE -T -d $O/pm_write -o w \
+                      --output-format csv -- python3 tools/multi_probe.py || exit $?
+                  run pmcmulti_sum 60 python3 tools/pmc_multi.py \
+                      "$(find $O/pm_fetch -name '*counter_collection.csv' | head -n 1)" \
+                      "$(find $O/pm_write -name '*counter_collection.csv' | head -n 1)" \
+                      $O/r04_pmc_multi.json || exit $? ;;
         bench) run bench 600 python3 bench.py || exit $? ;;
         pmcwide) run pmcwide_run 120 python3 tools/pmc_wide.py || exit $?
                  run pmcwide_fetch 120 rocprofv3 --pmc FETCH_SIZE -T -d $O/pw_fetch -o f \
