@@ -587,31 +587,33 @@ __device__ __forceinline__ v4u swap_pair(v4u v)
     return r;
 }
 
+// Tile t (tile = nt * U units) of one 32-byte combine: a full tile through
+// the packet loads and the lane swap, the last partial tile a unit per lane.
+// Block-uniform: every lane of the block takes the same branch (the swap
+// needs whole waves).
 template <class C, int U, bool NTL, bool NTS>
-__global__ void __launch_bounds__(256)
-k_contig32(const typename C::unit *in, const typename C::unit *io, typename C::unit *out, uint64_t n,
-           Params prm, uint32_t nblk, uint32_t nthreads)
+__device__ __forceinline__ void contig32_tile(const typename C::unit *in, const typename C::unit *io,
+                                              typename C::unit *out, uint64_t n, uint64_t t,
+                                              uint64_t nt, bool wt, const Params &prm)
 {
     using T = typename C::unit;
     static_assert(sizeof(T) == 32, "32-byte units");
     const v4u *vin = reinterpret_cast<const v4u *>(in);
     const v4u *vio = reinterpret_cast<const v4u *>(io);     // the inout role (read)
     v4u *vout = reinterpret_cast<v4u *>(out);               // io itself, or the tree's output
-    const bool wt = wt_block(prm);
     auto f = [&](const Pk32 &a, const Pk32 &b) {
         return __builtin_bit_cast(Pk32, C::apply(__builtin_bit_cast(T, a),
                                                  __builtin_bit_cast(T, b), prm));
     };
-    const uint64_t nt = nthreads, tile = nt * U;          // units per tile
-    const uint64_t nfull = n / tile;
-    const unsigned lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const bool odd = lane & 1;
-    // the unit a lane holds after the swap: run unit lane/2 (even) or 32 + lane/2 (odd)
-    auto gather = [&](v4u p0, v4u p1) {
-        const v4u y = swap_pair(odd ? p0 : p1);
-        return odd ? Pk32{y, p1} : Pk32{p0, y};
-    };
-    for (uint64_t t = blockIdx.x; t < nfull; t += nblk) {
+    const uint64_t tile = nt * U;
+    if ((t + 1) * tile <= n) {
+        const unsigned lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        const bool odd = lane & 1;
+        // the unit a lane holds after the swap: run unit lane/2 (even) or 32 + lane/2 (odd)
+        auto gather = [&](v4u p0, v4u p1) {
+            const v4u y = swap_pair(odd ? p0 : p1);
+            return odd ? Pk32{y, p1} : Pk32{p0, y};
+        };
         v4u a0[U], a1[U], b0[U], b1[U];
         // run u of this wave: units [t*tile + u*nt + wave*64, +64) = packets from q
 #pragma unroll
@@ -635,16 +637,44 @@ k_contig32(const typename C::unit *in, const typename C::unit *io, typename C::u
             st16_pol<NTS>(vout + q, odd ? y : r.lo, wt);
             st16_pol<NTS>(vout + q + 64, odd ? r.hi : y, wt);
         }
-    }
-    // the last partial tile, a unit per lane
-    if (blockIdx.x == nfull % nblk) {
-        for (uint64_t k = nfull * tile + threadIdx.x; k < n; k += nt) {
+    } else {
+        for (uint64_t k = t * tile + threadIdx.x; k < n; k += nt) {
             const Pk32 r = f(Pk32{ld16<NTL>(vio + 2 * k), ld16<NTL>(vio + 2 * k + 1)},
                              Pk32{ld16<NTL>(vin + 2 * k), ld16<NTL>(vin + 2 * k + 1)});
             st16_pol<NTS>(vout + 2 * k, r.lo, wt);
             st16_pol<NTS>(vout + 2 * k + 1, r.hi, wt);
         }
     }
+}
+
+template <class C, int U, bool NTL, bool NTS>
+__global__ void __launch_bounds__(256)
+k_contig32(const typename C::unit *in, const typename C::unit *io, typename C::unit *out, uint64_t n,
+           Params prm, uint32_t nblk, uint32_t nthreads)
+{
+    const uint64_t tile = (uint64_t) nthreads * U;
+    const uint64_t ntiles = (n + tile - 1) / tile;
+    const bool wt = wt_block(prm);
+    for (uint64_t t = blockIdx.x; t < ntiles; t += nblk)
+        contig32_tile<C, U, NTL, NTS>(in, io, out, n, t, nthreads, wt, prm);
+}
+
+// The batch entry's form for 32-byte units: segment s owns blocks [blk0,
+// blk0 + its tiles), one tile each (BatchSeg::npk holds its count in units),
+// each tile combined as k_contig32 combines it.
+template <class C, int U, bool NTL, bool NTS>
+__global__ void __launch_bounds__(256)
+k_batch32(BatchTab tab, int nseg, Params prm, uint32_t nt)
+{
+    using T = typename C::unit;
+    const uint32_t b = blockIdx.x;
+    const uint32_t lane = threadIdx.x & 63;
+    const bool le = lane < (uint32_t) nseg && tab.blk0[lane] <= b;
+    const int q = __popcll(__ballot(le)) - 1;
+    const BatchSeg &g = tab.s[q];
+    contig32_tile<C, U, NTL, NTS>(static_cast<const T *>(g.in), static_cast<const T *>(g.io),
+                                  static_cast<T *>(g.io), g.npk, b - tab.blk0[q], nt,
+                                  wt_block(prm), prm);
 }
 
 // Vector target (typerep_op.c:115-150 for MPI_Type_vector(count, bl, stride)):
@@ -1036,13 +1066,48 @@ hipError_t launch_batch(const void *const *ins, void *const *ios, const uint64_t
     Params p = prm;
     p.done = nullptr;
     if constexpr (sizeof(T) > 16) {
-        for (int i = 0; i < k; ++i)
-            if (counts[i]) {
-                hipError_t e = launch_contig<C>(ins[i], ios[i], counts[i], p, cfg, s);
+        // 32-byte units: the 16-byte-aligned triples as one k_batch32 launch,
+        // the others element-wise one launch each
+        constexpr int U32 = 2;
+        const uint64_t tile = (uint64_t) kContig32Block * U32;
+        BatchTab tab;
+        int n = 0;
+        uint64_t blocks = 0;
+        auto flush = [&]() -> hipError_t {
+            if (!n)
+                return hipSuccess;
+            Params q = p;
+            set_store_policy(q, cfg, (unsigned) blocks);
+            hipLaunchKernelGGL((k_batch32<C, U32, MPIX_REDOP_NT_LOAD, MPIX_REDOP_NT_STORE>),
+                               dim3((unsigned) blocks), dim3(kContig32Block), 0, s, tab, n, q,
+                               kContig32Block);
+            n = 0;
+            blocks = 0;
+            return hipGetLastError();
+        };
+        for (int i = 0; i < k; ++i) {
+            const uint64_t count = counts[i];
+            if (!count)
+                continue;
+            if (((reinterpret_cast<uintptr_t>(ins[i]) | reinterpret_cast<uintptr_t>(ios[i])) & 15) !=
+                0) {
+                hipError_t e = launch_contig<C>(ins[i], ios[i], count, p, cfg, s);
+                if (e != hipSuccess)
+                    return e;
+                continue;
+            }
+            const uint64_t nb = (count + tile - 1) / tile;
+            if (blocks + nb > 0x7fffffffull) {
+                hipError_t e = flush();
                 if (e != hipSuccess)
                     return e;
             }
-        return hipSuccess;
+            tab.blk0[n] = (uint32_t) blocks;
+            tab.s[n] = BatchSeg{ins[i], ios[i], count, 0, 0, 1, {0, 0, 0, 0, 0}};
+            blocks += nb;
+            ++n;
+        }
+        return flush();
     } else {
         constexpr uint64_t E = 16 / sizeof(T);
         const uint64_t tile = (uint64_t) cfg.block * MPIX_REDOP_UNROLL;

@@ -7,7 +7,7 @@ mpidu_sched.c:309-316); the oracle checks every segment.
 CPU: the argument checks, all made before any device work.  GPU: random
 batches over every kind of combiner (packet kernel at equal and unequal
 16-byte phases, the element-wise fallback for operands that are not even
-element-aligned, the 32-byte pair loop, REPLACE), zero counts, k = 1 and
+element-aligned, the 32-byte units' own batch kernel, REPLACE), zero counts, k = 1 and
 k = MPIX_BATCH_MAX, a large segment spanning many blocks, and the bits of
 the same triples issued as separate calls."""
 import ctypes
@@ -78,7 +78,8 @@ def _layout(rng, k, ext, max_count, odd=False):
     ('MPI_FLOAT', 'MPI_SUM', False), ('MPI_FLOAT', 'MPI_SUM', True), ('MPI_INT8_T', 'MPI_LXOR', False),
     ('MPI_DOUBLE', 'MPI_MAX', False), ('MPI_2INT', 'MPI_MAXLOC', True),
     ('MPI_COMPLEX4', 'MPI_PROD', False), ('MPI_C_DOUBLE_COMPLEX', 'MPI_PROD', False),
-    ('MPI_LONG_DOUBLE_INT', 'MPI_MINLOC', False), ('MPI_INT64_T', 'MPI_REPLACE', False),
+    ('MPI_LONG_DOUBLE_INT', 'MPI_MINLOC', False), ('MPI_LONG_DOUBLE_INT', 'MPI_MINLOC', True),
+    ('MPI_C_LONG_DOUBLE_COMPLEX', 'MPI_SUM', False), ('MPI_INT64_T', 'MPI_REPLACE', False),
     ('MPIX_C_FLOAT16', 'MPI_SUM', True)])
 @pytest.mark.parametrize('k', [1, 7, 64])
 def test_batch_matches_oracle_and_single_calls(R, oracle, dtname, opname, odd, k):
