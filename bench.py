@@ -74,7 +74,7 @@ def parse(argv=None):
                    help='watchdog (s) over the N>1 secondary collective figures and teardown')
     p.add_argument('--value-timeout', type=float, default=600.0,
                    help='watchdog (s) over the N>1 value leg (bootstrap, parity check, timed steps)')
-    p.add_argument('--pmc', default=os.path.join(ROOT, 'profiles', 'r04_late_pmc_summary.json'),
+    p.add_argument('--pmc', default=os.path.join(ROOT, 'profiles', 'r04_final_pmc_summary.json'),
                    help='PMC traffic summary (from tools/pmc_summary.py) to quote as traffic')
     return p.parse_args(argv)
 
