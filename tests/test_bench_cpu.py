@@ -253,3 +253,19 @@ def test_multipath_allreduce_small_step_reported_as_plain(oracle):
     finally:
         for c in comms:
             c.free()
+
+
+def test_overlap_note_names_what_ran(monkeypatch):
+    """the N > 1 line says whether the recursive-halving combine overlap ran:
+    on by default for RCCL communicators only, off with MPIX_COLL_RH_OVERLAP=0,
+    and off, named as a parity failure, when the overlapped form failed"""
+    import bench
+    monkeypatch.delenv('MPIX_COLL_RH_OVERLAP', raising=False)
+    assert bench.overlap_note(True).startswith('each step')
+    assert '1048576 B' in bench.overlap_note(True)
+    assert bench.overlap_note(False) == 'off (the default of a non-RCCL communicator)'
+    assert 'failed the parity check' in bench.overlap_note(True, failed=True)
+    monkeypatch.setenv('MPIX_COLL_RH_OVERLAP', '0')
+    assert bench.overlap_note(True) == 'off (MPIX_COLL_RH_OVERLAP=0)'
+    monkeypatch.setenv('MPIX_COLL_RH_OVERLAP', '4096')
+    assert '4096 B' in bench.overlap_note(False)
