@@ -556,10 +556,10 @@ k_elem_tree(MultiIn<typename C::unit> ins, int k, uint32_t pres, typename C::uni
 template <class C>
 __global__ void __launch_bounds__(1024)
 k_elem(const typename C::unit *__restrict__ in, typename C::unit *__restrict__ io, uint64_t n,
-       Params prm)
+       Params prm, uint32_t nblk, uint32_t nt)
 {
-    const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    const uint64_t stride = (uint64_t) nblk * nt;
+    for (uint64_t i = (uint64_t) blockIdx.x * nt + threadIdx.x; i < n; i += stride)
         io[i] = C::apply(io[i], in[i], prm);
 }
 
@@ -685,10 +685,10 @@ k_batch32(BatchTab tab, int nseg, Params prm, uint32_t nt)
 template <class C>
 __global__ void __launch_bounds__(1024)
 k_vector(const typename C::unit *__restrict__ in, typename C::unit *__restrict__ io, uint64_t n,
-         uint64_t bl, uint64_t st, Params prm)
+         uint64_t bl, uint64_t st, Params prm, uint32_t nblk, uint32_t nt)
 {
-    const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
-    for (uint64_t j = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride) {
+    const uint64_t stride = (uint64_t) nblk * nt;
+    for (uint64_t j = (uint64_t) blockIdx.x * nt + threadIdx.x; j < n; j += stride) {
         uint64_t b = j / bl, k = j - b * bl;
         uint64_t t = b * st + k;
         io[t] = C::apply(io[t], in[j], prm);
@@ -699,10 +699,10 @@ k_vector(const typename C::unit *__restrict__ in, typename C::unit *__restrict__
 template <class C>
 __global__ void __launch_bounds__(1024)
 k_vector1(const typename C::unit *__restrict__ in, typename C::unit *__restrict__ io, uint64_t n,
-          uint64_t st, Params prm)
+          uint64_t st, Params prm, uint32_t nblk, uint32_t nt)
 {
-    const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
-    for (uint64_t j = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride)
+    const uint64_t stride = (uint64_t) nblk * nt;
+    for (uint64_t j = (uint64_t) blockIdx.x * nt + threadIdx.x; j < n; j += stride)
         io[j * st] = C::apply(io[j * st], in[j], prm);
 }
 
@@ -768,12 +768,12 @@ __device__ __forceinline__ T ld_source_nt(const T *p)
 template <class C>
 __global__ void __launch_bounds__(256)
 k_vector_s2(const typename C::unit *__restrict__ in, typename C::unit *__restrict__ io, uint64_t n,
-            Params prm)
+            Params prm, uint32_t nblk)
 {
     using T = typename C::unit;
     using R = typename RawOf<2 * sizeof(T)>::type;
-    const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
-    for (uint64_t j = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride) {
+    const uint64_t stride = (uint64_t) nblk * 256;        // 256-thread blocks (launch_vector)
+    for (uint64_t j = (uint64_t) blockIdx.x * 256 + threadIdx.x; j < n; j += stride) {
         T t;
         if (j + 1 < n) {
             R raw = reinterpret_cast<const R *>(io)[j];
@@ -796,10 +796,11 @@ template <class C>
 __global__ void __launch_bounds__(256)
 k_iov(const typename C::unit *__restrict__ in, typename C::unit *__restrict__ io,
       const int64_t *__restrict__ seg_off, const int64_t *__restrict__ prefix,
-      const int64_t *__restrict__ src_off, int64_t nseg, uint64_t total, Params prm)
+      const int64_t *__restrict__ src_off, int64_t nseg, uint64_t total, Params prm,
+      uint32_t nblk)
 {
-    const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
-    for (uint64_t j = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x; j < total; j += stride) {
+    const uint64_t stride = (uint64_t) nblk * 256;        // 256-thread blocks (launch_iov)
+    for (uint64_t j = (uint64_t) blockIdx.x * 256 + threadIdx.x; j < total; j += stride) {
         int64_t lo = 0, hi = nseg - 1;
         while (lo < hi) {               // last s with prefix[s] <= j
             int64_t mid = (lo + hi + 1) >> 1;
@@ -867,7 +868,7 @@ hipError_t launch_contig(const void *in, void *io, uint64_t count, const Params 
         } else {
             unsigned grid = grid_for((uint64_t) cfg.block * 4, count, cfg.max_grid);
             hipLaunchKernelGGL((k_elem<C>), dim3(grid), dim3(cfg.block), 0, s, tin, tio, count,
-                               prm);
+                               prm, grid, (uint32_t) cfg.block);
         }
     } else if ((ao % sizeof(T)) == 0 && (ai % sizeof(T)) == 0) {
         uint64_t head = ((16 - (ao & 15)) & 15) / sizeof(T);
@@ -897,7 +898,8 @@ hipError_t launch_contig(const void *in, void *io, uint64_t count, const Params 
                 grid, (uint32_t) cfg.block);
     } else {
         unsigned grid = grid_for((uint64_t) cfg.block * 4, count, cfg.max_grid);
-        hipLaunchKernelGGL((k_elem<C>), dim3(grid), dim3(cfg.block), 0, s, tin, tio, count, prm);
+        hipLaunchKernelGGL((k_elem<C>), dim3(grid), dim3(cfg.block), 0, s, tin, tio, count, prm,
+                           grid, (uint32_t) cfg.block);
     }
     hipError_t e = hipGetLastError();
     if (e == hipSuccess && prm.done && !signalled)
@@ -1028,15 +1030,19 @@ hipError_t launch_vector(const void *in, void *io, uint64_t count, uint64_t bl, 
     if constexpr (sizeof(T) <= 16)
         s2 = bl == 1 && st == 2 && (reinterpret_cast<uintptr_t>(io) % (2 * sizeof(T))) == 0;
     if (s2) {
-        if constexpr (sizeof(T) <= 16)
-            hipLaunchKernelGGL((k_vector_s2<C>), dim3(grid_for(256, n, cfg.max_grid)), dim3(256), 0,
-                               s, static_cast<const T *>(in), static_cast<T *>(io), n, prm);
+        if constexpr (sizeof(T) <= 16) {
+            const unsigned g2 = grid_for(256, n, cfg.max_grid);
+            hipLaunchKernelGGL((k_vector_s2<C>), dim3(g2), dim3(256), 0, s,
+                               static_cast<const T *>(in), static_cast<T *>(io), n, prm, g2);
+        }
     } else if (bl == 1)
         hipLaunchKernelGGL((k_vector1<C>), dim3(grid), dim3(cfg.block), 0, s,
-                           static_cast<const T *>(in), static_cast<T *>(io), n, st, prm);
+                           static_cast<const T *>(in), static_cast<T *>(io), n, st, prm, grid,
+                           (uint32_t) cfg.block);
     else
         hipLaunchKernelGGL((k_vector<C>), dim3(grid), dim3(cfg.block), 0, s,
-                           static_cast<const T *>(in), static_cast<T *>(io), n, bl, st, prm);
+                           static_cast<const T *>(in), static_cast<T *>(io), n, bl, st, prm, grid,
+                           (uint32_t) cfg.block);
     return hipGetLastError();
 }
 
@@ -1050,7 +1056,7 @@ hipError_t launch_iov(const void *in, void *io, const int64_t *d_seg_off, const 
         return hipSuccess;
     unsigned grid = grid_for(256ull * 4, total, cfg.max_grid);
     hipLaunchKernelGGL((k_iov<C>), dim3(grid), dim3(256), 0, s, static_cast<const T *>(in),
-                       static_cast<T *>(io), d_seg_off, d_prefix, d_src_off, nseg, total, prm);
+                       static_cast<T *>(io), d_seg_off, d_prefix, d_src_off, nseg, total, prm, grid);
     return hipGetLastError();
 }
 

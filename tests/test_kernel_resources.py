@@ -72,15 +72,18 @@ def test_contiguous_kernels_under_the_vgpr_cap(kernels):
 
 
 def test_contiguous_kernels_carry_no_hidden_arguments(kernels):
-    """k_contig (every single stream-ordered call) gets its grid and block
-    sizes as arguments: reading gridDim / blockDim would append the runtime's
-    hidden-argument block (360 instead of 112 bytes), written by the host on
-    every launch (bench.py call_floor_parts: up to 1 us per call)"""
+    """the kernels of single calls (contiguous, 32-byte, batch, element-wise,
+    vector and iov targets) get their grid and block sizes as arguments:
+    reading gridDim / blockDim would append the runtime's hidden-argument
+    block (k_contig: 360 instead of 112 bytes), written by the host on every
+    launch (bench.py call_floor_parts: up to 1 us per call)"""
     contig = [(n, k) for n, _, _, k in kernels if n.startswith('_ZN4mpix8k_contig')]
     assert len(contig) >= 200
     assert max(k for _, k in contig) <= 128, max(contig, key=lambda x: x[1])
     # -1: the metadata lists hidden_* arguments
-    for prefix in ('_ZN4mpix8k_contig', '_ZN4mpix10k_contig32', '_ZN4mpix7k_batch'):
+    for prefix in ('_ZN4mpix8k_contig', '_ZN4mpix10k_contig32', '_ZN4mpix7k_batch',
+                   '_ZN4mpix6k_elem', '_ZN4mpix8k_vector', '_ZN4mpix9k_vector1',
+                   '_ZN4mpix11k_vector_s2', '_ZN4mpix5k_iov'):
         ks = [(n, k) for n, _, _, k in kernels if n.startswith(prefix)]
         assert ks, prefix
         assert all(k >= 0 for _, k in ks), [n for n, k in ks if k < 0][:3]
