@@ -146,7 +146,7 @@ def test_scan_random(oracle, P, case, exclusive, count, in_place, seed):
 
 
 GPU_SETTINGS = settings(max_examples=int(os.environ.get('MPIX_FUZZ_EXAMPLES_COLL', 25)),
-                        derandomize=True, deadline=None,
+                        derandomize=not os.environ.get('MPIX_FUZZ_RANDOM'), deadline=None,
                         suppress_health_check=[HealthCheck.function_scoped_fixture,
                                                HealthCheck.too_slow])
 

@@ -113,8 +113,8 @@ def _sweep():
 
 
 @pytest.mark.gpu
-@settings(max_examples=int(os.environ.get('MPIX_FUZZ_EXAMPLES', 300)), derandomize=True,
-          deadline=None,
+@settings(max_examples=int(os.environ.get('MPIX_FUZZ_EXAMPLES', 300)),
+          derandomize=not os.environ.get('MPIX_FUZZ_RANDOM'), deadline=None,
           suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
 @given(k=st.integers(0, 10 ** 6), n=st.one_of(st.integers(0, 2000), st.integers(2000, 70000)),
        off_io=st.integers(0, 3), off_in=st.integers(0, 3), sub=st.sampled_from([0, 0, 0, 1]),
