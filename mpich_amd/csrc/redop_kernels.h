@@ -352,12 +352,13 @@ template <typename T> struct MultiIn {
 template <class C, int U>
 __global__ void __launch_bounds__(1024)
 k_contig_multi(MultiIn<typename C::unit> ins, int k, typename C::unit *__restrict__ io,
-               uint64_t head, uint64_t npk, uint64_t tail_start, uint32_t ntail, Params prm)
+               uint64_t head, uint64_t npk, uint64_t tail_start, uint32_t ntail, Params prm,
+               uint32_t nblk, uint32_t nthreads)
 {
     v4u *__restrict__ vio = reinterpret_cast<v4u *>(io + head);
-    const uint64_t nt = blockDim.x;
+    const uint64_t nt = nthreads;
     const uint64_t tile = nt * U;
-    const uint64_t stride = (uint64_t) gridDim.x * tile;
+    const uint64_t stride = (uint64_t) nblk * tile;
     const bool wt = wt_block(prm);
     // input q + 1's packets are loaded before input q's are combined, so two
     // inputs' worth stay in flight through the fold (one at a time: 5.86 TB/s
@@ -412,10 +413,10 @@ k_contig_multi(MultiIn<typename C::unit> ins, int k, typename C::unit *__restric
 template <class C>
 __global__ void __launch_bounds__(1024)
 k_elem_multi(MultiIn<typename C::unit> ins, int k, typename C::unit *__restrict__ io, uint64_t n,
-             Params prm)
+             Params prm, uint32_t nblk, uint32_t nt)
 {
-    const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint64_t stride = (uint64_t) nblk * nt;
+    for (uint64_t i = (uint64_t) blockIdx.x * nt + threadIdx.x; i < n; i += stride) {
         typename C::unit a = io[i];
         for (int q = 0; q < k; ++q)
             a = C::apply(a, ins.p[q][i], prm);
@@ -456,12 +457,13 @@ __device__ __forceinline__ void tree_fold(V *v, int k, uint32_t pres, F f)
 template <class C, int KMAX, int U>
 __global__ void __launch_bounds__(256)
 k_contig_tree(MultiIn<typename C::unit> ins, int k, uint32_t pres, typename C::unit *__restrict__ out,
-              uint64_t head, uint64_t npk, uint64_t tail_start, uint32_t ntail, Params prm)
+              uint64_t head, uint64_t npk, uint64_t tail_start, uint32_t ntail, Params prm,
+              uint32_t nblk)
 {
     using T = typename C::unit;
     v4u *vout = reinterpret_cast<v4u *>(out + head);
-    const uint64_t nt = blockDim.x;
-    const uint64_t stride = (uint64_t) gridDim.x * nt * U;
+    const uint64_t nt = 256;                                // launch_tree's block
+    const uint64_t stride = (uint64_t) nblk * nt * U;
     auto cv = [&](v4u a, v4u b) { return combine16<C>(a, b, prm); };
     auto ce = [&](T a, T b) { return C::apply(a, b, prm); };
     const bool wt = wt_block(prm);
@@ -491,9 +493,9 @@ k_contig_tree(MultiIn<typename C::unit> ins, int k, uint32_t pres, typename C::u
             tree_fold<KMAX>(v, k, pres, ce);
             out[t] = v[0];
         };
-        for (uint64_t t = threadIdx.x; t < head; t += blockDim.x)
+        for (uint64_t t = threadIdx.x; t < head; t += nt)
             one(t);
-        for (uint64_t t = threadIdx.x; t < ntail; t += blockDim.x)
+        for (uint64_t t = threadIdx.x; t < ntail; t += nt)
             one(tail_start + t);
     }
 }
@@ -530,12 +532,12 @@ __device__ __forceinline__ bool tree_fold_rec(T &out, int k, uint32_t pres, L &l
 template <class C>
 __global__ void __launch_bounds__(256)
 k_elem_tree(MultiIn<typename C::unit> ins, int k, uint32_t pres, typename C::unit *__restrict__ out,
-            uint64_t n, Params prm)
+            uint64_t n, Params prm, uint32_t nblk)
 {
     using T = typename C::unit;
     auto ce = [&](T a, T b) { return C::apply(a, b, prm); };
-    const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
-    for (uint64_t t = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x; t < n; t += stride) {
+    const uint64_t stride = (uint64_t) nblk * 256;        // launch_tree's block
+    for (uint64_t t = (uint64_t) blockIdx.x * 256 + threadIdx.x; t < n; t += stride) {
         if constexpr (sizeof(T) > 16) {
             auto load = [&](int q) { return ins.p[q][t]; };
             T r;
@@ -936,11 +938,11 @@ hipError_t launch_multi(const void *const *ins, int k, void *io, uint64_t count,
         set_store_policy(p, cfg, grid);
         if constexpr (sizeof(T) <= 16)
             hipLaunchKernelGGL((k_contig_multi<C, U>), dim3(grid), dim3(cfg.block), 0, s, mi, k,
-                               tio, head, npk, tail_start, ntail, p);
+                               tio, head, npk, tail_start, ntail, p, grid, (uint32_t) cfg.block);
     } else {
         unsigned grid = grid_for((uint64_t) cfg.block * 4, count, cfg.max_grid);
         hipLaunchKernelGGL((k_elem_multi<C>), dim3(grid), dim3(cfg.block), 0, s, mi, k, tio, count,
-                           prm);
+                           prm, grid, (uint32_t) cfg.block);
     }
     return hipGetLastError();
 }
@@ -999,18 +1001,19 @@ hipError_t launch_tree(const void *const *ins, int k, void *out, uint64_t count,
         if constexpr (sizeof(T) <= 16) {
             if (k == 2)     // out = a OP b: the contiguous kernel's 4 packets per lane
                 hipLaunchKernelGGL((k_contig_tree<C, 2, 4>), dim3(grid), dim3(256), 0, s, mi, k,
-                                   pres, tout, head, npk, tail_start, ntail, p);
+                                   pres, tout, head, npk, tail_start, ntail, p, grid);
             else if (k <= 4)    // 4 slots x 2 packets per lane: 8 loads in flight, as k_contig
                 hipLaunchKernelGGL((k_contig_tree<C, 4, 2>), dim3(grid), dim3(256), 0, s, mi, k,
-                                   pres, tout, head, npk, tail_start, ntail, p);
+                                   pres, tout, head, npk, tail_start, ntail, p, grid);
             else            // one 16-slot form for k > 4 (an 8-slot form, more waves in
                             // flight, measured 4-9 % slower at k = 4 and 8)
                 hipLaunchKernelGGL((k_contig_tree<C, kMaxMulti, 1>), dim3(grid), dim3(256), 0, s,
-                                   mi, k, pres, tout, head, npk, tail_start, ntail, p);
+                                   mi, k, pres, tout, head, npk, tail_start, ntail, p, grid);
         }
     } else {
-        hipLaunchKernelGGL((k_elem_tree<C>), dim3(grid_for(256 * 4, count, 0)), dim3(256), 0, s,
-                           mi, k, pres, tout, count, prm);
+        const unsigned ge = grid_for(256 * 4, count, 0);
+        hipLaunchKernelGGL((k_elem_tree<C>), dim3(ge), dim3(256), 0, s, mi, k, pres, tout, count,
+                           prm, ge);
     }
     return hipGetLastError();
 }
