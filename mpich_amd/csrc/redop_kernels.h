@@ -457,13 +457,14 @@ __device__ __forceinline__ void tree_fold(V *v, int k, uint32_t pres, F f)
 template <class C, int KMAX, int U>
 __global__ void __launch_bounds__(256)
 k_contig_tree(MultiIn<typename C::unit> ins, int k, uint32_t pres, typename C::unit *__restrict__ out,
-              uint64_t head, uint64_t npk, uint64_t tail_start, uint32_t ntail, Params prm,
-              uint32_t nblk)
+              uint64_t head, uint64_t npk, uint64_t tail_start, uint32_t ntail, Params prm)
 {
     using T = typename C::unit;
     v4u *vout = reinterpret_cast<v4u *>(out + head);
-    const uint64_t nt = 256;                                // launch_tree's block
-    const uint64_t stride = (uint64_t) nblk * nt * U;
+    // gridDim / blockDim kept here: the same kernel with the sizes as
+    // arguments measured 2.5 % slower at k = 4 and 8 (tools/multi_probe.py)
+    const uint64_t nt = blockDim.x;
+    const uint64_t stride = (uint64_t) gridDim.x * nt * U;
     auto cv = [&](v4u a, v4u b) { return combine16<C>(a, b, prm); };
     auto ce = [&](T a, T b) { return C::apply(a, b, prm); };
     const bool wt = wt_block(prm);
@@ -532,12 +533,12 @@ __device__ __forceinline__ bool tree_fold_rec(T &out, int k, uint32_t pres, L &l
 template <class C>
 __global__ void __launch_bounds__(256)
 k_elem_tree(MultiIn<typename C::unit> ins, int k, uint32_t pres, typename C::unit *__restrict__ out,
-            uint64_t n, Params prm, uint32_t nblk)
+            uint64_t n, Params prm)
 {
     using T = typename C::unit;
     auto ce = [&](T a, T b) { return C::apply(a, b, prm); };
-    const uint64_t stride = (uint64_t) nblk * 256;        // launch_tree's block
-    for (uint64_t t = (uint64_t) blockIdx.x * 256 + threadIdx.x; t < n; t += stride) {
+    const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
+    for (uint64_t t = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x; t < n; t += stride) {
         if constexpr (sizeof(T) > 16) {
             auto load = [&](int q) { return ins.p[q][t]; };
             T r;
@@ -1001,19 +1002,18 @@ hipError_t launch_tree(const void *const *ins, int k, void *out, uint64_t count,
         if constexpr (sizeof(T) <= 16) {
             if (k == 2)     // out = a OP b: the contiguous kernel's 4 packets per lane
                 hipLaunchKernelGGL((k_contig_tree<C, 2, 4>), dim3(grid), dim3(256), 0, s, mi, k,
-                                   pres, tout, head, npk, tail_start, ntail, p, grid);
+                                   pres, tout, head, npk, tail_start, ntail, p);
             else if (k <= 4)    // 4 slots x 2 packets per lane: 8 loads in flight, as k_contig
                 hipLaunchKernelGGL((k_contig_tree<C, 4, 2>), dim3(grid), dim3(256), 0, s, mi, k,
-                                   pres, tout, head, npk, tail_start, ntail, p, grid);
+                                   pres, tout, head, npk, tail_start, ntail, p);
             else            // one 16-slot form for k > 4 (an 8-slot form, more waves in
                             // flight, measured 4-9 % slower at k = 4 and 8)
                 hipLaunchKernelGGL((k_contig_tree<C, kMaxMulti, 1>), dim3(grid), dim3(256), 0, s,
-                                   mi, k, pres, tout, head, npk, tail_start, ntail, p, grid);
+                                   mi, k, pres, tout, head, npk, tail_start, ntail, p);
         }
     } else {
-        const unsigned ge = grid_for(256 * 4, count, 0);
-        hipLaunchKernelGGL((k_elem_tree<C>), dim3(ge), dim3(256), 0, s, mi, k, pres, tout, count,
-                           prm, ge);
+        hipLaunchKernelGGL((k_elem_tree<C>), dim3(grid_for(256 * 4, count, 0)), dim3(256), 0, s,
+                           mi, k, pres, tout, count, prm);
     }
     return hipGetLastError();
 }
