@@ -74,6 +74,10 @@ def parse(argv=None):
                    help='watchdog (s) over the N>1 secondary collective figures and teardown')
     p.add_argument('--value-timeout', type=float, default=600.0,
                    help='watchdog (s) over the N>1 value leg (bootstrap, parity check, timed steps)')
+    p.add_argument('--no-ab', action='store_true',
+                   help='N>1: skip the interleaved A/B of the overlap and store-policy defaults')
+    p.add_argument('--ab-reps', type=int, default=3, help='N>1 defaults A/B: calls per variant')
+    p.add_argument('--ab-rounds', type=int, default=2, help='N>1 defaults A/B: interleaved passes')
     p.add_argument('--pmc', default=os.path.join(ROOT, 'profiles', 'r04_final_pmc_summary.json'),
                    help='PMC traffic summary (from tools/pmc_summary.py) to quote as traffic')
     return p.parse_args(argv)
@@ -453,18 +457,14 @@ def load_pmc(path, count):
     return None, None
 
 
-def overlap_note(rccl, failed=False):
-    """what the recursive-halving combine overlap does in this run
-    (libmpix_coll: on by default for RCCL communicators only)"""
-    if failed:
-        return 'off: the overlapped form failed the parity check in this run (parity.combine_overlap_failed)'
-    env = os.environ.get('MPIX_COLL_RH_OVERLAP')
-    if env == '0' or (env is None and not rccl):
-        return 'off (%s)' % ('MPIX_COLL_RH_OVERLAP=0' if env == '0' else
-                             'the default of a non-RCCL communicator')
+def overlap_note(min_bytes):
+    """what the recursive-halving combine overlap does in this run's timed
+    calls (libmpix_coll: MPIX_Comm_get_rh_overlap of the communicator; on by
+    default -- 1 MiB -- for RCCL communicators only)"""
+    if not min_bytes:
+        return 'off (every combine whole on the collective\'s stream)'
     return ('each step\'s kept half combined on a second stream under the next exchange '
-            '(half-steps >= %s B); the step breakdown is of one call with it off'
-            % (env or str(1 << 20)))
+            '(half-steps >= %d B); the step breakdown is of one call with it off' % min_bytes)
 
 
 # ------------------------------------------------------------------ N = 1
@@ -929,23 +929,19 @@ def multi_gpu(args, world, rank, dev):
     total = (args.rsb_bytes // 4) // world * world
     recvcount = total // world
     # parity before timing: fp32 SUM at a reduced size, bit for bit against
-    # the schedule's association restated in numpy on every rank
-    # checked twice: with every half-step's combine split onto the second
-    # stream (MPIX_COLL_RH_OVERLAP=1, the form the timed 4 GiB calls take at
-    # P = 2^k >= 4) and with none split
+    # the schedule's association restated in numpy on every rank, checked
+    # with every half-step's combine split onto the second stream (overlap
+    # threshold 1 byte) and with none split (0).  A failure in either form
+    # fails the run: the shipped default must never be timed unchecked.
+    shipped_overlap = cc.rh_overlap()
     rc_small = (1 << 16) + 3
     sends = [rsb_inputs_host(r, world, rc_small) for r in range(world)]
     ds = torch.from_numpy(sends[rank]).to(dev)
     dr = torch.empty(rc_small, dtype=torch.float32, device=dev)
     expected = rh_expected_block(sends, rank, rc_small).tobytes()
-    # A failure with the overlap on (and not off) is reported in the line and
-    # the timed calls then run with it off: the schedule's curve is kept, the
-    # overlap's fault stays visible; a failure with it off ends the leg.
-    overlap_env = os.environ.get('MPIX_COLL_RH_OVERLAP')
-    overlap_failed = False
     try:
-        for mode in ('1', '0'):
-            os.environ['MPIX_COLL_RH_OVERLAP'] = mode
+        for mode in (1, 0):
+            cc.set_rh_overlap(mode)
             dr.fill_(float('nan'))
             redop.check(ccl.reduce_scatter_block(ds, dr, rc_small, H.MPI_FLOAT, H.MPI_SUM, cc,
                                                  'recursive_halving'), 'MPIX_Reduce_scatter_block')
@@ -953,20 +949,12 @@ def multi_gpu(args, world, rank, dev):
             if 'error' in sched:
                 raise RuntimeError('value leg: recursive halving requested, ' + sched['error'])
             ok = dr.cpu().numpy().tobytes() == expected
-            ok_all = allreduce_scalar(1.0 if ok else 0.0, dist.ReduceOp.MIN, dev) == 1.0
-            if not ok_all and mode == '1':
-                overlap_failed = True
-            elif not ok_all:
-                raise RuntimeError('recursive-halving RSB over RCCL differs from the reference '
-                                   'association (fp32 SUM, recvcount %d, overlap off) on some rank'
-                                   % rc_small)
+            if allreduce_scalar(1.0 if ok else 0.0, dist.ReduceOp.MIN, dev) != 1.0:
+                raise RuntimeError('recursive-halving RSB differs from the reference association '
+                                   '(fp32 SUM, recvcount %d, combine overlap %s) on some rank'
+                                   % (rc_small, 'on every half-step' if mode else 'off'))
     finally:
-        if overlap_env is None:
-            os.environ.pop('MPIX_COLL_RH_OVERLAP', None)
-        else:
-            os.environ['MPIX_COLL_RH_OVERLAP'] = overlap_env
-    if overlap_failed:
-        os.environ['MPIX_COLL_RH_OVERLAP'] = '0'
+        cc.set_rh_overlap(shipped_overlap)
     del ds, dr, sends
 
     send = torch.empty(total, dtype=torch.float32, device=dev)
@@ -999,17 +987,14 @@ def multi_gpu(args, world, rank, dev):
     # per-step breakdown on rank 0's stream, of one extra
     # call with the combine overlap off (every combine whole on the collective's
     # stream, so its marks bracket the combine kernel alone; same bits)
-    overlap_env = os.environ.get('MPIX_COLL_RH_OVERLAP')
-    os.environ['MPIX_COLL_RH_OVERLAP'] = '0'
+    cc.set_rh_overlap(0)
     cc.set_step_timing(True)
     step()
     torch.cuda.synchronize()
     cc.set_step_timing(False)
-    if overlap_env is None:
-        del os.environ['MPIX_COLL_RH_OVERLAP']
-    else:
-        os.environ['MPIX_COLL_RH_OVERLAP'] = overlap_env
+    cc.set_rh_overlap(shipped_overlap)
     steps = cc.step_times()
+    ab = None if args.no_ab else defaults_ab(cc, step, recv, dev, args.ab_reps, args.ab_rounds)
     comb_ms = sum(s['ms'] for s in steps if s['phase'] == 'combine')
     exch_ms = sum(s['ms'] for s in steps if s['phase'] == 'exchange')
     combined = (pof2 - 1) / pof2 * total            # elements this rank combined (pof2 ranks)
@@ -1021,13 +1006,11 @@ def multi_gpu(args, world, rank, dev):
                             '4 GiB vector per rank, recursive halving, RCCL/xGMI chunk transport',
                 'vector_bytes_per_rank': total * 4, 'recvcount': recvcount,
                 'parallelism': 'rsb%d (one rank per GPU, libmpix_coll over RCCL)' % world},
-        parity=dict(checked=True, recvcount=rc_small, bit_exact_all_ranks=not overlap_failed,
+        parity=dict(checked=True, recvcount=rc_small, bit_exact_all_ranks=True,
                     combine_overlap_checked=['every half-step split', 'none split'],
-                    combine_overlap_failed=overlap_failed,
                     against='numpy restatement of the recursive-halving association'),
         schedule_ran=sched['schedule_ran'],
-        combine_overlap=overlap_note(os.environ.get('MPIX_BENCH_BACKEND', 'nccl') == 'nccl',
-                                     overlap_failed),
+        combine_overlap=overlap_note(shipped_overlap),
         roofline={'bound': 'hbm', 'unit': 'GB/s',
                   'achieved': round(comb_gbs, 1) if comb_gbs else None, 'peak': HBM_PEAK_GBS,
                   'frac': round(comb_gbs / HBM_PEAK_GBS, 4) if comb_gbs else None,
@@ -1040,10 +1023,76 @@ def multi_gpu(args, world, rank, dev):
                            'note': 'bytes a rank receives over its one active link across the '
                                    'log2(P) steps / step time'}},
         steps_rank0=steps,
-        step_split_rank0=dict(exchange_ms=round(exch_ms, 3), combine_ms=round(comb_ms, 3)))
+        step_split_rank0=dict(exchange_ms=round(exch_ms, 3), combine_ms=round(comb_ms, 3)),
+        defaults_ab=ab)
     del send, recv, ws
     torch.cuda.empty_cache()
     return result
+
+
+AB_VARIANTS = ('overlap_on_policy_on', 'overlap_off_policy_on', 'overlap_on_policy_off',
+               'overlap_off_policy_off')
+
+
+def defaults_ab(cc, step, recv, dev, reps=3, rounds=2):
+    """The value leg's two defaults that no earlier run could measure, timed
+    against their alternatives on the same buffers, interleaved: the
+    recursive-halving combine overlap (1 MiB half-steps and up, the RCCL
+    communicators' default, vs off) x libmpix_redop's store policy (the
+    default XCD write-through mask vs all non-temporal stores).  Every variant
+    first runs one untimed call whose result must equal, bit for bit on every
+    rank, the result of the shipped default's timed calls (same association,
+    so the same bits); then `reps` calls between barrier + synchronize, max
+    over ranks.  `rounds` passes, the order rotated each pass; ms_per_step is
+    the median over the passes.  The line's `value` stays on the shipped
+    default; this only says whether the defaults gain or cost."""
+    ref = recv.clone()
+    torch.cuda.synchronize()
+    shipped_overlap = cc.rh_overlap()
+    pol = redop.get_store_policy()
+    pol_on = pol['xcd_mask'] if pol['xcd_mask'] > 0 else 0x88
+    setting = {'overlap_on_policy_on': (1 << 20, pol_on), 'overlap_off_policy_on': (0, pol_on),
+               'overlap_on_policy_off': (1 << 20, 0), 'overlap_off_policy_off': (0, 0)}
+    times = {k: [] for k in AB_VARIANTS}
+    parity = {}
+    try:
+        for rnd in range(rounds):
+            order = AB_VARIANTS[rnd % 4:] + AB_VARIANTS[:rnd % 4]
+            for name in order:
+                ov, mask = setting[name]
+                cc.set_rh_overlap(ov)
+                redop.check(redop.set_store_policy(mask, 0, 0, 0), 'MPIX_Redop_set_store_policy')
+                recv.fill_(float('nan'))
+                step()
+                torch.cuda.synchronize()
+                same = bool(torch.equal(recv.view(torch.int32), ref.view(torch.int32)))
+                if not allreduce_scalar(1.0 if same else 0.0, dist.ReduceOp.MIN, dev):
+                    raise RuntimeError('defaults A/B: %s differs from the shipped default\'s bits '
+                                       'on some rank' % name)
+                parity[name] = True
+                dist.barrier()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(reps):
+                    step()
+                torch.cuda.synchronize()
+                dist.barrier()
+                times[name].append(allreduce_scalar(time.perf_counter() - t0, dist.ReduceOp.MAX,
+                                                    dev) / reps)
+    finally:
+        cc.set_rh_overlap(shipped_overlap)
+        redop.set_store_policy(pol['xcd_mask'], pol['every'], pol['phase'], pol['tail_blocks'])
+    shipped = '%s_%s' % ('overlap_on' if shipped_overlap else 'overlap_off',
+                         'policy_on' if pol['xcd_mask'] > 0 else 'policy_off')
+    out = {k: dict(ms_per_step=round(1e3 * float(np.median(v)), 4),
+                   ms_each_round=[round(1e3 * x, 4) for x in v],
+                   bit_identical_to_shipped_all_ranks=parity.get(k, False))
+           for k, v in times.items()}
+    best = min(AB_VARIANTS, key=lambda k: out[k]['ms_per_step'])
+    out.update(shipped=shipped, fastest=best, reps=reps, rounds=rounds,
+               overlap_bytes={'on': 1 << 20, 'off': 0}, store_policy_xcd_mask={'on': pol_on, 'off': 0},
+               note='value leg calls, interleaved, order rotated per round; median over rounds')
+    return out
 
 
 def _no_shared(e):
@@ -1310,14 +1359,33 @@ def world_plan(args, env=None):
     return ('launch', n) if n > 1 else ('single', 1)
 
 
-def check_devices(world, env=None):
+def count_devices(env=None):
+    """GPUs the ranks will see, counted in a short-lived child process: the
+    launcher parent must stay off the GPU (it starts the ranks with
+    subprocess, and a process that initialised HIP must not be the one that
+    outlives them), and torch.cuda.device_count() may initialise the HIP
+    runtime -- it does whenever amdsmi cannot enumerate and it falls back to
+    hipGetDeviceCount.  The child inherits `env`, so HIP_VISIBLE_DEVICES and
+    its relatives count as they will in the ranks.  0 if the child fails."""
+    import subprocess
+    env = os.environ if env is None else env
+    try:
+        p = subprocess.run([sys.executable, '-c', 'import torch; print(torch.cuda.device_count())'],
+                           env=dict(env), capture_output=True, text=True, timeout=300)
+        return int(p.stdout.strip().splitlines()[-1]) if p.returncode == 0 else 0
+    except (OSError, ValueError, IndexError, subprocess.TimeoutExpired):
+        return 0
+
+
+def check_devices(world, env=None, launcher=True):
     """one GPU per rank, unless the 1-GPU rehearsal knob shares device 0 (or
-    the dry run touches none); torch.cuda.device_count() does not initialise
-    the HIP runtime on this image"""
+    the dry run touches none).  The launcher counts through count_devices, so
+    it never initialises HIP (tests/test_launcher_gpu.py checks that on a
+    GPU); a rank under an external launcher is about to use its GPU anyway"""
     env = os.environ if env is None else env
     if env.get('MPIX_BENCH_SAME_DEVICE') == '1':
         return
-    have = torch.cuda.device_count()
+    have = count_devices(env) if launcher else torch.cuda.device_count()
     if have < world:
         raise SystemExit('bench.py: %d ranks need %d GPUs, this node shows %d' % (world, world, have))
 
@@ -1410,6 +1478,7 @@ def dry_run(world, rank):
     if rank == 0:
         print(json.dumps({'metric': METRIC_RSB if world > 1 else METRIC, 'value': None,
                           'n_gpus': world, 'ranks_seen': seen, 'dry_run': True,
+                          'defaults_ab': ({k: None for k in AB_VARIANTS} if world > 1 else None),
                           'launcher': 'bench.py' if os.environ.get('MPIX_BENCH_LAUNCHED')
                           else ('external' if world > 1 else None)}), flush=True)
     if world > 1:
@@ -1421,8 +1490,8 @@ def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse(argv)
     mode, world = world_plan(args)
-    if not args.dry_run:
-        check_devices(world)
+    if not args.dry_run and world > 1:
+        check_devices(world, launcher=mode == 'launch')
     if mode == 'launch':
         return launch_ranks(world, argv)
     rank = int(os.environ.get('RANK', '0'))

@@ -120,7 +120,8 @@ int MPIX_Comm_free(MPIX_Comm comm);
                                            the next step's split: the half sent next on the
                                            collective's stream, the half kept on a second
                                            stream under the next exchange (half-steps of
-                                           >= 1 MiB; env MPIX_COLL_RH_OVERLAP=N bytes sets
+                                           >= 1 MiB; MPIX_Comm_set_rh_overlap, or env
+                                           MPIX_COLL_RH_OVERLAP=N bytes at creation, sets
                                            it for any device communicator, 0 off); same
                                            bits */
 #define MPIX_RSB_PAIRWISE           2   /* the P-1 exchanges in ONE group + one multi-input combine */
@@ -268,6 +269,17 @@ int MPIX_Comm_set_stream(MPIX_Comm comm, void *stream);
  * on RCCL communicators (no count reaches 2^31; 0 or more than 1 GiB is refused
  * there), 0 = never split on the others. */
 int MPIX_Comm_set_max_message(MPIX_Comm comm, MPIX_Aint bytes);
+
+/* Smallest half-step (bytes) whose combine MPIX_RSB_RECURSIVE_HALVING cuts
+ * along the next step's split and runs under the next exchange (see
+ * MPIX_RSB_RECURSIVE_HALVING): 0 = never, -1 = the default of the
+ * communicator's kind (1 MiB on RCCL communicators, off on the others).  A
+ * communicator starts with env MPIX_COLL_RH_OVERLAP (read once, at creation)
+ * or that default.  Local, not collective: every rank of a communicator must
+ * set the same value before the collective (the split changes only which
+ * stream runs a combine, never the bits). */
+int MPIX_Comm_set_rh_overlap(MPIX_Comm comm, MPIX_Aint min_bytes);
+int MPIX_Comm_get_rh_overlap(MPIX_Comm comm, MPIX_Aint *min_bytes);
 
 /* Stream-ordered barrier: one 1-byte message to and from every peer on the
  * transport (on RCCL the stream passes it only once every peer's stream has

@@ -68,6 +68,8 @@ def lib():
             'MPIX_Comm_set_combine': ([vp, vp], i32),
             'MPIX_Comm_set_stream': ([vp, vp], i32),
             'MPIX_Comm_set_max_message': ([vp, ctypes.c_ssize_t], i32),
+            'MPIX_Comm_set_rh_overlap': ([vp, ctypes.c_ssize_t], i32),
+            'MPIX_Comm_get_rh_overlap': ([vp, ctypes.POINTER(ctypes.c_ssize_t)], i32),
             'MPIX_Comm_barrier': ([vp], i32),
             'MPIX_Comm_alloc_shared': ([vp, sz, ctypes.POINTER(vp)], i32),
             'MPIX_Comm_free_shared': ([vp, vp], i32),
@@ -151,6 +153,18 @@ class Comm:
         """MPIX_Comm_set_max_message: messages above nbytes go as several
         same-peer messages in one exchange group (0: never split)"""
         redop.check(lib().MPIX_Comm_set_max_message(self.h, nbytes), 'MPIX_Comm_set_max_message')
+
+    def set_rh_overlap(self, min_bytes):
+        """MPIX_Comm_set_rh_overlap: smallest recursive-halving half-step whose
+        combine runs under the next exchange (0 never, -1 the communicator
+        kind's default: 1 MiB on RCCL, off elsewhere); same bits either way"""
+        redop.check(lib().MPIX_Comm_set_rh_overlap(self.h, min_bytes), 'MPIX_Comm_set_rh_overlap')
+
+    def rh_overlap(self):
+        v = ctypes.c_ssize_t()
+        redop.check(lib().MPIX_Comm_get_rh_overlap(self.h, ctypes.byref(v)),
+                    'MPIX_Comm_get_rh_overlap')
+        return v.value
 
     def barrier(self):
         redop.check(lib().MPIX_Comm_barrier(self.h), 'MPIX_Comm_barrier')

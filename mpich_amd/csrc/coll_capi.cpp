@@ -118,6 +118,7 @@ struct MPIX_Comm_s {
     int fallbacks = 0, win_retries = 0;
     int same_node = -1;                // every rank on this host (IPC possible): -1 not yet asked
     size_t max_msg = 0;                // MPIX_Comm_set_max_message: split above this (0: never)
+    size_t rh_min = 0;                 // MPIX_Comm_set_rh_overlap (rh_overlap_default at creation)
     struct Nonce { int rank, attempt; uint64_t n0, n1; };
     std::vector<Nonce> nonce_hist;     // every window nonce published (MPIX_COLL_TRACE)
     struct Shared {                    // MPIX_Comm_alloc_shared windows
@@ -672,11 +673,12 @@ int ensure_aux(MPIX_Comm c, size_t nev)
 // a device copy on the same GPU (local communicators) the two compete for HBM
 // and the split only adds its launches and events -- 1.8 % (4 ranks) and
 // 5.8 % (8 ranks) slower on one GPU (tools/rh_overlap_probe.py,
-// profiles/r04_rh_overlap_probe.json).  MPIX_COLL_RH_OVERLAP overrides for
-// every communicator: 0 off, N > 0 the bytes.
-size_t rh_overlap_min(MPIX_Comm c)
+// profiles/r04_rh_overlap_probe.json).  MPIX_COLL_RH_OVERLAP (0 off, N > 0
+// the bytes) overrides the default for every communicator created after it is
+// set -- read once, at creation; MPIX_Comm_set_rh_overlap per communicator.
+size_t rh_overlap_default(Kind kind)
 {
-    const size_t dflt = c->kind == K_CCL ? size_t(1) << 20 : 0;
+    const size_t dflt = kind == K_CCL ? size_t(1) << 20 : 0;
     const char *e = getenv("MPIX_COLL_RH_OVERLAP");
     if (!e || !*e)
         return dflt;
@@ -684,6 +686,8 @@ size_t rh_overlap_min(MPIX_Comm c)
     unsigned long long v = strtoull(e, &end, 10);
     return (end && *end == '\0') ? (size_t) v : dflt;
 }
+
+size_t rh_overlap_min(MPIX_Comm c) { return c->rh_min; }
 
 // The overlapped form applies to P a power of two >= 4 with equal blocks on a
 // device communicator combining with the library's kernels (a custom combine
@@ -2405,6 +2409,7 @@ MPIX_Comm new_comm(int rank, int size, Kind kind)
     c->kind = kind;
     c->send_seq.assign(size, 0);
     c->recv_seq.assign(size, 0);
+    c->rh_min = rh_overlap_default(kind);
     return c;
 }
 
@@ -2535,6 +2540,22 @@ int MPIX_Comm_set_max_message(MPIX_Comm comm, MPIX_Aint bytes)
     if (!comm || bytes < 0 || (comm->kind == K_CCL && (bytes == 0 || (size_t) bytes > kMaxMsg)))
         return MPIX_REDOP_ERR_ARG;
     comm->max_msg = (size_t) bytes;
+    return MPIX_REDOP_SUCCESS;
+}
+
+int MPIX_Comm_set_rh_overlap(MPIX_Comm comm, MPIX_Aint min_bytes)
+{
+    if (!comm || min_bytes < -1)
+        return MPIX_REDOP_ERR_ARG;
+    comm->rh_min = min_bytes == -1 ? (comm->kind == K_CCL ? size_t(1) << 20 : 0) : (size_t) min_bytes;
+    return MPIX_REDOP_SUCCESS;
+}
+
+int MPIX_Comm_get_rh_overlap(MPIX_Comm comm, MPIX_Aint *min_bytes)
+{
+    if (!comm || !min_bytes)
+        return MPIX_REDOP_ERR_ARG;
+    *min_bytes = (MPIX_Aint) comm->rh_min;
     return MPIX_REDOP_SUCCESS;
 }
 

@@ -18,6 +18,9 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <linux/futex.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <atomic>
 #include <chrono>
@@ -897,6 +900,20 @@ int bounced(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext,
     return rc;
 }
 
+// Host workers for one pageable call: the configured count, at most one per
+// CPU this process may run on (more would only take turns on the same cores).
+int worker_count(int nthreads)
+{
+    int w = nthreads < 1 ? 1 : nthreads;
+    cpu_set_t mine;
+    if (sched_getaffinity(0, sizeof mine, &mine) == 0) {
+        const int cpus = CPU_COUNT(&mine);
+        if (cpus >= 1 && w > cpus)
+            w = cpus;
+    }
+    return w;
+}
+
 // Large pageable operand(s): W host workers take chunks k = w, w + W, ...; per
 // chunk a worker memcpys the pageable operand(s) into its pinned slot, runs one
 // zero-copy kernel over the slot's device mapping on its own stream (a pinned
@@ -1080,7 +1097,7 @@ int pipelined(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ex
     if (chunk == 0)
         return -1;
     const uint64_t nchunks = (count + chunk - 1) / chunk;
-    const int W = (int) std::min<uint64_t>((uint64_t) nthreads, nchunks);
+    const int W = (int) std::min<uint64_t>((uint64_t) worker_count(nthreads), nchunks);
     std::atomic<int> err{MPIX_REDOP_SUCCESS};
     // MPIX_REDOP_PIPE_TRACE=1: per chunk the host times (ns from the call's
     // start) of copy-in start / end, wait start / end, copy-out end, printed
@@ -1176,32 +1193,48 @@ int pipelined(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ex
     return err.load();
 }
 
-// Spin barrier for the wave workers (sense reversal).  Waiters spin with
-// `pause` and give the CPU up only after 20 ms: a yielding waiter on a CPU
-// shared with other runnable tasks can be left off it for a whole scheduler
-// slice, and every step of the wave waits for the last worker to leave the
-// barrier -- one such stall took a 256 MiB call from 12.6 to 21 ms
-// (profiles/r04_pageable_swing.json, the slowest trace's step 7).
+// Barrier of the wave workers (sense reversal).  A waiter spins with `pause`
+// for up to kSpinNs, then sleeps on a futex on the generation word until the
+// last worker arrives and wakes it.  Not a yield loop: a yielding waiter on a
+// CPU shared with other runnable tasks can be left off it for a whole
+// scheduler slice, and every step waits for the last worker to leave -- one
+// such stall took a 256 MiB call from 12.6 to 21 ms
+// (profiles/r04_pageable_swing.json, the slowest trace's step 7).  Not a long
+// spin either: with fewer cores than workers, spinning waiters
+// would keep the worker they wait for off the core.  The steps' own imbalance
+// is well under the spin window, so a balanced wave never sleeps.
 struct SpinBarrier {
+    static constexpr int64_t kSpinNs = 200000;
     std::atomic<int> left;
     std::atomic<int> gen{0};
+    std::atomic<int> sleepers{0};
     const int n;
     explicit SpinBarrier(int n_) : left(n_), n(n_) {}
     void wait()
     {
-        const int g = gen.load(std::memory_order_acquire);
-        if (left.fetch_sub(1, std::memory_order_acq_rel) == 1) {
-            left.store(n, std::memory_order_relaxed);
-            gen.fetch_add(1, std::memory_order_release);
+        const int g = gen.load();
+        if (left.fetch_sub(1) == 1) {
+            left.store(n);
+            gen.fetch_add(1);           // seq_cst: ordered before the sleepers check
+            if (sleepers.load() > 0)
+                syscall(SYS_futex, reinterpret_cast<int *>(&gen), FUTEX_WAKE_PRIVATE, INT32_MAX,
+                        nullptr, nullptr, 0);
             return;
         }
         const auto t0 = std::chrono::steady_clock::now();
         for (uint32_t spins = 1; gen.load(std::memory_order_acquire) == g; ++spins) {
             _mm_pause();
-            if ((spins & 0x3ff) == 0 &&
-                std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20))
-                std::this_thread::yield();
+            if ((spins & 0xff) == 0 &&
+                std::chrono::steady_clock::now() - t0 > std::chrono::nanoseconds(kSpinNs))
+                break;
         }
+        if (gen.load() != g)
+            return;
+        sleepers.fetch_add(1);          // seq_cst: the releaser sees it, or we see its gen
+        while (gen.load() == g)
+            syscall(SYS_futex, reinterpret_cast<int *>(&gen), FUTEX_WAIT_PRIVATE, g, nullptr,
+                    nullptr, 0);
+        sleepers.fetch_sub(1);
     }
 };
 
@@ -1276,7 +1309,7 @@ int waved(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext, u
         }
     }
     const int64_t n = (int64_t) chunks.size();
-    const int W = nthreads < 1 ? 1 : nthreads;
+    const int W = worker_count(nthreads);
     SpinBarrier bar(W);
     // MPIX_REDOP_PIPE_TRACE=1: per step and worker the host times (ns from the
     // call's start) at which the kernel launch (worker 0), the copy-in, the

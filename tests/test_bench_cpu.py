@@ -255,17 +255,62 @@ def test_multipath_allreduce_small_step_reported_as_plain(oracle):
             c.free()
 
 
-def test_overlap_note_names_what_ran(monkeypatch):
-    """the N > 1 line says whether the recursive-halving combine overlap ran:
-    on by default for RCCL communicators only, off with MPIX_COLL_RH_OVERLAP=0,
-    and off, named as a parity failure, when the overlapped form failed"""
+def test_overlap_note_names_what_ran():
+    """the N > 1 line says whether the recursive-halving combine overlap ran
+    in its timed calls (the communicator's MPIX_Comm_get_rh_overlap)"""
     import bench
+    assert bench.overlap_note(1 << 20).startswith('each step')
+    assert '1048576 B' in bench.overlap_note(1 << 20)
+    assert bench.overlap_note(0).startswith('off')
+
+
+def test_rh_overlap_setting_per_communicator(monkeypatch):
+    """the overlap threshold is read once, when a communicator is
+    created (env MPIX_COLL_RH_OVERLAP), and set per communicator afterwards --
+    never re-read from the environment mid-call"""
+    from mpich_amd import ccl, redop
     monkeypatch.delenv('MPIX_COLL_RH_OVERLAP', raising=False)
-    assert bench.overlap_note(True).startswith('each step')
-    assert '1048576 B' in bench.overlap_note(True)
-    assert bench.overlap_note(False) == 'off (the default of a non-RCCL communicator)'
-    assert 'failed the parity check' in bench.overlap_note(True, failed=True)
-    monkeypatch.setenv('MPIX_COLL_RH_OVERLAP', '0')
-    assert bench.overlap_note(True) == 'off (MPIX_COLL_RH_OVERLAP=0)'
-    monkeypatch.setenv('MPIX_COLL_RH_OVERLAP', '4096')
-    assert '4096 B' in bench.overlap_note(False)
+    comms = ccl.comm_create_local(2)
+    try:
+        assert comms[0].rh_overlap() == 0           # local communicators: off by default
+        monkeypatch.setenv('MPIX_COLL_RH_OVERLAP', '4096')
+        assert comms[0].rh_overlap() == 0           # not re-read after creation
+        comms[0].set_rh_overlap(1 << 20)
+        assert comms[0].rh_overlap() == 1 << 20 and comms[1].rh_overlap() == 0
+        comms[0].set_rh_overlap(-1)                 # the kind's default
+        assert comms[0].rh_overlap() == 0
+        with pytest.raises(redop.RedopError):
+            comms[0].set_rh_overlap(-2)
+    finally:
+        for c in comms:
+            c.free()
+    comms = ccl.comm_create_local(2)                # created with the env set
+    try:
+        assert [c.rh_overlap() for c in comms] == [4096, 4096]
+    finally:
+        for c in comms:
+            c.free()
+
+
+def test_dry_run_line_names_the_defaults_ab():
+    """the N > 1 line carries `defaults_ab`, the four
+    overlap x store-policy variants of the value leg"""
+    import json
+    import bench
+    p = _bench(['--gpus', '2', '--dry-run', '--no-extras', '--no-cpu-baseline'])
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith('{')][0])
+    assert sorted(d['defaults_ab']) == sorted(bench.AB_VARIANTS), d
+
+
+def test_launcher_counts_devices_in_a_child(monkeypatch):
+    """the launcher's device count runs in a child process (count_devices):
+    here (no GPU) it is 0, and the parent never imports the HIP runtime's
+    device state for it"""
+    import bench
+    import torch
+    assert bench.count_devices() == 0
+    assert not torch.cuda.is_initialized()
+    with pytest.raises(SystemExit):
+        bench.check_devices(2, {})
+    bench.check_devices(4, {'MPIX_BENCH_SAME_DEVICE': '1'})

@@ -431,6 +431,107 @@ def test_staged_rsb_config4_full_size(tmp_path):
         assert got == '1 1', (r, detail)
 
 
+def _c4_shape_worker(rank, world, port, outdir, total_bytes):
+    """The exact shape of the N > 1 value leg (bench.multi_gpu at the default
+    --rsb-bytes), ranks as processes on the test GPU: a 4 GiB fp32 vector per
+    rank, recursive halving with the combine overlap at the RCCL default
+    (half-steps >= 1 MiB split, kept half on the second stream) and off, and
+    every message above 1 GiB split into consecutive 1 GiB messages (the
+    RCCL communicators' maximum) -- the step-1 send of 2 GiB goes as two.
+    Each rank checks its 512 MiB (P = 8) block bit for bit on the device
+    against the schedule's association (bench.rh_expected_block: per step with
+    mask = P/2 .. 1 every rank adds its partner's partial, one IEEE add each)
+    over inputs regenerated from the seeds."""
+    import torch.distributed as dist
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    os.environ['MPIX_COLL_TRACE'] = '1'
+    torch.cuda.set_device(0)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    trace = open(os.path.join(outdir, 'c4trace%d.txt' % rank), 'w')
+    os.dup2(trace.fileno(), 2)          # the library's trace lines land in the file
+    from mpich_amd import coll
+    n = total_bytes // 4
+    rc = n // world
+
+    def vec(r):
+        g = torch.Generator(device='cuda')
+        g.manual_seed(0x5EED0C80 + r)
+        return torch.empty(n, dtype=torch.float32, device='cuda').uniform_(-1, 1, generator=g)
+    # the expected block: block `rank` of every rank's vector, folded as the
+    # schedule folds it (parts[q] = parts[q] + parts[q ^ m]; an IEEE add is
+    # commutative, so both members of a pair share one sum tensor)
+    parts = []
+    for q in range(world):
+        v = vec(q)
+        parts.append(v[rank * rc:(rank + 1) * rc].clone())
+        del v
+    m = world // 2
+    while m:
+        for q in range(world):
+            if q < q ^ m:
+                t = parts[q] + parts[q ^ m]
+                parts[q] = parts[q ^ m] = t
+        m //= 2
+    expected = parts[rank]
+    del parts, t
+    torch.cuda.empty_cache()
+    c = coll.comm_for(None, True)
+    x = vec(rank)
+    out = torch.empty(rc, dtype=torch.float32, device='cuda')
+    res = {}
+    for mode in (1 << 20, 0):
+        c.set_rh_overlap(mode)
+        out.fill_(float('nan'))
+        timer = []
+        coll.reduce_scatter_block(x, out, rc, MPI_FLOAT, MPI_SUM, algorithm='recursive_halving',
+                                  timer=timer)
+        torch.cuda.synchronize()
+        phases = [t['phase'] for t in timer]
+        res[str(mode)] = dict(bits=bool(torch.equal(out.view(torch.int32),
+                                                     expected.view(torch.int32))),
+                              split=phases.count('combine (sent half)'),
+                              whole=phases.count('combine'),
+                              state=c.state()['last_rs'])
+    trace.flush()
+    with open(os.path.join(outdir, 'c4res%d.json' % rank), 'w') as f:
+        import json
+        json.dump(res, f)
+    del x, out, expected
+    dist.barrier()
+    coll.free_comms()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize('world', [4, 8])
+def test_staged_rsb_config4_value_leg_shape(tmp_path, world):
+    """P = 4 and 8 at 4 GiB fp32 per rank, overlap at the
+    RCCL default and off, 1 GiB message split -- bit-exact on every rank"""
+    import json
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    mp.spawn(_c4_shape_worker, args=(world, _free_port(), str(tmp_path), 4 << 30), nprocs=world,
+             join=True)
+    steps = world.bit_length() - 1
+    for r in range(world):
+        res = json.load(open(tmp_path / ('c4res%d.json' % r)))
+        on, off = res[str(1 << 20)], res['0']
+        assert on['bits'] and off['bits'], (r, res)
+        assert on['state'] == off['state'] == 'recursive_halving', res
+        # overlap on: every step but the last (no next split) cuts its combine
+        assert on['split'] == steps - 1 and on['whole'] == 1, (r, on)
+        assert off['split'] == 0 and off['whole'] == steps, (r, off)
+        import re
+        lines = [ln for ln in open(tmp_path / ('c4trace%d.txt' % r)).read().splitlines()
+                 if ln.startswith('[mpix_coll rank') and len(ln.split()) > 3 and
+                 all(re.fullmatch(r'[<>]\d+:\d+', f) for f in ln.split()[3:])]
+        # step 1 of each call: 2 GiB each way, posted as two 1 GiB messages each
+        first = lines[0].split()[3:]
+        assert len(first) == 4 and all(f.endswith(':%d' % (1 << 30)) for f in first), lines[0]
+        assert max(int(f.split(':')[1]) for ln in lines for f in ln.split()[3:]) == 1 << 30
+
+
 def test_rccl_rsb_matches_oracle(oracle, tmp_path):
     """one process per GPU over RCCL (the bench's transport at N > 1)"""
     ndev = torch.cuda.device_count() if torch.cuda.is_available() else 0
