@@ -441,10 +441,11 @@ def cpu_baseline(seconds, count, crossover_rows):
 
 
 def load_pmc(path, count):
-    """(HBM bytes per launch, the file they come from): the PMC summary of a
-    separate rocprofv3 FETCH_SIZE / WRITE_SIZE pass over the same command
+    """The PMC summary of a separate rocprofv3 pass over the same command
     (tools/gpu_evidence.sh, tools/pmc_summary.py) -- quoted, not measured in
-    this process, so the line names its source"""
+    this process, so the line names its source: (HBM bytes per launch, the
+    file, the summary's kernel record with the traced average duration and
+    the traced run's own ms_per_step)"""
     for p in (path, os.path.join(ROOT, 'profiles', 'r01_pmc_summary.json')):
         try:
             with open(p) as f:
@@ -453,8 +454,8 @@ def load_pmc(path, count):
             continue
         k = d.get('kernels', {}).get('reduce_local_fp32_sum')
         if k and k.get('count') == count:
-            return k.get('hbm_bytes_per_launch'), os.path.relpath(p, ROOT)
-    return None, None
+            return k.get('hbm_bytes_per_launch'), os.path.relpath(p, ROOT), k
+    return None, None, None
 
 
 def overlap_note(min_bytes):
@@ -519,7 +520,7 @@ def single_gpu(args, dev):
     leg = reduce_local_leg(args, 1, 0, dev)
     inb, inout, stream, kreps = leg['inb'], leg['inout'], leg['stream'], leg['kreps']
     achieved = nbytes_alg / (leg['k_avg'] * 1e-3) / 1e9
-    traffic, traffic_src = load_pmc(args.pmc, n)
+    traffic, traffic_src, traced = load_pmc(args.pmc, n)
     result = {
         'metric': METRIC,
         'value': round(nbytes_alg * args.steps / leg['t'] / GIB, 2),
@@ -552,6 +553,17 @@ def single_gpu(args, dev):
             'algorithmic_bytes_per_launch': nbytes_alg,
         },
     }
+    if traced and traced.get('avg_duration_ns'):
+        # the same kernel's rocprofv3 kernel-trace average from the quoted
+        # evidence pass, and that run's own step time: frac_traced follows
+        # from the file alone (algorithmic bytes / traced average / peak)
+        t_ns = float(traced['avg_duration_ns'])
+        result['roofline'].update(
+            frac_traced=round(nbytes_alg / t_ns / HBM_PEAK_GBS, 4),
+            traced_kernel_ms_avg=round(t_ns * 1e-6, 4),
+            traced_launches=traced.get('launches_traced'),
+            traced_run_ms_per_step=traced.get('traced_run_ms_per_step'),
+            traced_source=traffic_src)
     crossover = None
     if not args.no_extras:
         B = bench_lib()

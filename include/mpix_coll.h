@@ -238,8 +238,11 @@ int MPIX_Exscan_async(const void *sendbuf, void *recvbuf, MPIX_Aint count, MPIX_
 #define MPIX_ALLREDUCE_RSAG_MULTIPATH       5   /* REDUCE_SCATTER_ALLGATHER with every
                                                    reduce-scatter step spread over all links
                                                    through relays (P a power of two >= 4,
-                                                   count a multiple of P; else plain steps);
-                                                   same bits */
+                                                   count a multiple of P; else plain steps;
+                                                   a step too small for the relay slots runs
+                                                   plain, and a call none of whose steps
+                                                   could use the relays counts as
+                                                   REDUCE_SCATTER_ALLGATHER); same bits */
 #define MPIX_ALLREDUCE_PULL                 6   /* REDUCE_SCATTER_ALLGATHER's association (same
                                                    bits) as two pulls (pull windows, as
                                                    MPIX_RSB_PULL): ONE tree kernel reads this
@@ -320,7 +323,7 @@ int MPIX_Comm_free_shared(MPIX_Comm comm, void *ptr);
 /* Which schedule actually ran -- an explicitly requested algorithm may not be
  * able to run (a pull whose windows failed verification on some rank, a
  * device pair without peer access, MULTIPATH on a shape it does not cover or
- * with a step too small for its relay slots), in which case the schedule with
+ * with every step too small for its relay slots), in which case the schedule with
  * the same bits runs instead; this is how a caller tells.  pulls_enabled: 1
  * while the pull schedules can run on this communicator (0 once it is known to
  * span nodes; before the first pull that is not yet known and counts as 1);

@@ -1713,7 +1713,7 @@ int allreduce_rsag(char *rb, size_t count, MPIX_Datatype dt, MPIX_Op op, MPIX_Co
         };
         auto real = [&](int nr) { return nr < rem ? nr * 2 + 1 : nr + rem; };
         int mask = 1, send_idx = 0, recv_idx = 0, last_idx = pof2;
-        bool mp_fell = false;
+        int mp_steps = 0;           // reduce-scatter steps that ran over the relays
         while (mask < pof2) {                                               // :138-189
             int newdst = newrank ^ mask;
             size_t send_cnt, recv_cnt;
@@ -1729,13 +1729,8 @@ int allreduce_rsag(char *rb, size_t count, MPIX_Datatype dt, MPIX_Op op, MPIX_Co
             const size_t parts = (size_t) pof2 / 2;
             const bool mp_step = multipath && rem == 0 && pof2 >= 4 && count % pof2 == 0 &&
                                  send_cnt >= parts * (parts - 1);
-            if (multipath && !mp_step && !mp_fell) {
-                // a step too small for the relay slots runs the plain
-                // exchange: the call is then reported as the plain schedule
-                mp_fell = true;
-                ran_instead(c, &c->last_ar, MPIX_ALLREDUCE_REDUCE_SCATTER_ALLGATHER);
-            }
             if (mp_step) {
+                ++mp_steps;
                 // send_cnt == recv_cnt here; relay slots fit in send_cnt elements
                 const size_t slot = (send_cnt + parts - 1) / parts * ext;
                 TRY(multipath_exchange(c, rb + disps[send_idx] * ext, tmp + disps[recv_idx] * ext,
@@ -1752,6 +1747,12 @@ int allreduce_rsag(char *rb, size_t count, MPIX_Datatype dt, MPIX_Op op, MPIX_Co
             if (mask < pof2)
                 last_idx = recv_idx + pof2 / mask;
         }
+        // a step too small for the relay slots runs the plain exchange (the
+        // last, smallest steps first); the call counts as MULTIPATH while its
+        // first step -- the one that moves the most -- went over the relays,
+        // and as the plain schedule only when no step did
+        if (multipath && !mp_steps)
+            ran_instead(c, &c->last_ar, MPIX_ALLREDUCE_REDUCE_SCATTER_ALLGATHER);
         mask >>= 1;
         if (direct) {
             const int mine = bitrev(newrank, pof2);

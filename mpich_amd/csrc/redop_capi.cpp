@@ -396,6 +396,7 @@ void read_env()
         g_pinned_floor = atoll(s);
     if (const char *s = getenv("MPIX_REDOP_OPFN_ABORT"))
         g_opfn_abort = atoi(s) != 0;
+
     if (const char *s = getenv("MPIX_REDOP_BOUNCE_BYTES")) {
         long long c = atoll(s);
         if (c >= 0 && c <= (64ll << 20))
@@ -1851,29 +1852,44 @@ int MPIX_Reduce_local_batch_async(const void *const *inbufs, void *const *inoutb
     const void *pin[MPIX_BATCH_MAX];
     void *pio[MPIX_BATCH_MAX];
     uint64_t cnt[MPIX_BATCH_MAX];
+    bool zc[MPIX_BATCH_MAX];
     int m = 0, launch = -2;
     for (int i = 0; i < k; ++i) {
         if (!counts[i])
             continue;
         const void *a, *b;
-        if (!reachable(inbufs[i], (hipStream_t) stream, &launch, &a) ||
-            !reachable(inoutbufs[i], (hipStream_t) stream, &launch, &b))
+        bool pinned = false;
+        if (!reachable(inbufs[i], (hipStream_t) stream, &launch, &a, &pinned) ||
+            !reachable(inoutbufs[i], (hipStream_t) stream, &launch, &b, &pinned))
             return set_err(MPIX_REDOP_ERR_BUFFER);
         pin[m] = a;
         pio[m] = (void *) b;
+        zc[m] = pinned;
         cnt[m++] = (uint64_t) counts[i];
     }
     if (!m)
         return set_err(MPIX_REDOP_SUCCESS);
-    if (!e) {       // REPLACE / NO_OP / EQUAL: one call each
-        for (int i = 0; i < m; ++i) {
-            int rc = enqueue(pin[i], pio[i], cnt[i], it, ext, (uint32_t) op, (hipStream_t) stream);
+    // REPLACE / NO_OP / EQUAL, and every triple with a page-locked host
+    // operand: a call each -- a kernel reading host memory over PCIe runs the
+    // capped, looping zero-copy grid (g_zc_grid), which the
+    // batch kernels' one-tile-per-block layout cannot.  The triples are
+    // independent (checked above), so their order does not matter.
+    int nd = 0;
+    for (int i = 0; i < m; ++i) {
+        if (!e || zc[i]) {
+            int rc = enqueue(pin[i], pio[i], cnt[i], it, ext, (uint32_t) op, (hipStream_t) stream,
+                             nullptr, nullptr, 0, nullptr, zc[i]);
             if (rc != MPIX_REDOP_SUCCESS)
                 return set_err(rc);
+            continue;
         }
-        return set_err(MPIX_REDOP_SUCCESS);
+        pin[nd] = pin[i];
+        pio[nd] = pio[i];
+        cnt[nd++] = cnt[i];
     }
-    return set_err(hip_err(e->batch(pin, pio, cnt, m, params(), launch_cfg(), (hipStream_t) stream)));
+    if (!nd)
+        return set_err(MPIX_REDOP_SUCCESS);
+    return set_err(hip_err(e->batch(pin, pio, cnt, nd, params(), launch_cfg(), (hipStream_t) stream)));
 }
 
 int MPIX_Reduce_local(const void *inbuf, void *inoutbuf, MPIX_Aint count, MPIX_Datatype datatype,

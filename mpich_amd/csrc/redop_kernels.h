@@ -528,6 +528,63 @@ __device__ __forceinline__ bool tree_fold_rec(T &out, int k, uint32_t pres, L &l
     }
 }
 
+// The tree fold in tree_fold_rec's order (pairs (0,1), (2,3), their sum, ...)
+// with U packets per lane: the slots are loaded as the recursion reaches
+// them, so the compiler may keep fewer of them live (more waves per SIMD)
+// instead of issuing all KMAX x U loads up front as k_contig_tree does.
+template <int U> struct PkU {
+    v4u x[U];
+};
+
+template <class C, int KMAX, int U>
+__global__ void __launch_bounds__(256)
+k_contig_tree_rec(MultiIn<typename C::unit> ins, int k, uint32_t pres,
+                  typename C::unit *__restrict__ out, uint64_t head, uint64_t npk,
+                  uint64_t tail_start, uint32_t ntail, Params prm)
+{
+    using T = typename C::unit;
+    v4u *vout = reinterpret_cast<v4u *>(out + head);
+    const uint64_t nt = blockDim.x;
+    const uint64_t stride = (uint64_t) gridDim.x * nt * U;
+    const bool wt = wt_block(prm);
+    for (uint64_t i = (uint64_t) blockIdx.x * nt * U + threadIdx.x; i < npk; i += stride) {
+        auto load = [&](int q) {
+            PkU<U> v;
+            const v4u *p = reinterpret_cast<const v4u *>(ins.p[q] + head) + i;
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (i + u * nt < npk)
+                    v.x[u] = ld16<true>(p + u * nt);
+            return v;
+        };
+        auto f = [&](PkU<U> a, const PkU<U> &b) {
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                a.x[u] = combine16<C>(a.x[u], b.x[u], prm);
+            return a;
+        };
+        PkU<U> r;
+        tree_fold_rec<0, KMAX>(r, k, pres, load, f);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (i + u * nt < npk)
+                st16_pol<true>(vout + i + u * nt, r.x[u], wt);
+    }
+    if (blockIdx.x == 0) {
+        auto ce = [&](T a, T b) { return C::apply(a, b, prm); };
+        auto one = [&](uint64_t t) {
+            auto ld = [&](int q) { return ins.p[q][t]; };
+            T r;
+            tree_fold_rec<0, KMAX>(r, k, pres, ld, ce);
+            out[t] = r;
+        };
+        for (uint64_t t = threadIdx.x; t < head; t += nt)
+            one(t);
+        for (uint64_t t = threadIdx.x; t < ntail; t += nt)
+            one(tail_start + t);
+    }
+}
+
 // the same fold element by element, for operands not sharing a 16-byte phase
 // (and every 32-byte unit)
 template <class C>
@@ -933,7 +990,10 @@ hipError_t launch_multi(const void *const *ins, int k, void *io, uint64_t count,
         uint64_t npk = (count - head) / E;
         uint64_t tail_start = head + npk * E;
         uint32_t ntail = (uint32_t) (count - tail_start);
-        constexpr int U = 2;    // 4 measured no better (k = 1..15, tools/multi_probe.py)
+        // one packet per lane per input: 6.16 / 6.20 TB/s at k = 7 (256 MiB /
+        // 1 GiB, store policy on) against 6.04 / 5.83 with two; 4 measured no
+        // better than 2 (tools/tree8_probe.hip, tools/multi_probe.py)
+        constexpr int U = 1;
         unsigned grid = grid_for((uint64_t) cfg.block * U, npk, cfg.max_grid);
         Params p = prm;
         set_store_policy(p, cfg, grid);
@@ -994,21 +1054,36 @@ hipError_t launch_tree(const void *const *ins, int k, void *out, uint64_t count,
         uint64_t tail_start = head + npk * E;
         uint32_t ntail = (uint32_t) (count - tail_start);
         Params p = prm;
-        const unsigned grid = grid_for(k == 2 ? 256 * 4 : k <= 4 ? 256 * 2 : 256, npk, 0);
-        // the store policy pays for the k = 2 form (+5 %); the 16-slot form
-        // gains nothing at k = 4 / 8 / 16 (profiles/r03_tree_probe_policy.json)
-        if (k == 2)
-            set_store_policy(p, cfg, grid);
+        // forms by slot count (tools/tree8_probe.hip, profiles/r05_tree_forms.json;
+        // fp32 SUM at 256 MiB / 1 GiB per operand, store policy on):
+        //   k = 2   the fold order, 2 packets per lane     6.81 / 6.94 TB/s
+        //           (all 4 x 2 loads up front: 6.44 / 6.84)
+        //   k = 4   all 4 x 2 loads up front               6.40 / 6.61
+        //           (the fold order, 1 packet: 6.34 / 6.53)
+        //   k = 8   the fold order, 1 packet per lane      6.47 / 6.36
+        //           (8 x 2 up front 5.79 / 5.43, 16 x 1 up front 5.68 / 5.22)
+        //   k = 16  the fold order, 1 packet per lane      6.37 / 5.92
+        //           (16 x 1 up front 5.86 / 5.50)
+        // Loading slots only as the fold reaches them keeps 39 VGPRs live at
+        // k = 8 (8 waves per SIMD) against 111 for the up-front form (4), and
+        // with nine streams the waves, not each wave's bytes in flight, carry
+        // the rate.  The store policy: +5 % at k = 2, +3.8 % at k = 4, neutral
+        // above.
+        const unsigned per = k == 2 ? 256 * 2 : k == 4 ? 256 * 2 : 256;
+        const unsigned grid = grid_for(per, npk, 0);
+        set_store_policy(p, cfg, grid);
         if constexpr (sizeof(T) <= 16) {
-            if (k == 2)     // out = a OP b: the contiguous kernel's 4 packets per lane
-                hipLaunchKernelGGL((k_contig_tree<C, 2, 4>), dim3(grid), dim3(256), 0, s, mi, k,
+            if (k == 2)     // out = a OP b (recursive halving's combine_to)
+                hipLaunchKernelGGL((k_contig_tree_rec<C, 2, 2>), dim3(grid), dim3(256), 0, s, mi, k,
                                    pres, tout, head, npk, tail_start, ntail, p);
-            else if (k <= 4)    // 4 slots x 2 packets per lane: 8 loads in flight, as k_contig
+            else if (k == 4)
                 hipLaunchKernelGGL((k_contig_tree<C, 4, 2>), dim3(grid), dim3(256), 0, s, mi, k,
                                    pres, tout, head, npk, tail_start, ntail, p);
-            else            // one 16-slot form for k > 4 (an 8-slot form, more waves in
-                            // flight, measured 4-9 % slower at k = 4 and 8)
-                hipLaunchKernelGGL((k_contig_tree<C, kMaxMulti, 1>), dim3(grid), dim3(256), 0, s,
+            else if (k == 8)    // the P = 8 pull's fold
+                hipLaunchKernelGGL((k_contig_tree_rec<C, 8, 1>), dim3(grid), dim3(256), 0, s, mi, k,
+                                   pres, tout, head, npk, tail_start, ntail, p);
+            else
+                hipLaunchKernelGGL((k_contig_tree_rec<C, kMaxMulti, 1>), dim3(grid), dim3(256), 0, s,
                                    mi, k, pres, tout, head, npk, tail_start, ntail, p);
         }
     } else {
@@ -1106,6 +1181,12 @@ hipError_t launch_batch(const void *const *ins, void *const *ios, const uint64_t
                 continue;
             }
             const uint64_t nb = (count + tile - 1) / tile;
+            if (nb > 0x7fffffffull) {       // more tiles than one grid holds: a call of its own
+                hipError_t e = launch_contig<C>(ins[i], ios[i], count, p, cfg, s);
+                if (e != hipSuccess)
+                    return e;
+                continue;
+            }
             if (blocks + nb > 0x7fffffffull) {
                 hipError_t e = flush();
                 if (e != hipSuccess)
@@ -1155,6 +1236,12 @@ hipError_t launch_batch(const void *const *ins, void *const *ios, const uint64_t
             uint64_t nb = (npk + tile - 1) / tile;
             if (nb == 0)
                 nb = 1;         // a segment of head / tail elements only
+            if (nb > 0x7fffffffull) {       // more tiles than one grid holds: launch_contig
+                hipError_t e = launch_contig<C>(ins[i], ios[i], count, p, cfg, s);   // loops
+                if (e != hipSuccess)
+                    return e;
+                continue;
+            }
             if (blocks + nb > 0x7fffffffull) {
                 hipError_t e = flush();
                 if (e != hipSuccess)

@@ -169,3 +169,34 @@ def test_batch_refuses_host_operand(R):
     assert rc == H.MPI_ERR_BUFFER
     torch.cuda.synchronize()
     assert bool(torch.all(y == 1))          # refused before any launch
+
+
+@pytest.mark.gpu
+def test_batch_with_page_locked_operands(R, oracle):
+    """a triple with a page-locked host operand (in, inout or
+    both) runs as its own zero-copy call, with the capped looping grid every
+    kernel reading host memory gets; the device triples of the same batch
+    still go as one launch.  Every triple = the oracle."""
+    from mpich_amd import handles as H
+    rng = np.random.default_rng(0x5EED0702)
+    sizes = [4099, (4 << 20) // 4 + 3, 1000, (1 << 20) + 1, 17]
+    kinds = [('dev', 'dev'), ('pin', 'dev'), ('dev', 'dev'), ('pin', 'pin'), ('dev', 'pin')]
+
+    def buf(kind, v):
+        t = torch.from_numpy(v.copy())
+        return t.pin_memory() if kind == 'pin' else t.cuda()
+    ins, ios, want = [], [], []
+    for c, (ki, ko) in zip(sizes, kinds):
+        a = rng.uniform(-1, 1, c).astype(np.float32)
+        b = rng.uniform(-1, 1, c).astype(np.float32)
+        w = b.copy()
+        assert oracle.reduce_local(a, w, c, H.MPI_FLOAT, H.MPI_SUM) == 0
+        ins.append(buf(ki, a))
+        ios.append(buf(ko, b))
+        want.append(w)
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    R.check(R.reduce_local_batch_async(ins, ios, sizes, H.MPI_FLOAT, H.MPI_SUM, s))
+    s.synchronize()
+    for q, (b, w) in enumerate(zip(ios, want)):
+        assert np.array_equal(b.cpu().numpy(), w), q

@@ -223,10 +223,13 @@ def test_world_plan_rules():
 
 
 def test_multipath_allreduce_small_step_reported_as_plain(oracle):
-    """rsag_multipath needs send_cnt >= parts * (parts - 1) at
-    every reduce-scatter step; a step below that runs the plain exchange, and
-    the call must then be reported as reduce_scatter_allgather (P = 4: count 4
-    halves to a 1-element second step; count 8 keeps 2 per step)"""
+    """rsag_multipath needs send_cnt >= parts * (parts - 1)
+    at a reduce-scatter step; a step below that runs the plain exchange.  A
+    call none of whose steps could use the relays is reported as
+    reduce_scatter_allgather (count 6: not a multiple of P = 4); a call whose
+    first step went over the relays and whose last did not (count 4: 2 then 1
+    element per step) ran multipath and is reported so; count 8 keeps 2 per
+    step"""
     import bench
     from mpich_amd import ccl
     P = 4
@@ -235,7 +238,7 @@ def test_multipath_allreduce_small_step_reported_as_plain(oracle):
         c.set_combine(oracle.combine_fn_address())
     MPI_FLOAT, MPI_SUM = 0x4c00040a, 0x58000003
     try:
-        for count, fell in ((4, True), (8, False), (4096, False)):
+        for count, fell in ((6, True), (4, False), (8, False), (4096, False)):
             sends = [np.arange(count, dtype=np.float32) + r for r in range(P)]
             outs = [np.zeros(count, np.float32) for _ in range(P)]
             before = comms[0].state()['fallbacks']

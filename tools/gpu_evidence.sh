@@ -18,7 +18,8 @@ timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -T -d $O/write -o write --output-
 python3 tools/pmc_summary.py --kt "$(find $O/kt -name '*kernel_stats.csv' | head -n 1)" \
     --fetch "$(find $O/fetch -name '*counter_collection.csv' | head -n 1)" \
     --write "$(find $O/write -name '*counter_collection.csv' | head -n 1)" \
-    --out $O/${R}_pmc_summary.json --stats-copy $O/${R}_rocprof_kernel_stats.csv > /dev/null && \
+    --out $O/${R}_pmc_summary.json --stats-copy $O/${R}_rocprof_kernel_stats.csv \
+    --traced-line $O/prof_bench.json > /dev/null && \
 timeout -k 10 500 python3 bench.py --pmc $O/${R}_pmc_summary.json > $O/bench.json 2> $O/bench.err
 rc=$?
 echo rc=$rc

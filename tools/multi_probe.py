@@ -26,6 +26,10 @@ def main():
     ap.add_argument('--mib', type=int, default=256)
     ap.add_argument('--ks', default='1,2,3,4,7,15')
     ap.add_argument('--tree-ks', default='2,4,8,16')
+    ap.add_argument('--tree-inplace', action='store_true',
+                    help='tree folds write slot 0 in place instead of a separate output')
+    ap.add_argument('--skew', type=int, default=0,
+                    help='operand q starts q * SKEW bytes into its allocation (placement probe)')
     a = ap.parse_args()
     S = a.mib << 20
     n = S // 4
@@ -33,7 +37,9 @@ def main():
     tks = [int(x) for x in a.tree_ks.split(',')]
     top = max(ks + tks)
     dev = torch.device('cuda', 0)
-    bufs = [torch.empty(n, dtype=torch.float32, device=dev).uniform_(-1, 1) for _ in range(top + 1)]
+    sk = a.skew // 4
+    bufs = [torch.empty(n + q * sk, dtype=torch.float32, device=dev)[q * sk:].uniform_(-1, 1)
+            for q in range(top + 1)]
     out = torch.empty(n, dtype=torch.float32, device=dev)
     torch.cuda.synchronize()
     s = torch.cuda.current_stream()
@@ -52,13 +58,15 @@ def main():
                          GBs=round((k + 2) * S / (ms * 1e-3) / 1e9, 1)))
     for k in tks:
         ins = bufs[:k]
-        f = lambda: redop.check(redop.reduce_local_tree_async(ins, out, n, H.MPI_FLOAT,  # noqa
+        dst = ins[0] if a.tree_inplace else out
+        f = lambda: redop.check(redop.reduce_local_tree_async(ins, dst, n, H.MPI_FLOAT,  # noqa
                                                                H.MPI_SUM, s))
         f()
         ms, _, _ = bench.event_time_per_launch(f, 10, s)
         rows.append(dict(kind='tree', k=k, ms=round(ms, 4),
                          GBs=round((k + 1) * S / (ms * 1e-3) / 1e9, 1)))
-    print(json.dumps(dict(what='fp32 SUM multi-input and tree combines, %d MiB per operand, HIP '
+    print(json.dumps(dict(skew=a.skew, tree_inplace=a.tree_inplace, env={k: v for k, v in os.environ.items()
+                                            if k.startswith('MPIX_REDOP_')}, what='fp32 SUM multi-input and tree combines, %d MiB per operand, HIP '
                                'events (average of 3 batches of 10 launches)' % a.mib, rows=rows)),
           flush=True)
 

@@ -37,6 +37,9 @@ def main():
     ap.add_argument('--elem', type=int, default=4)
     ap.add_argument('--out', required=True)
     ap.add_argument('--stats-copy', required=True)
+    ap.add_argument('--traced-line', default=None,
+                    help="the traced bench run's own JSON line (its ms_per_step is kept beside the "
+                         "traced kernel average: traced kernel <= step time)")
     a = ap.parse_args()
     stats = {r['Name']: r for r in csv.DictReader(open(a.kt))}
     shutil.copy(a.kt, a.stats_copy)
@@ -58,7 +61,15 @@ def main():
             hbm_bytes_per_launch=int(hbm), algorithmic_bytes_per_launch=alg,
             traffic_over_algorithmic=round(hbm / alg, 5),
             achieved_GBs_from_trace=round(alg / avg_ns, 1),
+            frac_from_trace=round(alg / avg_ns / 8000.0, 4),
             correction='hbm = (2*FETCH_SIZE + WRITE_SIZE) KiB * 1024 (gfx950 FETCH_SIZE half-count)')})
+    if a.traced_line:
+        line = json.loads(open(a.traced_line).read().strip().splitlines()[-1])
+        kk = summary['kernels']['reduce_local_fp32_sum']
+        kk['traced_run_ms_per_step'] = line.get('ms_per_step')
+        kk['traced_run_value'] = line.get('value')
+        kk['traced_kernel_within_step'] = (line.get('ms_per_step') is not None and
+                                           avg_ns * 1e-6 <= line['ms_per_step'])
     with open(a.out, 'w') as fo:
         json.dump(summary, fo, indent=1)
     print(json.dumps(summary, indent=1))
