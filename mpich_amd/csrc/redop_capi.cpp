@@ -246,11 +246,15 @@ std::atomic<int> g_block{256}, g_max_grid{0};
 // Grid cap of kernels reading page-locked host memory over PCIe (zero-copy):
 // with one tile per block every block loads its whole tile (host to device)
 // before it stores (device to host), and a grid of a few hundred blocks is
-// one round, so the two link directions take turns.  32 looping blocks keep
-// both busy: 4 MiB 235 -> 186 us, 16 MiB 780 -> 655 us, 1 GiB 39.2 -> 38.1 ms
-// (tools/pinned_grid.py, profiles/r04_pinned_grid.json; 32-64 equal, 16 and
-// 8 lose).  MPIX_REDOP_ZC_GRID overrides (0: uncapped).
-std::atomic<int> g_zc_grid{32};
+// one round, so the two link directions take turns.  Looping blocks keep
+// both busy: with 4 packets per lane 32 blocks took 4 MiB 235 -> 186 us,
+// 16 MiB 780 -> 655 us, 1 GiB 39.2 -> 38.1 ms (profiles/r04_pinned_grid.json);
+// with one packet per lane (round 5) 64 blocks hold the same bytes in flight:
+// 1 MiB 69 -> 55 us, 4 MiB 238 -> 182 us, 16 MiB 769 -> 655 us, 256 MiB
+// 10.1 -> 9.4 ms, where 32 gave 59 / 197 / 682 us / 9.8 ms
+// (tools/pinned_grid.py, profiles/r05_pinned_grid.json).  MPIX_REDOP_ZC_GRID
+// overrides (0: uncapped).
+std::atomic<int> g_zc_grid{64};
 // Store policy of the contiguous and multi-input kernels and the two-slot tree
 // (MPIX_Redop_set_store_policy): the blocks running on the XCDs of g_wt_xcd
 // store write-through (sc0 sc1), the others non-temporally.  Two XCDs of eight

@@ -5,7 +5,11 @@
 // the ALUs (no MFMA, no LDS on the contiguous path):
 //   * both operands are read as 16-byte packets (global_load_dwordx4), each
 //     lane keeping MPIX_REDOP_UNROLL packets per operand in flight before the
-//     first combine, so a 256-thread block has 256*U*32 B outstanding;
+//     first combine, so a 256-thread block has 256*U*32 B outstanding (U = 1
+//     since round 5: the latency is covered by waves, not by each wave's
+//     loads -- 8 waves per SIMD at 1 GiB fp32 SUM ran 4.0 % faster than U = 4,
+//     every config-3 row 2.8-8.2 % faster; tools/contig_u_probe.hip,
+//     tools/gpu_u_ab.sh, profiles/r05_unroll_ab.json);
 //   * inout is written back with 16-byte stores to the lines it just read;
 //   * each packet holds 16/sizeof(unit) elements, combined in registers;
 //   * elements before the first 16-byte boundary of inout (head) and after
@@ -24,7 +28,7 @@
 #include "redop_ops.h"
 
 #ifndef MPIX_REDOP_UNROLL
-#define MPIX_REDOP_UNROLL 4
+#define MPIX_REDOP_UNROLL 1
 #endif
 #ifndef MPIX_REDOP_NT_LOAD
 #define MPIX_REDOP_NT_LOAD 1
@@ -939,7 +943,7 @@ hipError_t launch_contig(const void *in, void *io, uint64_t count, const Params 
         uint32_t ntail = (uint32_t) (count - tail_start);
         const uint64_t tile = (uint64_t) cfg.block * MPIX_REDOP_UNROLL;
         unsigned grid = grid_for(tile, npk, cfg.max_grid);
-        // up to kSignalMaxGrid workgroups (64 KiB at the defaults): the
+        // up to kSignalMaxGrid workgroups (64 KiB per operand at the defaults): the
         // kernel stores the completion word itself (Params::done)
         Params p = prm;
         if (grid > (prm.done_ctr ? kSignalMaxGrid : 1u))

@@ -80,6 +80,7 @@ int main(int argc, char **argv)
     std::vector<int> same(vs.size(), 1);
     for (size_t v = 0; v < vs.size(); ++v) {
         CK(hipMemcpy(io, io0, S, hipMemcpyDeviceToDevice));
+        CK(hipDeviceSynchronize());     // the copy ran on the null stream, s does not wait for it
         vs[v].fn(in, io, npk, vs[v].block, prm, s);
         CK(hipStreamSynchronize(s));
         CK(hipMemcpy(v ? h_got.data() : h_ref.data(), io, S, hipMemcpyDeviceToHost));
