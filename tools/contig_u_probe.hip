@@ -6,7 +6,8 @@
 // lane faster than the up-front forms, and k_contig itself at U = 1 ahead of
 // the shipped U = 4 in the same process (6.93 vs 6.79 TB/s at 256 MiB, 6.84
 // vs 6.64 at 1 GiB).  This probe times the headline shape only: 1 GiB fp32
-// SUM per operand, U in {1, 2, 4} x block in {256, 512, 1024}, interleaved,
+// SUM per operand, U in {1, 2, 4} x block in {256, 512, 1024}, and at U = 1 the
+// store-policy XCD masks and plain (not non-temporal) loads / stores, interleaved,
 // 7 rounds of 10 launches, median; every form's result bit-identical to
 // U = 4 / 256 (same combine per element, so it must be).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
@@ -40,13 +41,13 @@ __global__ void fill(float *p, uint64_t n, uint32_t seed)
     }
 }
 
-template <int U> void contig(const float *in, float *io, uint64_t npk, unsigned block, const Params &p,
-                             hipStream_t s)
+template <int U, unsigned MASK = 0x88, bool NTL = true, bool NTS = true>
+void contig(const float *in, float *io, uint64_t npk, unsigned block, const Params &p, hipStream_t s)
 {
     const unsigned g = grid_for((uint64_t) block * U, npk, 0);
     Params q = p;
-    q.wt_xcd = 0x88;
-    hipLaunchKernelGGL((k_contig<C, U, true, true, true>), dim3(g), dim3(block), 0, s, in, io, 0, npk,
+    q.wt_xcd = MASK;
+    hipLaunchKernelGGL((k_contig<C, U, NTL, NTS, true>), dim3(g), dim3(block), 0, s, in, io, 0, npk,
                        npk * 4, 0, q, g, block);
 }
 
@@ -74,7 +75,13 @@ int main(int argc, char **argv)
     std::vector<V> vs = {{"u4_b256", contig<4>, 256},  {"u2_b256", contig<2>, 256},
                          {"u1_b256", contig<1>, 256},  {"u4_b512", contig<4>, 512},
                          {"u2_b512", contig<2>, 512},  {"u1_b512", contig<1>, 512},
-                         {"u1_b1024", contig<1>, 1024}, {"u2_b1024", contig<2>, 1024}};
+                         {"u1_b1024", contig<1>, 1024}, {"u2_b1024", contig<2>, 1024},
+                         // one packet per lane: store policy masks and cache flavours
+                         {"u1_b256_wt00", contig<1, 0x00>, 256}, {"u1_b256_wt08", contig<1, 0x08>, 256},
+                         {"u1_b256_wt80", contig<1, 0x80>, 256}, {"u1_b256_wtAA", contig<1, 0xAA>, 256},
+                         {"u1_b256_wtCC", contig<1, 0xCC>, 256}, {"u1_b256_wtFF", contig<1, 0xFF>, 256},
+                         {"u1_b256_plainload", contig<1, 0x88, false, true>, 256},
+                         {"u1_b256_plainstore", contig<1, 0x88, true, false>, 256}};
     // bits: one launch of each on a fresh copy of io0, against u4_b256's
     std::vector<float> h_ref(n), h_got(n);
     std::vector<int> same(vs.size(), 1);
