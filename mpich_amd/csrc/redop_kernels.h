@@ -30,6 +30,13 @@
 #ifndef MPIX_REDOP_UNROLL
 #define MPIX_REDOP_UNROLL 1
 #endif
+#ifndef MPIX_REDOP_UNROLL32
+// 32-byte units: 64-unit runs per lane per operand -- one since round 5 (two
+// before): C_LONG_DOUBLE_COMPLEX and COMPLEX32 SUM +6-7 %, the pair types'
+// MINLOC / MAXLOC and the complex PROD even (tools/gpu_u_ab.sh,
+// profiles/r05_unroll32_ab.json)
+#define MPIX_REDOP_UNROLL32 1
+#endif
 #ifndef MPIX_REDOP_NT_LOAD
 #define MPIX_REDOP_NT_LOAD 1
 #endif
@@ -921,7 +928,7 @@ hipError_t launch_contig(const void *in, void *io, uint64_t count, const Params 
         // flight as k_contig's four packets; operands off the 16-byte grid go
         // element-wise
         if (((ai | ao) & 15) == 0) {
-            constexpr int U32 = 2;
+            constexpr int U32 = MPIX_REDOP_UNROLL32;
             unsigned grid = grid_for((uint64_t) kContig32Block * U32, count, cfg.max_grid);
             Params p = prm;
             p.done = nullptr;
@@ -1039,7 +1046,7 @@ hipError_t launch_tree(const void *const *ins, int k, void *out, uint64_t count,
         if (k == 2 && pres == 3u &&
             ((ao | reinterpret_cast<uintptr_t>(ins[0]) | reinterpret_cast<uintptr_t>(ins[1])) & 15) ==
                 0) {
-            constexpr int U32 = 2;
+            constexpr int U32 = MPIX_REDOP_UNROLL32;
             const unsigned grid = grid_for((uint64_t) kContig32Block * U32, count, cfg.max_grid);
             Params p = prm;
             p.done = nullptr;
@@ -1156,7 +1163,7 @@ hipError_t launch_batch(const void *const *ins, void *const *ios, const uint64_t
     if constexpr (sizeof(T) > 16) {
         // 32-byte units: the 16-byte-aligned triples as one k_batch32 launch,
         // the others element-wise one launch each
-        constexpr int U32 = 2;
+        constexpr int U32 = MPIX_REDOP_UNROLL32;
         const uint64_t tile = (uint64_t) kContig32Block * U32;
         BatchTab tab;
         int n = 0;
