@@ -874,6 +874,13 @@ def size_sweep(inb, inout, n, stream, nbytes_alg):
 
 
 # ------------------------------------------------------------------ N > 1
+def progress(rank, what):
+    """one stderr line per leg from rank 0 (long N > 1 runs show they move)"""
+    if rank == 0:
+        sys.stderr.write('[bench %s] %s\n' % (time.strftime('%H:%M:%S'), what))
+        sys.stderr.flush()
+
+
 def schedule_ran(cc, requested, kind='rs'):
     """which schedule the last collective on communicator `cc` actually ran
     (MPIX_Comm_get_state): a requested pull whose windows failed verification
@@ -945,6 +952,7 @@ def multi_gpu(args, world, rank, dev):
     # with every half-step's combine split onto the second stream (overlap
     # threshold 1 byte) and with none split (0).  A failure in either form
     # fails the run: the shipped default must never be timed unchecked.
+    progress(rank, 'value leg: parity gate')
     shipped_overlap = cc.rh_overlap()
     rc_small = (1 << 16) + 3
     sends = [rsb_inputs_host(r, world, rc_small) for r in range(world)]
@@ -981,6 +989,7 @@ def multi_gpu(args, world, rank, dev):
                                              'recursive_halving', workspace=ws),
                     'MPIX_Reduce_scatter_block')
 
+    progress(rank, 'value leg: %d warmup + %d timed calls' % (args.warmup, args.steps))
     for _ in range(args.warmup):
         step()
     dist.barrier()
@@ -1006,6 +1015,7 @@ def multi_gpu(args, world, rank, dev):
     cc.set_step_timing(False)
     cc.set_rh_overlap(shipped_overlap)
     steps = cc.step_times()
+    progress(rank, 'value leg: defaults A/B')
     ab = None if args.no_ab else defaults_ab(cc, step, recv, dev, args.ab_reps, args.ab_rounds)
     comb_ms = sum(s['ms'] for s in steps if s['phase'] == 'combine')
     exch_ms = sum(s['ms'] for s in steps if s['phase'] == 'exchange')
@@ -1143,6 +1153,7 @@ def rsb_secondary(args, world, rank, dev, out):
     legs.append(('recursive_halving_pull_shared', 'recursive_halving_pull', True))
     shared = None
     for name, algo, on_shared in legs:
+        progress(rank, 'reduce-scatter leg %s' % name)
         if on_shared and shared is None:
             try:        # collective: every rank gets the memory, or none does
                 shared = cc.shared_tensor(total, torch.float32)
@@ -1264,6 +1275,7 @@ def allreduce_secondary(args, world, rank, dev, res):
                                                         cc, 'pull'), 'MPIX_Allreduce'))):
         if name == 'rccl_all_reduce' and dist.get_backend() != 'nccl':
             continue
+        progress(rank, 'allreduce leg %s' % name)
         if name == 'c_pull_shared':
             try:
                 sh_in = cc.shared_tensor(n, torch.float32)

@@ -5,10 +5,15 @@
 # hold), where every pull leg must be reported as "fell back to ..." and not
 # timed under the pull's name.
 # usage (on the GPU box): P=4 bash tools/gpu_rehearse.sh
+# (RSB=<bytes per rank> STEPS=<k> MODES="normal" for the full-size form: round 5
+# ran P=8 RSB=4294967296 STEPS=2 MODES=normal, the driver's N = 8 shape)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 P=${P:-4}
+RSB=${RSB:-268435456}
+STEPS=${STEPS:-3}
+MODES=${MODES:-normal fault}
 O=gpurun_out/rehearse
 rm -rf $O && mkdir -p $O
 summ() {
@@ -22,11 +27,12 @@ for sec in ('reduce_scatter_block_other', 'allreduce'):
             print(' ', sec, k, 'ran:', v.get('schedule_ran'), 'ms:', v.get('ms'), 'error:', v.get('error'))
 " $1
 }
-for mode in normal fault; do
+for mode in $MODES; do
     if [ $mode = fault ]; then export MPIX_COLL_WINDOW_FAULT=1; fi
     # bench.py starts the P ranks itself (no torchrun): the driver's own form
-    MPIX_BENCH_SAME_DEVICE=1 MPIX_BENCH_BACKEND=gloo timeout -k 10 500 python3 bench.py --gpus $P \
-        --steps 3 --warmup 1 --count 67108864 --rsb-bytes 268435456 > $O/n${P}_$mode.json 2> $O/n${P}_$mode.err
+    MPIX_BENCH_SAME_DEVICE=1 MPIX_BENCH_BACKEND=gloo timeout -k 10 ${LIMIT:-500} python3 bench.py --gpus $P \
+        --steps $STEPS --warmup 1 --ab-reps 1 --count 67108864 --rsb-bytes $RSB $BENCH_ARGS \
+        > $O/n${P}_$mode.json 2> $O/n${P}_$mode.err
     rc=$?
     echo "$mode rc=$rc"
     summ $O/n${P}_$mode.json || tail -20 $O/n${P}_$mode.err
