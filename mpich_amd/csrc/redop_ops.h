@@ -33,13 +33,41 @@ template <> struct Wide<uint64_t> { using type = uint64_t; };
 template <> struct Wide<__int128> { using type = unsigned __int128; };
 template <> struct Wide<unsigned __int128> { using type = unsigned __int128; };
 
+// 1-byte MAX / MIN four per dword (combine16 uses apply4 for 1-byte
+// combiners): a byte in the high half of a 16-bit lane whose low half is zero
+// keeps its order as a 16-bit integer of the same signedness, so two packed
+// 16-bit max / min (v_pk_max_[iu]16) do the odd and the even bytes and one
+// v_perm_b32 interleaves them back -- 9 VALU per 4 elements.  Integers have no
+// NaN or signed zero, so this is (a > b) ? a : b byte for byte
+// (tests/test_swar.py checks every byte pair in every lane).
+template <typename T, bool MAX> MPIX_DEV uint32_t minmax_bytes(uint32_t a, uint32_t b)
+{
+    typedef __attribute__((ext_vector_type(2)))
+        typename std::conditional<std::is_signed<T>::value, short, unsigned short>::type v2;
+    const uint32_t m = 0xff00ff00u;
+    const v2 ao = __builtin_bit_cast(v2, a & m), bo = __builtin_bit_cast(v2, b & m);
+    const v2 ae = __builtin_bit_cast(v2, (a << 8) & m), be = __builtin_bit_cast(v2, (b << 8) & m);
+    uint32_t ro, re;
+    if constexpr (MAX) {
+        ro = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(ao, bo));
+        re = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(ae, be));
+    } else {
+        ro = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(ao, bo));
+        re = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(ae, be));
+    }
+    // bytes 0..3 = re.b1, ro.b1, re.b3, ro.b3 (selector 0-3: re, 4-7: ro)
+    return __builtin_amdgcn_perm(ro, re, 0x07030501u);
+}
+
 template <typename T> struct IMax {
     using unit = T;
     static MPIX_DEV T apply(T a, T b, const Params &) { return (a > b) ? a : b; }
+    static MPIX_DEV uint32_t apply4(uint32_t a, uint32_t b) { return minmax_bytes<T, true>(a, b); }
 };
 template <typename T> struct IMin {
     using unit = T;
     static MPIX_DEV T apply(T a, T b, const Params &) { return (a < b) ? a : b; }
+    static MPIX_DEV uint32_t apply4(uint32_t a, uint32_t b) { return minmax_bytes<T, false>(a, b); }
 };
 template <typename T> struct ISum {
     using unit = T;

@@ -76,3 +76,40 @@ def test_swar_fortran_logical1_every_byte_pair():
                 exp = np.where(c, np.uint8(ftrue & 0xff), np.uint8(ffalse & 0xff))
                 g = got[k].astype(np.uint32).view(np.uint8).reshape(-1, 4)
                 assert np.array_equal(g, exp), (k, lane, ftrue, ffalse)
+
+
+def _minmax_bytes(A, B, signed, is_max):
+    """IMax / IMin<1-byte T>::apply4 (redop_ops.h minmax_bytes): each byte in
+    the high half of a 16-bit lane (low half zero), a packed 16-bit max / min
+    of that signedness for the odd and for the even bytes, then the bytes
+    interleaved back"""
+    m = np.uint32(0xff00ff00)
+    t = np.int16 if signed else np.uint16
+    f = np.maximum if is_max else np.minimum
+    ro = f((A & m).view(t), (B & m).view(t)).view(np.uint32)
+    re = f(((A << np.uint32(8)) & m).view(t), ((B << np.uint32(8)) & m).view(t)).view(np.uint32)
+    # v_perm_b32(ro, re, 0x07030501): bytes re.b1, ro.b1, re.b3, ro.b3
+    rb, ob = re.view(np.uint8).reshape(-1, 4), ro.view(np.uint8).reshape(-1, 4)
+    return np.stack([rb[:, 1], ob[:, 1], rb[:, 3], ob[:, 3]], 1)
+
+
+def test_swar_minmax_every_byte_pair():
+    """1-byte MAX / MIN four per dword against (a > b) ? a : b and
+    (a < b) ? a : b (mpl_base.h:105-106 via op_fns.c), signed and unsigned,
+    every pair of byte values in every lane beside random neighbours"""
+    a8, b8 = np.meshgrid(np.arange(256, dtype=np.uint8), np.arange(256, dtype=np.uint8))
+    a8, b8 = a8.ravel(), b8.ravel()
+    rng = np.random.default_rng(0x5EED5C)
+    for lane in range(4):
+        fill_a = rng.integers(0, 256, (a8.size, 4), dtype=np.uint8)
+        fill_b = rng.integers(0, 256, (a8.size, 4), dtype=np.uint8)
+        fill_a[:, lane], fill_b[:, lane] = a8, b8
+        A = fill_a.copy().view(np.uint32).ravel()
+        B = fill_b.copy().view(np.uint32).ravel()
+        for signed in (False, True):
+            va = fill_a.view(np.int8) if signed else fill_a
+            vb = fill_b.view(np.int8) if signed else fill_b
+            for is_max in (True, False):
+                exp = np.where(va > vb, va, vb) if is_max else np.where(va < vb, va, vb)
+                got = _minmax_bytes(A, B, signed, is_max)
+                assert np.array_equal(got, exp.view(np.uint8)), (lane, signed, is_max)
