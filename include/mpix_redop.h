@@ -383,9 +383,11 @@ int MPIX_Reduce_local_batch_async(const void *const *inbufs, void *const *inoutb
  * grid-stride loop).  The packets-per-thread unroll is a compile-time
  * constant (MPIX_REDOP_UNROLL).  Env MPIX_REDOP_BLOCK / MPIX_REDOP_MAXGRID
  * override the defaults at first use.  Kernels that read page-locked host
- * memory over PCIe (zero-copy) run at most 32 looping blocks unless max_grid
- * is smaller, so loads and stores share the link both ways; env
- * MPIX_REDOP_ZC_GRID sets that cap (0: none). */
+ * memory over PCIe (zero-copy) run at most 16384 threads' worth of looping
+ * blocks (256 at the default 64 threads) unless max_grid is smaller, so loads
+ * and stores share the link both ways; env MPIX_REDOP_ZC_GRID sets that cap
+ * in blocks (0: none).  Defaults: 64-thread blocks, one 16-byte packet per
+ * lane per operand. */
 int MPIX_Redop_set_launch(int block_threads, int max_grid);
 int MPIX_Redop_get_launch(int *block_threads, int *unroll, int *max_grid);
 

@@ -242,19 +242,27 @@ const Entry *gpu_entry(uint32_t opi, uint32_t it)
 
 // ---------------------------------------------------------------- state
 std::atomic<long long> g_ftrue{1}, g_ffalse{0};
-std::atomic<int> g_block{256}, g_max_grid{0};
+// One-wave (64-thread) blocks of one packet per lane (round 5): kernel-trace
+// durations of the synchronous 1 GiB fp32 SUM call 478 -> 460 us against
+// 256-thread blocks, 448.7 against 480.6 us back to back; config-3 rows
+// +3.3 % (median), the multi-input fold +4-8 % (tools/contig_u_probe.hip,
+// tools/gpu_env_ab.sh, profiles/r05_block64_ab.json).
+std::atomic<int> g_block{64}, g_max_grid{0};
 // Grid cap of kernels reading page-locked host memory over PCIe (zero-copy):
 // with one tile per block every block loads its whole tile (host to device)
 // before it stores (device to host), and a grid of a few hundred blocks is
 // one round, so the two link directions take turns.  Looping blocks keep
-// both busy: with 4 packets per lane 32 blocks took 4 MiB 235 -> 186 us,
+// both busy: with 4 packets per lane 32 blocks of 256 took 4 MiB 235 -> 186 us,
 // 16 MiB 780 -> 655 us, 1 GiB 39.2 -> 38.1 ms (profiles/r04_pinned_grid.json);
-// with one packet per lane (round 5) 64 blocks hold the same bytes in flight:
-// 1 MiB 69 -> 55 us, 4 MiB 238 -> 182 us, 16 MiB 769 -> 655 us, 256 MiB
-// 10.1 -> 9.4 ms, where 32 gave 59 / 197 / 682 us / 9.8 ms
-// (tools/pinned_grid.py, profiles/r05_pinned_grid.json).  MPIX_REDOP_ZC_GRID
-// overrides (0: uncapped).
-std::atomic<int> g_zc_grid{64};
+// with one packet per lane (round 5) twice the lanes hold the same bytes in
+// flight -- 64 blocks of 256: 1 MiB 69 -> 55 us, 4 MiB 238 -> 182 us, 16 MiB
+// 769 -> 655 us, 256 MiB 10.1 -> 9.4 ms, where 32 gave 59 / 197 / 682 us /
+// 9.8 ms (tools/pinned_grid.py, profiles/r05_pinned_grid.json).  The default
+// cap is that many lanes (kZcLanes) in blocks of the current size;
+// MPIX_REDOP_ZC_GRID sets it in blocks (0: uncapped).
+constexpr int kZcLanes = 64 * 256;
+constexpr int kZcAuto = -1;
+std::atomic<int> g_zc_grid{kZcAuto};
 // Store policy of the contiguous and multi-input kernels and the two-slot tree
 // (MPIX_Redop_set_store_policy): the blocks running on the XCDs of g_wt_xcd
 // store write-through (sc0 sc1), the others non-temporally.  Two XCDs of eight
@@ -579,7 +587,9 @@ LaunchCfg launch_cfg()
 LaunchCfg launch_cfg(bool zero_copy)
 {
     LaunchCfg c = launch_cfg();
-    const int z = g_zc_grid.load();
+    int z = g_zc_grid.load();
+    if (z == kZcAuto)
+        z = kZcLanes / (c.block > 0 ? c.block : 64);
     if (zero_copy && z > 0 && (c.max_grid <= 0 || c.max_grid > z))
         c.max_grid = z;
     return c;

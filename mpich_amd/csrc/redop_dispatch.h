@@ -30,7 +30,7 @@ struct Params {
     uint32_t wt_xcd = 0;        // and every block running on an XCD whose bit is set
 };
 
-constexpr unsigned kSignalMaxGrid = 16;     // 16 tiles of 256 x 1 packets: 64 KiB per operand
+constexpr unsigned kSignalMaxGrid = 64;     // 64 tiles of 64 x 1 packets: 64 KiB per operand
 
 struct LaunchCfg {
     int block;          // threads per block (multiple of 64)

@@ -1080,22 +1080,27 @@ hipError_t launch_tree(const void *const *ins, int k, void *out, uint64_t count,
         // with nine streams the waves, not each wave's bytes in flight, carry
         // the rate.  The store policy: +5 % at k = 2, +3.8 % at k = 4, neutral
         // above.
-        const unsigned per = k == 2 ? 256 * 2 : k == 4 ? 256 * 2 : 256;
+        // One-wave (64-thread) blocks, as the contiguous kernel: k = 2 / 4 / 8
+        // / 16 at 6.84-6.96 / 6.48-6.61 / 6.58-6.67 / 6.06-6.45 TB/s against
+        // 6.64-6.76 / 6.36-6.43 / 6.25-6.28 / 5.82-6.43 with 256 threads
+        // (r05_tree_forms.json, last run).
+        constexpr unsigned kTreeBlock = 64;
+        const unsigned per = (k == 2 || k == 4) ? kTreeBlock * 2 : kTreeBlock;
         const unsigned grid = grid_for(per, npk, 0);
         set_store_policy(p, cfg, grid);
         if constexpr (sizeof(T) <= 16) {
             if (k == 2)     // out = a OP b (recursive halving's combine_to)
-                hipLaunchKernelGGL((k_contig_tree_rec<C, 2, 2>), dim3(grid), dim3(256), 0, s, mi, k,
-                                   pres, tout, head, npk, tail_start, ntail, p);
-            else if (k == 4)
-                hipLaunchKernelGGL((k_contig_tree<C, 4, 2>), dim3(grid), dim3(256), 0, s, mi, k,
-                                   pres, tout, head, npk, tail_start, ntail, p);
-            else if (k == 8)    // the P = 8 pull's fold
-                hipLaunchKernelGGL((k_contig_tree_rec<C, 8, 1>), dim3(grid), dim3(256), 0, s, mi, k,
-                                   pres, tout, head, npk, tail_start, ntail, p);
-            else
-                hipLaunchKernelGGL((k_contig_tree_rec<C, kMaxMulti, 1>), dim3(grid), dim3(256), 0, s,
+                hipLaunchKernelGGL((k_contig_tree_rec<C, 2, 2>), dim3(grid), dim3(kTreeBlock), 0, s,
                                    mi, k, pres, tout, head, npk, tail_start, ntail, p);
+            else if (k == 4)
+                hipLaunchKernelGGL((k_contig_tree<C, 4, 2>), dim3(grid), dim3(kTreeBlock), 0, s, mi,
+                                   k, pres, tout, head, npk, tail_start, ntail, p);
+            else if (k == 8)    // the P = 8 pull's fold
+                hipLaunchKernelGGL((k_contig_tree_rec<C, 8, 1>), dim3(grid), dim3(kTreeBlock), 0, s,
+                                   mi, k, pres, tout, head, npk, tail_start, ntail, p);
+            else
+                hipLaunchKernelGGL((k_contig_tree_rec<C, kMaxMulti, 1>), dim3(grid), dim3(kTreeBlock),
+                                   0, s, mi, k, pres, tout, head, npk, tail_start, ntail, p);
         }
     } else {
         hipLaunchKernelGGL((k_elem_tree<C>), dim3(grid_for(256 * 4, count, 0)), dim3(256), 0, s,

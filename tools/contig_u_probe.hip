@@ -81,7 +81,9 @@ int main(int argc, char **argv)
                          {"u1_b256_wt80", contig<1, 0x80>, 256}, {"u1_b256_wtAA", contig<1, 0xAA>, 256},
                          {"u1_b256_wtCC", contig<1, 0xCC>, 256}, {"u1_b256_wtFF", contig<1, 0xFF>, 256},
                          {"u1_b256_plainload", contig<1, 0x88, false, true>, 256},
-                         {"u1_b256_plainstore", contig<1, 0x88, true, false>, 256}};
+                         {"u1_b256_plainstore", contig<1, 0x88, true, false>, 256},
+                         {"u1_b128", contig<1>, 128}, {"u1_b64", contig<1>, 64},
+                         {"u2_b128", contig<2>, 128}};
     // bits: one launch of each on a fresh copy of io0, against u4_b256's
     std::vector<float> h_ref(n), h_got(n);
     std::vector<int> same(vs.size(), 1);

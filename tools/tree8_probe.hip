@@ -42,37 +42,37 @@ __global__ void fill(float *p, uint64_t n, uint32_t seed)
     }
 }
 
-template <int KMAX, int U> void tree(const MultiIn<float> &mi, int k, float *o, uint64_t npk,
-                                      const Params &p, hipStream_t s)
+template <int KMAX, int U, unsigned B = 256> void tree(const MultiIn<float> &mi, int k, float *o,
+                                                        uint64_t npk, const Params &p, hipStream_t s)
 {
-    hipLaunchKernelGGL((k_contig_tree<C, KMAX, U>), dim3(grid_for(256 * U, npk, 0)), dim3(256), 0, s,
+    hipLaunchKernelGGL((k_contig_tree<C, KMAX, U>), dim3(grid_for(B * U, npk, 0)), dim3(B), 0, s,
                        mi, k, (1u << k) - 1, o, 0, npk, npk * 4, 0, p);
 }
-template <int KMAX, int U> void rec(const MultiIn<float> &mi, int k, float *o, uint64_t npk,
-                                     const Params &p, hipStream_t s)
+template <int KMAX, int U, unsigned B = 256> void rec(const MultiIn<float> &mi, int k, float *o,
+                                                       uint64_t npk, const Params &p, hipStream_t s)
 {
-    hipLaunchKernelGGL((k_contig_tree_rec<C, KMAX, U>), dim3(grid_for(256 * U, npk, 0)), dim3(256), 0,
+    hipLaunchKernelGGL((k_contig_tree_rec<C, KMAX, U>), dim3(grid_for(B * U, npk, 0)), dim3(B), 0,
                        s, mi, k, (1u << k) - 1, o, 0, npk, npk * 4, 0, p);
 }
-template <int U> void multi(const MultiIn<float> &mi, int k, float *o, uint64_t npk, const Params &p,
-                            hipStream_t s)
+template <int U, unsigned B = 256> void multi(const MultiIn<float> &mi, int k, float *o, uint64_t npk,
+                                              const Params &p, hipStream_t s)
 {
     // k - 1 inputs folded into o (which then holds garbage; timing only)
     MultiIn<float> m{};
     for (int q = 1; q < k; ++q)
         m.p[q - 1] = mi.p[q];
-    const unsigned g = grid_for(256 * U, npk, 0);
-    hipLaunchKernelGGL((k_contig_multi<C, U>), dim3(g), dim3(256), 0, s, m, k - 1, o, 0, npk, npk * 4,
-                       0, p, g, 256u);
+    const unsigned g = grid_for(B * U, npk, 0);
+    hipLaunchKernelGGL((k_contig_multi<C, U>), dim3(g), dim3(B), 0, s, m, k - 1, o, 0, npk, npk * 4,
+                       0, p, g, B);
 }
 
 // the headline kernel's form for comparison: o OP= slot 0 in place (k_contig, U packets per lane)
-template <int U> void contig(const MultiIn<float> &mi, int, float *o, uint64_t npk, const Params &p,
-                             hipStream_t s)
+template <int U, unsigned B = 256> void contig(const MultiIn<float> &mi, int, float *o, uint64_t npk,
+                                               const Params &p, hipStream_t s)
 {
-    const unsigned g = grid_for(256 * U, npk, 0);
-    hipLaunchKernelGGL((k_contig<C, U, true, true, true>), dim3(g), dim3(256), 0, s, mi.p[0], o, 0, npk,
-                       npk * 4, 0, p, g, 256u);
+    const unsigned g = grid_for(B * U, npk, 0);
+    hipLaunchKernelGGL((k_contig<C, U, true, true, true>), dim3(g), dim3(B), 0, s, mi.p[0], o, 0, npk,
+                       npk * 4, 0, p, g, B);
 }
 
 typedef void (*LaunchFn)(const MultiIn<float> &, int, float *, uint64_t, const Params &, hipStream_t);
@@ -127,6 +127,12 @@ int main(int argc, char **argv)
         {"k16_multi15_u1_wt", 16, wt<multi<1>>, nullptr},
         {"k2_contig_u4_wt", 2, wt<contig<4>>, nullptr}, {"k2_contig_u2_wt", 2, wt<contig<2>>, nullptr},
         {"k2_contig_u1_wt", 2, wt<contig<1>>, nullptr},
+        // 64-thread (one-wave) blocks
+        {"k2_contig_u1_b64_wt", 2, wt<contig<1, 64>>, nullptr},
+        {"k2_rec2x2_b64_wt", 2, wt<rec<2, 2, 64>>, "k2_slots2x4_wt"}, {"k2_rec2x1_b64_wt", 2, wt<rec<2, 1, 64>>, "k2_slots2x4_wt"},
+        {"k4_slots4x2_b64_wt", 4, wt<tree<4, 2, 64>>, "k4_slots4x2"}, {"k4_rec4x1_b64_wt", 4, wt<rec<4, 1, 64>>, "k4_slots4x2"},
+        {"k8_rec8x1_b64_wt", 8, wt<rec<8, 1, 64>>, "k8_slots8x2"}, {"k16_rec16x1_b64_wt", 16, wt<rec<16, 1, 64>>, "k16_slots16x1"},
+        {"k8_multi7_u1_b64_wt", 8, wt<multi<1, 64>>, nullptr}, {"k16_multi15_u1_b64_wt", 16, wt<multi<1, 64>>, nullptr},
     };
     std::vector<int> same(vs.size(), -1);
     std::vector<float> h_ref(n), h_got(n);
