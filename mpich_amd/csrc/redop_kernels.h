@@ -839,12 +839,12 @@ __device__ __forceinline__ T ld_source_nt(const T *p)
 template <class C>
 __global__ void __launch_bounds__(256)
 k_vector_s2(const typename C::unit *__restrict__ in, typename C::unit *__restrict__ io, uint64_t n,
-            Params prm, uint32_t nblk)
+            Params prm, uint32_t nblk, uint32_t nt)
 {
     using T = typename C::unit;
     using R = typename RawOf<2 * sizeof(T)>::type;
-    const uint64_t stride = (uint64_t) nblk * 256;        // 256-thread blocks (launch_vector)
-    for (uint64_t j = (uint64_t) blockIdx.x * 256 + threadIdx.x; j < n; j += stride) {
+    const uint64_t stride = (uint64_t) nblk * nt;
+    for (uint64_t j = (uint64_t) blockIdx.x * nt + threadIdx.x; j < n; j += stride) {
         T t;
         if (j + 1 < n) {
             R raw = reinterpret_cast<const R *>(io)[j];
@@ -909,7 +909,13 @@ inline void set_store_policy(Params &p, const LaunchCfg &cfg, unsigned grid)
 }
 
 // k_contig32's block (its __launch_bounds__)
-constexpr unsigned kContig32Block = 256;
+#ifndef MPIX_REDOP_VBLOCK
+#define MPIX_REDOP_VBLOCK 256       // the stride-2 vector target's block
+#endif
+#ifndef MPIX_REDOP_BLOCK32
+#define MPIX_REDOP_BLOCK32 256
+#endif
+constexpr unsigned kContig32Block = MPIX_REDOP_BLOCK32;
 
 // Contiguous launcher: chooses the packet or the element-wise kernel.
 template <class C>
@@ -1125,9 +1131,10 @@ hipError_t launch_vector(const void *in, void *io, uint64_t count, uint64_t bl, 
         s2 = bl == 1 && st == 2 && (reinterpret_cast<uintptr_t>(io) % (2 * sizeof(T))) == 0;
     if (s2) {
         if constexpr (sizeof(T) <= 16) {
-            const unsigned g2 = grid_for(256, n, cfg.max_grid);
-            hipLaunchKernelGGL((k_vector_s2<C>), dim3(g2), dim3(256), 0, s,
-                               static_cast<const T *>(in), static_cast<T *>(io), n, prm, g2);
+            constexpr unsigned kVb = MPIX_REDOP_VBLOCK;
+            const unsigned g2 = grid_for(kVb, n, cfg.max_grid);
+            hipLaunchKernelGGL((k_vector_s2<C>), dim3(g2), dim3(kVb), 0, s,
+                               static_cast<const T *>(in), static_cast<T *>(io), n, prm, g2, kVb);
         }
     } else if (bl == 1)
         hipLaunchKernelGGL((k_vector1<C>), dim3(grid), dim3(cfg.block), 0, s,

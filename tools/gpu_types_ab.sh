@@ -3,8 +3,8 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 bash tools/gpu_steps.sh "tests=random_parity or c3 or golden_on_gpu or batch or fuzz" || exit 1
-mkdir -p gpurun_out/uab2
+O=gpurun_out/${OUT:-uab2}; mkdir -p $O
 for i in 1 2; do
-  timeout -k 10 300 python3 tools/ab_types.py mpich_amd/libmpix_redop.so swar >> gpurun_out/uab2/types.jsonl || exit 1
-  timeout -k 10 300 python3 tools/ab_types.py mpich_amd/libmpix_redop_alt.so perbyte >> gpurun_out/uab2/types.jsonl || exit 1
+  timeout -k 10 300 python3 tools/ab_types.py mpich_amd/libmpix_redop.so ${LA:-shipped} >> $O/types.jsonl || exit 1
+  timeout -k 10 300 python3 tools/ab_types.py mpich_amd/libmpix_redop_alt.so ${LB:-alt} >> $O/types.jsonl || exit 1
 done
