@@ -909,11 +909,15 @@ inline void set_store_policy(Params &p, const LaunchCfg &cfg, unsigned grid)
 }
 
 // k_contig32's block (its __launch_bounds__)
+// One-wave blocks for the stride-2 vector target and the 32-byte units too
+// (round 5, tools/gpu_u_ab.sh against 256 threads, profiles/r05_block64_vec32.json):
+// config 5 0.449 -> 0.433 ms; LONG_DOUBLE_INT MINLOC / MAXLOC 6.74-6.78 ->
+// 7.06-7.09 TB/s, the complex long double / binary128 rows even to +2 %
 #ifndef MPIX_REDOP_VBLOCK
-#define MPIX_REDOP_VBLOCK 256       // the stride-2 vector target's block
+#define MPIX_REDOP_VBLOCK 64        // the stride-2 vector target's block
 #endif
 #ifndef MPIX_REDOP_BLOCK32
-#define MPIX_REDOP_BLOCK32 256
+#define MPIX_REDOP_BLOCK32 64
 #endif
 constexpr unsigned kContig32Block = MPIX_REDOP_BLOCK32;
 
