@@ -41,13 +41,13 @@ __global__ void fill(float *p, uint64_t n, uint32_t seed)
     }
 }
 
-template <int U, unsigned MASK = 0x88, bool NTL = true, bool NTS = true>
+template <int U, unsigned MASK = 0x88, bool NTL = true, bool NTS = true, bool GRP = true>
 void contig(const float *in, float *io, uint64_t npk, unsigned block, const Params &p, hipStream_t s)
 {
     const unsigned g = grid_for((uint64_t) block * U, npk, 0);
     Params q = p;
     q.wt_xcd = MASK;
-    hipLaunchKernelGGL((k_contig<C, U, NTL, NTS, true>), dim3(g), dim3(block), 0, s, in, io, 0, npk,
+    hipLaunchKernelGGL((k_contig<C, U, NTL, NTS, true, GRP>), dim3(g), dim3(block), 0, s, in, io, 0, npk,
                        npk * 4, 0, q, g, block);
 }
 
@@ -83,7 +83,12 @@ int main(int argc, char **argv)
                          {"u1_b256_plainload", contig<1, 0x88, false, true>, 256},
                          {"u1_b256_plainstore", contig<1, 0x88, true, false>, 256},
                          {"u1_b128", contig<1>, 128}, {"u1_b64", contig<1>, 64},
-                         {"u2_b128", contig<2>, 128}};
+                         {"u2_b128", contig<2>, 128},
+                         // one-wave blocks (the round-5 default): policy masks, 2 packets
+                         {"u1_b64_wt00", contig<1, 0x00>, 64}, {"u1_b64_wt08", contig<1, 0x08>, 64},
+                         {"u1_b64_wt80", contig<1, 0x80>, 64}, {"u1_b64_wtCC", contig<1, 0xCC>, 64},
+                         {"u1_b64_wt44", contig<1, 0x44>, 64}, {"u1_b64_wt11", contig<1, 0x11>, 64},
+                         {"u2_b64", contig<2>, 64}, {"u2_b64_alt", contig<2, 0x88, true, true, false>, 64}};
     // bits: one launch of each on a fresh copy of io0, against u4_b256's
     std::vector<float> h_ref(n), h_got(n);
     std::vector<int> same(vs.size(), 1);
