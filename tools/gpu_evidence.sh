@@ -19,6 +19,7 @@ python3 tools/pmc_summary.py --kt "$(find $O/kt -name '*kernel_stats.csv' | head
     --fetch "$(find $O/fetch -name '*counter_collection.csv' | head -n 1)" \
     --write "$(find $O/write -name '*counter_collection.csv' | head -n 1)" \
     --out $O/${R}_pmc_summary.json --stats-copy $O/${R}_rocprof_kernel_stats.csv \
+    --trace "$(find $O/kt -name '*kernel_trace.csv' | head -n 1)" \
     --traced-line $O/prof_bench.json > /dev/null && \
 timeout -k 10 500 python3 bench.py --pmc $O/${R}_pmc_summary.json > $O/bench.json 2> $O/bench.err
 rc=$?

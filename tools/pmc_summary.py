@@ -37,6 +37,10 @@ def main():
     ap.add_argument('--elem', type=int, default=4)
     ap.add_argument('--out', required=True)
     ap.add_argument('--stats-copy', required=True)
+    ap.add_argument('--trace', default=None,
+                    help='the kernel-trace CSV of the --kt pass: launches that started from an idle '
+                         'GPU (more than 5 us after the previous one ended: the synchronous loop and '
+                         "bench.py's idle-start event timing) averaged apart from back-to-back ones")
     ap.add_argument('--traced-line', default=None,
                     help="the traced bench run's own JSON line (its ms_per_step is kept beside the "
                          "traced kernel average: traced kernel <= step time)")
@@ -63,6 +67,22 @@ def main():
             achieved_GBs_from_trace=round(alg / avg_ns, 1),
             frac_from_trace=round(alg / avg_ns / 8000.0, 4),
             correction='hbm = (2*FETCH_SIZE + WRITE_SIZE) KiB * 1024 (gfx950 FETCH_SIZE half-count)')})
+    if a.trace:
+        rows = [r for r in csv.DictReader(open(a.trace)) if r['Kernel_Name'].startswith(a.kernel)]
+        rows.sort(key=lambda r: int(r['Start_Timestamp']))
+        idle, b2b = [], []
+        for i, r in enumerate(rows):
+            d = int(r['End_Timestamp']) - int(r['Start_Timestamp'])
+            gap = int(r['Start_Timestamp']) - int(rows[i - 1]['End_Timestamp']) if i else 10 ** 9
+            (idle if gap > 5000 else b2b).append(d)
+        kk = summary['kernels']['reduce_local_fp32_sum']
+        if idle:
+            kk['idle_start_launches'] = len(idle)
+            kk['idle_start_avg_ns'] = round(sum(idle) / len(idle), 1)
+            kk['frac_from_trace_idle_start'] = round(alg / (sum(idle) / len(idle)) / 8000.0, 4)
+        if b2b:
+            kk['back_to_back_launches'] = len(b2b)
+            kk['back_to_back_avg_ns'] = round(sum(b2b) / len(b2b), 1)
     if a.traced_line:
         line = json.loads(open(a.traced_line).read().strip().splitlines()[-1])
         kk = summary['kernels']['reduce_local_fp32_sum']
