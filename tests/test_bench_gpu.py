@@ -2,7 +2,8 @@
 its two ranks itself (no torchrun), both on device 0 over the gloo staged
 transport (the rehearsal knobs; RCCL refuses two ranks on one device), runs
 the recursive-halving reduce-scatter value leg with its bit-exact parity gate,
-and rank 0's one line carries n_gpus = 2 and the schedule that ran."""
+and rank 0's one line carries n_gpus = 2, the schedule that ran and the
+defaults A/B."""
 import json
 import os
 import subprocess
@@ -28,3 +29,9 @@ def test_bench_gpus_2_self_launched_line():
     d = json.loads(lines[0])
     assert d['n_gpus'] == 2 and d['schedule_ran'] == 'recursive_halving', d
     assert d['parity']['bit_exact_all_ranks'] and d['value'] > 0, d
+    # the overlap x store-policy defaults timed beside the
+    # shipped one, every variant first bit-identical on every rank
+    ab = d['defaults_ab']
+    for k in ('overlap_on_policy_on', 'overlap_off_policy_on', 'overlap_on_policy_off',
+              'overlap_off_policy_off'):
+        assert ab[k]['bit_identical_to_shipped_all_ranks'] and ab[k]['ms_per_step'] > 0, ab
