@@ -14,9 +14,9 @@
 #   bench                   the default bench.py line
 #   pmcwide                 tools/pmc_wide.py: FETCH/WRITE passes over the 32-byte-unit kernels
 #   evidence                tools/gpu_evidence.sh (R=r04): rocprofv3 stats + PMC passes + bench
-#   treeab                  tools/multi_probe.py, tree folds k = 4, 8, 16: the 8-slot x 2-packet
-#                           form (MPIX_REDOP_TREE8=1) against the 16-slot form, alternating processes
 #   pmctree                 FETCH/WRITE passes over the tree folds k = 8, 16 (default form)
+# (round 5's treeab / treeab2 / treeab3 steps A/B-ed two library knobs since removed;
+#  their results are profiles/r05_tree_knob_ab.json, the step text in git history)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -60,31 +60,6 @@ for step in "$@"; do
                       "$(find $O/pm_write -name '*counter_collection.csv' | head -n 1)" \
                       $O/r04_pmc_multi.json || exit $? ;;
         bench) run bench 600 python3 bench.py || exit $? ;;
-        treeab) for i in 1 2 3; do
-                    for f in 0 1; do
-                        run treeab_${f}_$i 120 env MPIX_REDOP_TREE8=$f python3 tools/multi_probe.py \
-                            --ks 7 --tree-ks 4,8,16 || exit $?
-                        echo "{\"tree8\": $f, \"run\": $i, \"line\": $(tail -n 1 $O/treeab_${f}_$i.out)}" \
-                            >> $O/treeab.jsonl
-                    done
-                done ;;
-        treeab2) for i in 1 2; do
-                     for cfg in "0 0 0" "1 0 0" "1 1 0" "0 0 4352" "1 0 4352" "1 1 4352"; do
-                         set -- $cfg
-                         run treeab2 120 env MPIX_REDOP_TREE8=$1 MPIX_REDOP_TREE_WT=$2 python3 \
-                             tools/multi_probe.py --ks 7 --tree-ks 4,8,16 --skew $3 || exit $?
-                         tail -n 1 $O/treeab2.out >> $O/treeab2.jsonl
-                     done
-                 done ;;
-        treeab3) for i in 1 2; do
-                     for cfg in "0 0" "1 0" "0 1" "1 1"; do
-                         set -- $cfg
-                         ip=""; if [ $2 = 1 ]; then ip="--tree-inplace"; fi
-                         run treeab3 120 env MPIX_REDOP_TREE8=$1 python3 \
-                             tools/multi_probe.py --ks 7 --tree-ks 2,4,8,16 $ip || exit $?
-                         tail -n 1 $O/treeab3.out >> $O/treeab3.jsonl
-                     done
-                 done ;;
         pmctree) run pmctree_fetch 180 rocprofv3 --pmc FETCH_SIZE -T -d $O/pt_fetch -o f \
                      --output-format csv -- python3 tools/multi_probe.py --ks 7 --tree-ks 8,16 || exit $?
                  run pmctree_write 180 rocprofv3 --pmc WRITE_SIZE -T -d $O/pt_write -o w \
