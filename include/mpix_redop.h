@@ -370,9 +370,10 @@ const char *MPIX_Redop_error_string(int code);
  * segments run in no particular order); zero counts are skipped; every
  * operand must be reachable from the stream's device, as for
  * MPIX_Reduce_local_async.  All checks happen before any device work.
- * MPI_REPLACE / MPI_NO_OP / MPIX_EQUAL and operands that are not element-aligned
- * (for the 32-byte pair and complex types: not 16-byte aligned) are issued one
- * launch per triple. */
+ * MPI_REPLACE / MPI_NO_OP / MPIX_EQUAL, operands that are not element-aligned
+ * (for the 32-byte pair and complex types: not 16-byte aligned) and triples
+ * with a page-locked host operand (read over PCIe by the capped, looping
+ * zero-copy grid) are issued one launch per triple. */
 #define MPIX_BATCH_MAX 64
 int MPIX_Reduce_local_batch_async(const void *const *inbufs, void *const *inoutbufs,
                                   const MPIX_Aint *counts, int k, MPIX_Datatype datatype,
