@@ -421,57 +421,6 @@ k_contig_multi(MultiIn<typename C::unit> ins, int k, typename C::unit *__restric
     }
 }
 
-// The same in-order fold unrolled over KMAX input slots (inputs q >= k skipped
-// by uniform branches): UPFRONT issues every present input's packet before the
-// first combine, otherwise each is loaded where the fold reaches it and the
-// compiler schedules the loads.  One packet per lane.
-template <class C, int KMAX, bool UPFRONT>
-__global__ void __launch_bounds__(256)
-k_contig_multi_k(MultiIn<typename C::unit> ins, int k, typename C::unit *__restrict__ io,
-                 uint64_t head, uint64_t npk, uint64_t tail_start, uint32_t ntail, Params prm,
-                 uint32_t nblk, uint32_t nthreads)
-{
-    v4u *__restrict__ vio = reinterpret_cast<v4u *>(io + head);
-    const uint64_t nt = nthreads;
-    const uint64_t stride = (uint64_t) nblk * nt;
-    const bool wt = wt_block(prm);
-    for (uint64_t i = (uint64_t) blockIdx.x * nt + threadIdx.x; i < npk; i += stride) {
-        v4u acc = ld16<true>(vio + i);
-        if constexpr (UPFRONT) {
-            v4u v[KMAX];
-#pragma unroll
-            for (int q = 0; q < KMAX; ++q)
-                if (q < k)
-                    v[q] = ld16<true>(reinterpret_cast<const v4u *>(ins.p[q] + head) + i);
-#pragma unroll
-            for (int q = 0; q < KMAX; ++q)
-                if (q < k)
-                    acc = combine16<C>(acc, v[q], prm);
-        } else {
-#pragma unroll
-            for (int q = 0; q < KMAX; ++q)
-                if (q < k)
-                    acc = combine16<C>(acc, ld16<true>(reinterpret_cast<const v4u *>(ins.p[q] + head) + i),
-                                       prm);
-        }
-        st16_pol<true>(vio + i, acc, wt);
-    }
-    if (blockIdx.x == 0) {
-        for (uint64_t t = threadIdx.x; t < head; t += nt) {
-            typename C::unit a = io[t];
-            for (int q = 0; q < k; ++q)
-                a = C::apply(a, ins.p[q][t], prm);
-            io[t] = a;
-        }
-        for (uint64_t t = threadIdx.x; t < ntail; t += nt) {
-            typename C::unit a = io[tail_start + t];
-            for (int q = 0; q < k; ++q)
-                a = C::apply(a, ins.p[q][tail_start + t], prm);
-            io[tail_start + t] = a;
-        }
-    }
-}
-
 template <class C>
 __global__ void __launch_bounds__(1024)
 k_elem_multi(MultiIn<typename C::unit> ins, int k, typename C::unit *__restrict__ io, uint64_t n,

@@ -8,8 +8,10 @@
 //   rec8xU      k_contig_tree_rec<C, 8, U> for U = 1, 2, 4 (the fold's pair order,
 //               slots loaded as the recursion reaches them)
 // plus the multi-input folds of 7 and 15 inputs (U = 2 shipped in round 4, and
-// U = 1), the 2- and 4-slot forms, and each with the store policy (_wt); and
-// the in-order multi-input fold unrolled over 8 / 16 slots (k_contig_multi_k).
+// U = 1), the 2- and 4-slot forms, and each with the store policy (_wt).
+// (Round 5 also timed the in-order multi-input fold unrolled over 8 / 16 slots,
+// k_contig_multi_k, since removed: profiles/r05_multi_unrolled.json, source in
+// git history.)
 // Every tree form's output is checked bit-identical to the shipped form's.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
 //        -Impich_amd/csrc -Iinclude -o tools/bin/tree8_probe tools/tree8_probe.hip
@@ -65,18 +67,6 @@ template <int U, unsigned B = 256> void multi(const MultiIn<float> &mi, int k, f
     const unsigned g = grid_for(B * U, npk, 0);
     hipLaunchKernelGGL((k_contig_multi<C, U>), dim3(g), dim3(B), 0, s, m, k - 1, o, 0, npk, npk * 4,
                        0, p, g, B);
-}
-
-// k_contig_multi_k: the in-order fold unrolled over KMAX slots (UP: all loads up front)
-template <int KMAX, bool UP, unsigned B = 64> void multik(const MultiIn<float> &mi, int k, float *o,
-                                                          uint64_t npk, const Params &p, hipStream_t s)
-{
-    MultiIn<float> m{};
-    for (int q = 1; q < k; ++q)
-        m.p[q - 1] = mi.p[q];
-    const unsigned g = grid_for(B, npk, 0);
-    hipLaunchKernelGGL((k_contig_multi_k<C, KMAX, UP>), dim3(g), dim3(B), 0, s, m, k - 1, o, 0, npk,
-                       npk * 4, 0, p, g, B);
 }
 
 // the headline kernel's form for comparison: o OP= slot 0 in place (k_contig, U packets per lane)
@@ -146,15 +136,6 @@ int main(int argc, char **argv)
         {"k4_slots4x2_b64_wt", 4, wt<tree<4, 2, 64>>, "k4_slots4x2"}, {"k4_rec4x1_b64_wt", 4, wt<rec<4, 1, 64>>, "k4_slots4x2"},
         {"k8_rec8x1_b64_wt", 8, wt<rec<8, 1, 64>>, "k8_slots8x2"}, {"k16_rec16x1_b64_wt", 16, wt<rec<16, 1, 64>>, "k16_slots16x1"},
         {"k8_multi7_u1_b64_wt", 8, wt<multi<1, 64>>, nullptr}, {"k16_multi15_u1_b64_wt", 16, wt<multi<1, 64>>, nullptr},
-        // the in-order fold unrolled over 8 / 16 slots (k_contig_multi_k), against the loop above
-        {"k4_multi3_u1_b64_wt", 4, wt<multi<1, 64>>, nullptr},
-        {"k4_multik8_b64_wt", 4, wt<multik<8, false>>, "k4_multi3_u1_b64_wt"},
-        {"k4_multik8up_b64_wt", 4, wt<multik<8, true>>, "k4_multi3_u1_b64_wt"},
-        {"k8_multik8_b64_wt", 8, wt<multik<8, false>>, "k8_multi7_u1_b64_wt"},
-        {"k8_multik8up_b64_wt", 8, wt<multik<8, true>>, "k8_multi7_u1_b64_wt"},
-        {"k8_multik16_b64_wt", 8, wt<multik<16, false>>, "k8_multi7_u1_b64_wt"},
-        {"k16_multik16_b64_wt", 16, wt<multik<16, false>>, "k16_multi15_u1_b64_wt"},
-        {"k16_multik16up_b64_wt", 16, wt<multik<16, true>>, "k16_multi15_u1_b64_wt"},
     };
     std::vector<int> same(vs.size(), -1);
     std::vector<float> h_ref(n), h_got(n);
