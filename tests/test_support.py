@@ -201,7 +201,7 @@ def test_collectives_refuse_split_equal(oracle, H):
 
 def test_default_host_floors():
     """the floors MPIX_Redop_is_supported_buffers applies by default: the
-    measured crossover (128 MiB pageable, 16 MiB page-locked
+    measured crossover (128 MiB pageable, 4 MiB page-locked
     per operand), in a fresh process with no MPIX_REDOP_* in the environment"""
     code = ('import sys; sys.path.insert(0, %r)\n'
             'from mpich_amd import redop as R\n'
