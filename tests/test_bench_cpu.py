@@ -180,6 +180,34 @@ def test_gpus_n_launches_n_ranks_itself(n):
     assert d['n_gpus'] == n and d['ranks_seen'] == n and d['launcher'] == 'bench.py', d
 
 
+def _torchrun(nproc, args, env_extra=None):
+    """the driver's N-rank form: python -m torch.distributed.run --nnodes=1
+    --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py ..."""
+    import bench
+    env = {k: v for k, v in os.environ.items()
+           if k not in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_PORT', 'MASTER_ADDR')}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+                           '--nproc-per-node', str(nproc), '--master-addr', '127.0.0.1',
+                           '--master-port', str(bench.free_port()), os.path.join(ROOT, 'bench.py')]
+                          + args, cwd=ROOT, capture_output=True, text=True, timeout=180, env=env)
+
+
+@pytest.mark.parametrize('n', [1, 2])
+def test_dry_run_under_torchrun_is_one_n_rank_line(n):
+    """under the driver's launcher (WORLD_SIZE set by torchrun) every rank runs
+    as given, and only rank 0 prints: one line with n_gpus = N"""
+    import json
+    p = _torchrun(n, ['--gpus', str(n), '--dry-run', '--no-extras', '--no-cpu-baseline'])
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith('{')]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    assert d['n_gpus'] == n, d
+    if n > 1:
+        assert d['ranks_seen'] == n and d['launcher'] == 'external', d
+
+
 def test_gpus_1_dry_run_is_single():
     import json
     p = _bench(['--dry-run'])

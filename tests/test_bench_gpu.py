@@ -3,7 +3,8 @@ its two ranks itself (no torchrun), both on device 0 over the gloo staged
 transport (the rehearsal knobs; RCCL refuses two ranks on one device), runs
 the recursive-halving reduce-scatter value leg with its bit-exact parity gate,
 and rank 0's one line carries n_gpus = 2, the schedule that ran and the
-defaults A/B."""
+defaults A/B; then the same under torch.distributed.run, the driver's own N > 1
+form."""
 import json
 import os
 import subprocess
@@ -35,3 +36,32 @@ def test_bench_gpus_2_self_launched_line():
     for k in ('overlap_on_policy_on', 'overlap_off_policy_on', 'overlap_on_policy_off',
               'overlap_off_policy_off'):
         assert ab[k]['bit_identical_to_shipped_all_ranks'] and ab[k]['ms_per_step'] > 0, ab
+
+
+@pytest.mark.gpu
+def test_bench_gpus_2_under_torchrun_line():
+    """the same line in the driver's own N > 1 form, `python -m
+    torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1
+    --master-port P bench.py --gpus 2 ...`: the ranks run as the launcher gives
+    them (WORLD_SIZE set, no self-launch) and rank 0's one line is the N-rank
+    line"""
+    sys.path.insert(0, ROOT)
+    import bench
+    env = {k: v for k, v in os.environ.items()
+           if k not in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_PORT', 'MASTER_ADDR')}
+    env.update(MPIX_BENCH_SAME_DEVICE='1', MPIX_BENCH_BACKEND='gloo')
+    p = subprocess.run([sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+                        '--nproc-per-node', '2', '--master-addr', '127.0.0.1',
+                        '--master-port', str(bench.free_port()), os.path.join(ROOT, 'bench.py'),
+                        '--gpus', '2', '--steps', '2', '--warmup', '1', '--count', str(1 << 22),
+                        '--rsb-bytes', str(16 << 20), '--no-extras', '--no-cpu-baseline'],
+                       cwd=ROOT, capture_output=True, text=True, timeout=110, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith('{')]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    assert d['n_gpus'] == 2 and d['launcher'] == 'external', d
+    assert d['schedule_ran'] == 'recursive_halving' and d['parity']['bit_exact_all_ranks'], d
+    for k in ('overlap_on_policy_on', 'overlap_off_policy_on', 'overlap_on_policy_off',
+              'overlap_off_policy_off'):
+        assert d['defaults_ab'][k]['bit_identical_to_shipped_all_ranks'], d['defaults_ab']

@@ -6,7 +6,9 @@
 # timed under the pull's name.
 # usage (on the GPU box): P=4 bash tools/gpu_rehearse.sh
 # (RSB=<bytes per rank> STEPS=<k> MODES="normal" for the full-size form: round 5
-# ran P=8 RSB=4294967296 STEPS=2 MODES=normal, the driver's N = 8 shape)
+# ran P=8 RSB=4294967296 STEPS=2 MODES=normal, the driver's N = 8 shape;
+# LAUNCH=torchrun starts the ranks with python -m torch.distributed.run, the
+# driver's launcher, instead of bench.py's own)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -29,8 +31,12 @@ for sec in ('reduce_scatter_block_other', 'allreduce'):
 }
 for mode in $MODES; do
     if [ $mode = fault ]; then export MPIX_COLL_WINDOW_FAULT=1; fi
-    # bench.py starts the P ranks itself (no torchrun): the driver's own form
-    MPIX_BENCH_SAME_DEVICE=1 MPIX_BENCH_BACKEND=gloo timeout -k 10 ${LIMIT:-500} python3 bench.py --gpus $P \
+    # bench.py starts the P ranks itself, or (LAUNCH=torchrun) torch.distributed.run does
+    L="python3"
+    if [ "${LAUNCH:-self}" = torchrun ]; then
+        L="python3 -m torch.distributed.run --nnodes=1 --nproc-per-node $P --master-addr 127.0.0.1 --master-port 29517"
+    fi
+    MPIX_BENCH_SAME_DEVICE=1 MPIX_BENCH_BACKEND=gloo timeout -k 10 ${LIMIT:-500} $L bench.py --gpus $P \
         --steps $STEPS --warmup 1 --ab-reps 1 --count 67108864 --rsb-bytes $RSB $BENCH_ARGS \
         > $O/n${P}_$mode.json 2> $O/n${P}_$mode.err
     rc=$?
