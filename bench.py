@@ -672,6 +672,30 @@ def single_gpu(args, dev):
     print(json.dumps(result, default=str), flush=True)
 
 
+def fill_soft_slots(buf8, enc, seed):
+    """buf8 (a multiple of 16 bytes) as 16-byte slots, each a uniform [-1, 1)
+    double widened exactly to `enc`: 'x87' (64-bit significand with its
+    explicit integer bit, 15-bit exponent, sign; bytes 10-15 zero) or
+    'binary128' (IEEE quad, 112-bit fraction)"""
+    slots = buf8.view(torch.int64).view(-1, 2)
+    d = torch.empty(slots.shape[0], dtype=torch.float64, device=buf8.device)
+    fill_uniform(d, seed)
+    bits = d.view(torch.int64)
+    sign = (bits >> 63) & 1
+    e = (bits >> 52) & 0x7ff
+    f = bits & ((1 << 52) - 1)
+    ex = torch.where(e == 0, torch.zeros_like(e), e - 1023 + 16383)   # +-0 stays zero
+    if enc == 'x87':
+        lo = torch.where(e == 0, torch.zeros_like(f), (f << 11) | torch.tensor(-(1 << 63), device=d.device))
+        hi = (sign << 15) | ex
+    else:
+        lo = (f & 0xf) << 60
+        hi = (sign << 63) | (ex << 48) | (f >> 4)
+    slots[:, 0] = lo
+    slots[:, 1] = hi
+    del d
+
+
 def other_configs(inb, inout, n, stream):
     """BASELINE configs 3 and 5 on the same buffers (kernel-only, HIP events):
     every supported (op, type) pair at 1 GiB per operand (past the 256 MB
@@ -706,10 +730,16 @@ def other_configs(inb, inout, n, stream):
     rows.sort()
     gbs = [r[0] for r in rows]
     # beyond config 3's types: the x87 / binary128 families (software
-    # arithmetic for SUM / PROD, integer compare-and-select for the rest)
+    # arithmetic for SUM / PROD, integer compare-and-select for the rest), on
+    # normal values: every 16-byte slot holds a uniform [-1, 1) double widened
+    # to the type's encoding (small random bytes would make every x87 slot an
+    # unnormal -- integer bit clear -- and time the invalid-operand path)
     soft = []
     for tn in ('MPI_LONG_DOUBLE', 'MPI_REAL16', 'MPI_C_LONG_DOUBLE_COMPLEX', 'MPI_COMPLEX32',
                'MPI_LONG_DOUBLE_INT'):
+        fill_soft_slots(a8, 'x87' if 'LONG_DOUBLE' in tn else 'binary128', 0x5EED0003)
+        fill_soft_slots(b8, 'x87' if 'LONG_DOUBLE' in tn else 'binary128', 0x5EED0004)
+        torch.cuda.synchronize()
         dt = getattr(H, tn)
         ext = redop.datatype_extent(dt)
         m = nbytes // ext
@@ -736,6 +766,8 @@ def other_configs(inb, inout, n, stream):
                                    max_GBs=gbs[-1], min_frac=round(gbs[0] / HBM_PEAK_GBS, 4),
                                    slowest=[dict(GBs=g, type=t, op=o) for g, t, o in rows[:3]]),
         x87_binary128_1GiB=soft,
+        x87_binary128_values='every 16-byte slot a uniform [-1, 1) double widened exactly to the '
+                             'x87 / binary128 encoding (bench.fill_soft_slots)',
         config5_vector=dict(kernel_ms=round(vavg, 4),
                             GBs_algorithmic=round(3 * cnt * 8 / (vavg * 1e-3) / 1e9, 1),
                             GBs_physical=round(2.5 * GIB / (vavg * 1e-3) / 1e9, 1),

@@ -204,6 +204,31 @@ MPIX_SDEV X87 x87_add(const X87 &a, const X87 &b, bool sub)
 MPIX_SDEV X87 x87_mul(const X87 &a, const X87 &b)
 {
     const uint32_t ea = (uint32_t) a.se & 0x7fff, eb = (uint32_t) b.se & 0x7fff;
+    if (ea - 1u < 0x7ffeu && eb - 1u < 0x7ffeu && (a.m >> 63) && (b.m >> 63)) {
+        // both normal: the product of the significands is in [2^126, 2^128),
+        // so its leading bit sits at 126 + top and the rounding cut at a
+        // fixed place -- the general path below with its shifts constant.
+        // A result that would be denormal or overflow takes the general path.
+        const u128 P = (u128) a.m * b.m;
+        const uint64_t hi = (uint64_t) (P >> 64), lo = (uint64_t) P;
+        const int top = (int) (hi >> 63);
+        const uint64_t q0 = top ? hi : (hi << 1) | (lo >> 63);
+        const bool rnd = top ? (lo >> 63) != 0 : ((lo >> 62) & 1) != 0;
+        const bool sticky = top ? (lo << 1) != 0 : (lo << 2) != 0;
+        int64_t E = (int64_t) ea + eb - 16383 + top;
+        if (E >= 1) {
+            uint64_t q = q0;
+            if (rnd && (sticky || (q & 1))) {
+                q += 1;
+                if (q == 0) {           // carried out of the significand
+                    q = 1ull << 63;
+                    E += 1;
+                }
+            }
+            if (E <= 0x7ffe)
+                return x87_make(a, ((a.se ^ b.se) >> 15) & 1, (uint32_t) E, q);
+        }
+    }
     const int ca = x87_class(a.m, ea), cb = x87_class(b.m, eb);
     if (ca == kX87Bad || cb == kX87Bad)
         return x87_indefinite(a);
@@ -332,6 +357,40 @@ MPIX_SDEV Quad quad_add(const Quad &x, const Quad &y, bool sub)
 // x * y: __multf3 (the 226-bit product folded to 128 bits plus a sticky bit)
 MPIX_SDEV Quad quad_mul(const Quad &x, const Quad &y)
 {
+    const uint32_t ex = (uint32_t) (x.hi >> 48) & 0x7fff, ey = (uint32_t) (y.hi >> 48) & 0x7fff;
+    if (ex - 1u < 0x7ffeu && ey - 1u < 0x7ffeu) {
+        // both normal: significands in [2^112, 2^113), the product in
+        // [2^224, 2^226) with its leading bit at 224 + top, so the cut below
+        // the 113-bit result is at a fixed place (the general path's shifts
+        // constant).  A denormal or overflowing result takes the general path.
+        const uint64_t a0 = x.lo, a1 = (x.hi & 0xffffffffffffull) | (1ull << 48);
+        const uint64_t b0 = y.lo, b1 = (y.hi & 0xffffffffffffull) | (1ull << 48);
+        const u128 p00 = (u128) a0 * b0, p01 = (u128) a0 * b1, p10 = (u128) a1 * b0;
+        const u128 p11 = (u128) a1 * b1;
+        const u128 mid = p01 + p10;     // a1, b1 < 2^49: no carry out
+        const u128 lo = p00 + (mid << 64);
+        const u128 hi = p11 + (mid >> 64) + (lo < p00 ? 1 : 0);
+        const int top = (int) (hi >> 97) & 1;
+        const u128 q112 = (hi << 16) | (lo >> 112);         // P >> 112
+        const u128 rest = lo & (((u128) 1 << 112) - 1);
+        const u128 q0 = top ? q112 >> 1 : q112;
+        const bool rnd = top ? (q112 & 1) != 0 : ((rest >> 111) & 1) != 0;
+        const bool sticky = top ? rest != 0 : (rest & (((u128) 1 << 111) - 1)) != 0;
+        int64_t E = (int64_t) ex + ey - 16383 + top;
+        if (E >= 1) {
+            u128 q = q0;
+            if (rnd && (sticky || (q & 1))) {
+                q += 1;
+                if (q >> 113) {         // carried out of the significand
+                    q >>= 1;
+                    E += 1;
+                }
+            }
+            if (E <= 0x7ffe)
+                return quad_make(((x.hi ^ y.hi) >> 63) & 1, (uint32_t) E,
+                                 q & (((u128) 1 << 112) - 1));
+        }
+    }
     const int cx = quad_class(x), cy = quad_class(y);
     if (cx == kX87Nan || cy == kX87Nan)
         return quad_nan(x, cx == kX87Nan, y, cy == kX87Nan, true);

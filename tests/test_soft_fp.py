@@ -212,3 +212,54 @@ def test_complex_prod_special_parts(soft, oracle, which, dt):
             X[:, 10:16] = rng.integers(0, 256, (len(X), 6), dtype=np.uint8)
             X[:, 26:32] = rng.integers(0, 256, (len(X), 6), dtype=np.uint8)
     _check(soft, oracle, which, dt, MPI_PROD, a, b, 32)
+
+
+def _short_x87(rng, n, bits):
+    """normal x87 values whose significand has only `bits` significant bits,
+    so a product of two lands on or next to a rounding tie"""
+    top = rng.integers(0, 1 << (bits - 1), n, dtype=np.uint64)
+    m = (top << np.uint64(64 - bits)) | np.uint64(1 << 63)
+    e = rng.integers(0x3e00, 0x4200, n).astype(np.uint64)
+    e[::5] = rng.integers(1, 0x7fff, len(e[::5])).astype(np.uint64)   # near both ends too
+    s = rng.integers(0, 2, n).astype(np.uint64)
+    out = np.zeros((n, 16), np.uint8)
+    out[:, :8] = m.view(np.uint8).reshape(n, 8)
+    out[:, 8:10] = ((s << 15) | e).astype(np.uint16).view(np.uint8).reshape(n, 2)
+    out[:, 10:] = rng.integers(0, 256, (n, 6), dtype=np.uint8)
+    return out
+
+
+def _short_quad(rng, n, bits):
+    """normal binary128 values with `bits` significant bits (implicit one
+    included): products of two hit the 113-bit rounding ties"""
+    f = bits - 1                # fraction bits kept, from the top of the 112
+    top = rng.integers(0, 1 << min(f, 48), n, dtype=np.uint64)
+    hi48 = top << np.uint64(48 - min(f, 48))
+    lo = np.zeros(n, np.uint64)
+    if f > 48:
+        lo = rng.integers(0, 1 << (f - 48), n, dtype=np.uint64) << np.uint64(64 - (f - 48))
+    e = rng.integers(0x3e00, 0x4200, n).astype(np.uint64)
+    e[::5] = rng.integers(1, 0x7fff, len(e[::5])).astype(np.uint64)
+    s = rng.integers(0, 2, n).astype(np.uint64)
+    out = np.zeros((n, 16), np.uint8)
+    out[:, :8] = lo.view(np.uint8).reshape(n, 8)
+    out[:, 8:] = ((s << np.uint64(63)) | (e << np.uint64(48)) | hi48).view(np.uint8).reshape(n, 8)
+    return out
+
+
+@pytest.mark.parametrize('ba,bb', [(32, 34), (33, 33), (31, 34)])
+def test_x87_prod_rounding_ties(soft, oracle, ba, bb):
+    """products of short significands (ba + bb - 1 or ba + bb bits) round at
+    the 64-bit cut with the sticky bits often all zero: ties to even, and the
+    carry out of an all-ones significand"""
+    rng = np.random.default_rng(0x5EED0860 + ba)
+    n = 200000
+    _check(soft, oracle, 1, LD, MPI_PROD, _short_x87(rng, n, ba), _short_x87(rng, n, bb), 16)
+
+
+@pytest.mark.parametrize('ba,bb', [(57, 58), (56, 58), (60, 55)])
+def test_quad_prod_rounding_ties(soft, oracle, ba, bb):
+    """the same at binary128's 113-bit cut"""
+    rng = np.random.default_rng(0x5EED0870 + ba)
+    n = 200000
+    _check(soft, oracle, 3, REAL16, MPI_PROD, _short_quad(rng, n, ba), _short_quad(rng, n, bb), 16)
