@@ -23,9 +23,11 @@
 //     NaNs the larger fraction, on a tie the first operand (inout) for + and
 //     *, the second for -; quieted; invalid results are the default NaN
 //     (sign 1, quiet bit only).
-// Both: exact result, then one rounding (RNE, gradual underflow).  These
-// combiners are not on any hot path: each element costs ~100 VALU, still
-// far under the HBM time of its 48 bytes at 8 TB/s per CU share.
+// Both: exact result, then one rounding (RNE, gradual underflow).  Products
+// of normal operands, and scalar sums of normal operands that do not nearly
+// cancel, take a fast path that rounds at a fixed cut (the general path's
+// shifts made constant); anything else -- specials, denormal or overflowing
+// results, cancellation -- takes the general path.
 #pragma once
 
 #include <stdint.h>
@@ -161,9 +163,64 @@ MPIX_SDEV X87 x87_from_round(const X87 &pad, bool s, u128 S, int64_t E0)
 }
 
 // a + b (sub: a - b), as fldt a; fldt b; faddp (fsubp); the result keeps a's padding
+// Round S (leading bit at p = 125..127, the exact sum's scale as round_exact's)
+// to `bits` bits at the fixed cut sh = p - (bits - 1), RNE: the normal-result
+// case of round_exact without its normalisation and underflow branches.
+// Returns false (caller takes the general path) if E0 + p - 126 is not a normal
+// exponent before or after the rounding carry.
+MPIX_SDEV bool round_top(u128 S, int64_t E0, int bits, u128 *m, int64_t *e)
+{
+    const int p = (S >> 127) ? 127 : ((S >> 126) ? 126 : 125);
+    int64_t E = E0 + p - 126;
+    if (E < 1)
+        return false;
+    const int sh = p - (bits - 1);
+    u128 q = S >> sh;
+    const u128 rest = S & (((u128) 1 << sh) - 1);
+    const u128 half = (u128) 1 << (sh - 1);
+    if (rest > half || (rest == half && (q & 1)))
+        q += 1;
+    if (q >> bits) {
+        q >>= 1;
+        E += 1;
+    }
+    if (E > 0x7ffe)
+        return false;
+    *m = q;
+    *e = E;
+    return true;
+}
+
+// FAST: the normal-operand path first (kept out of the complex combiners, whose
+// two or more adds per unit then ran slower: more registers, fewer waves)
+template <bool FAST = true>
 MPIX_SDEV X87 x87_add(const X87 &a, const X87 &b, bool sub)
 {
     const uint32_t ea = (uint32_t) a.se & 0x7fff, eb = (uint32_t) b.se & 0x7fff;
+    if (FAST && ea - 1u < 0x7ffeu && eb - 1u < 0x7ffeu && (a.m >> 63) && (b.m >> 63)) {
+        // both normal; unless the operands nearly cancel (opposite effective
+        // signs, exponents within 1), the exact sum's leading bit is at 125..127
+        // and the rounding cut sits at one of three fixed places
+        const bool swap = ea < eb || (ea == eb && a.m < b.m);
+        const bool sa0 = (a.se >> 15) & 1, sb0 = ((b.se >> 15) & 1) ^ (sub ? 1 : 0);
+        const bool sa = swap ? sb0 : sa0, sb = swap ? sa0 : sb0;
+        const uint64_t ma = swap ? b.m : a.m, mb = swap ? a.m : b.m;
+        const int64_t xa = swap ? eb : ea, d = swap ? (int64_t) eb - ea : (int64_t) ea - eb;
+        if (sa == sb || d >= 2) {
+            const u128 A = (u128) ma << 63;
+            u128 B = 1;
+            if (d < 128) {
+                const u128 full = (u128) mb << 63;
+                B = full >> (int) d;
+                if (d > 0 && (full & (((u128) 1 << (int) d) - 1)))
+                    B |= 1;
+            }
+            u128 m;
+            int64_t e;
+            if (round_top(sa == sb ? A + B : A - B, xa, 64, &m, &e))
+                return x87_make(a, sa, (uint32_t) e, (uint64_t) m);
+        }
+    }
     const int ca = x87_class(a.m, ea), cb = x87_class(b.m, eb);
     if (ca == kX87Bad || cb == kX87Bad)
         return x87_indefinite(a);
@@ -314,8 +371,36 @@ MPIX_SDEV Quad quad_from_round(bool s, u128 S, int64_t E0)
 }
 
 // x + y (sub: x - y): __addtf3 / __subtf3
+template <bool FAST = true>
 MPIX_SDEV Quad quad_add(const Quad &x, const Quad &y, bool sub)
 {
+    const uint32_t ex = (uint32_t) (x.hi >> 48) & 0x7fff, ey = (uint32_t) (y.hi >> 48) & 0x7fff;
+    if (FAST && ex - 1u < 0x7ffeu && ey - 1u < 0x7ffeu) {
+        // both normal: as x87_add's fast path (magnitudes ordered by the
+        // encoding without its sign bit)
+        const uint64_t hx = x.hi & ~(1ull << 63), hy = y.hi & ~(1ull << 63);
+        const bool swap = hx < hy || (hx == hy && x.lo < y.lo);
+        const bool sx = x.hi >> 63, sy = (bool) (y.hi >> 63) ^ sub;
+        const bool sa = swap ? sy : sx, sb = swap ? sx : sy;
+        const uint64_t bh = swap ? hy : hx, bl = swap ? y.lo : x.lo;
+        const uint64_t th = swap ? hx : hy, tl = swap ? x.lo : y.lo;
+        const int64_t xa = (int64_t) (bh >> 48), d = xa - (int64_t) (th >> 48);
+        if (sa == sb || d >= 2) {
+            const uint64_t lead = 1ull << 48, f48 = 0xffffffffffffull;
+            const u128 A = ((((u128) ((bh & f48) | lead)) << 64) | bl) << 14;
+            u128 B = 1;
+            if (d < 128) {
+                const u128 full = ((((u128) ((th & f48) | lead)) << 64) | tl) << 14;
+                B = full >> (int) d;
+                if (d > 0 && (full & (((u128) 1 << (int) d) - 1)))
+                    B |= 1;
+            }
+            u128 m;
+            int64_t e;
+            if (round_top(sa == sb ? A + B : A - B, xa, 113, &m, &e))
+                return quad_make(sa, (uint32_t) e, m & (((u128) 1 << 112) - 1));
+        }
+    }
     const int cx = quad_class(x), cy = quad_class(y);
     if (cx == kX87Nan || cy == kX87Nan)
         return quad_nan(x, cx == kX87Nan, y, cy == kX87Nan, !sub);
@@ -453,8 +538,8 @@ struct QuadCSum {
     static MPIX_SDEV QuadC apply(QuadC a, QuadC b, const Params &)
     {
         QuadC r;
-        r.re = quad_add(a.re, b.re, false);
-        r.im = quad_add(a.im, b.im, false);
+        r.re = quad_add<false>(a.re, b.re, false);
+        r.im = quad_add<false>(a.im, b.im, false);
         return r;
     }
 };
@@ -463,8 +548,8 @@ struct QuadCProd {
     static MPIX_SDEV QuadC apply(QuadC c, QuadC b, const Params &)
     {
         QuadC r;
-        r.re = quad_add(quad_mul(c.re, b.re), quad_mul(c.im, b.im), true);
-        r.im = quad_add(quad_mul(c.im, b.re), quad_mul(c.re, b.im), false);
+        r.re = quad_add<false>(quad_mul(c.re, b.re), quad_mul(c.im, b.im), true);
+        r.im = quad_add<false>(quad_mul(c.im, b.re), quad_mul(c.re, b.im), false);
         return r;
     }
 };
@@ -498,7 +583,7 @@ struct X87CProd {
     {
         X87 a = x.re, b = x.im, c = y.re, d = y.im;
         const X87 ac = x87_mul(a, c), bd = x87_mul(b, d), ad = x87_mul(a, d), bc = x87_mul(b, c);
-        X87 re = x87_add(ac, bd, true), im = x87_add(ad, bc, false);
+        X87 re = x87_add<false>(ac, bd, true), im = x87_add<false>(ad, bc, false);
         if (x87_isnan(re) && x87_isnan(im)) {
             bool recalc = false;
             if (x87_isinf(a) || x87_isinf(b)) {
@@ -526,8 +611,8 @@ struct X87CProd {
                 X87 inf;
                 inf.m = 1ull << 63;
                 inf.se = 0x7fff;
-                re = x87_mul(inf, x87_add(x87_mul(a, c), x87_mul(b, d), true));
-                im = x87_mul(inf, x87_add(x87_mul(a, d), x87_mul(b, c), false));
+                re = x87_mul(inf, x87_add<false>(x87_mul(a, c), x87_mul(b, d), true));
+                im = x87_mul(inf, x87_add<false>(x87_mul(a, d), x87_mul(b, c), false));
             }
         }
         X87C r;     // stored with fstpt: each part keeps inout's padding
@@ -541,8 +626,8 @@ struct X87CSum {
     static MPIX_SDEV X87C apply(X87C a, X87C b, const Params &)
     {
         X87C r;
-        r.re = x87_add(a.re, b.re, false);
-        r.im = x87_add(a.im, b.im, false);
+        r.re = x87_add<false>(a.re, b.re, false);
+        r.im = x87_add<false>(a.im, b.im, false);
         return r;
     }
 };

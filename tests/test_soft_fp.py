@@ -263,3 +263,30 @@ def test_quad_prod_rounding_ties(soft, oracle, ba, bb):
     rng = np.random.default_rng(0x5EED0870 + ba)
     n = 200000
     _check(soft, oracle, 3, REAL16, MPI_PROD, _short_quad(rng, n, ba), _short_quad(rng, n, bb), 16)
+
+
+@pytest.mark.parametrize('which,dt,ext_bits,spread', [(0, LD, 40, 30), (2, REAL16, 80, 40)])
+def test_sum_rounding_ties(soft, oracle, which, dt, ext_bits, spread):
+    """sums of short significands whose exponents differ by 0..spread: the
+    exact sum lands on rounding ties (RNE), carries into a new binade and
+    cancels, on both sides of every fixed cut of the normal-operand path"""
+    rng = np.random.default_rng(0x5EED0880 + which)
+    n = 300000
+    make = _short_x87 if which == 0 else _short_quad
+    a = make(rng, n, ext_bits)
+    b = make(rng, n, ext_bits)
+    if which == 0:
+        ea = a[:, 8:10].copy().view(np.uint16).reshape(-1) & 0x7fff
+        k = rng.integers(0, spread + 1, n).astype(np.uint16)
+        eb = np.clip(ea.astype(np.int64) + k - spread // 2, 1, 0x7ffe).astype(np.uint16)
+        sb = b[:, 8:10].copy().view(np.uint16).reshape(-1) & 0x8000
+        b[:, 8:10] = (sb | eb).view(np.uint8).reshape(n, 2)
+    else:
+        ha = a[:, 8:].copy().view(np.uint64).reshape(-1)
+        hb = b[:, 8:].copy().view(np.uint64).reshape(-1)
+        ea = ((ha >> np.uint64(48)) & np.uint64(0x7fff)).astype(np.int64)
+        k = rng.integers(0, spread + 1, n)
+        eb = np.clip(ea + k - spread // 2, 1, 0x7ffe).astype(np.uint64)
+        hb = (hb & ~np.uint64(0x7fff << 48)) | (eb << np.uint64(48))
+        b[:, 8:] = hb.view(np.uint8).reshape(n, 8)
+    _check(soft, oracle, which, dt, MPI_SUM, a, b, 16)
