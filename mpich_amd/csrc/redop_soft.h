@@ -23,11 +23,11 @@
 //     NaNs the larger fraction, on a tie the first operand (inout) for + and
 //     *, the second for -; quieted; invalid results are the default NaN
 //     (sign 1, quiet bit only).
-// Both: exact result, then one rounding (RNE, gradual underflow).  Products
-// of normal operands, and scalar sums of normal operands that do not nearly
-// cancel, take a fast path that rounds at a fixed cut (the general path's
-// shifts made constant); anything else -- specials, denormal or overflowing
-// results, cancellation -- takes the general path.
+// Both: exact result, then one rounding (RNE, gradual underflow).  Sums and
+// products of two normal operands take a fast path that rounds at a fixed cut
+// (the general path's shifts made constant; a near-cancelling sum is exact and
+// only normalised); anything else -- specials, denormal or overflowing
+// results, exact cancellation -- takes the general path.
 #pragma once
 
 #include <stdint.h>
@@ -162,14 +162,28 @@ MPIX_SDEV X87 x87_from_round(const X87 &pad, bool s, u128 S, int64_t E0)
     return x87_make(pad, s, (uint32_t) e, (uint64_t) m);
 }
 
-// a + b (sub: a - b), as fldt a; fldt b; faddp (fsubp); the result keeps a's padding
-// Round S (leading bit at p = 125..127, the exact sum's scale as round_exact's)
-// to `bits` bits at the fixed cut sh = p - (bits - 1), RNE: the normal-result
-// case of round_exact without its normalisation and underflow branches.
-// Returns false (caller takes the general path) if E0 + p - 126 is not a normal
-// exponent before or after the rounding carry.
+// The sum of two normal operands, aligned as the add paths below align them
+// (the larger's leading bit at 126, the smaller's shifted right by the exponent
+// difference d with a sticky bit), rounded to `bits` bits: round_exact's
+// normal-result case without its underflow branches.  S >= 2^125 unless the
+// operands nearly cancel (opposite signs, d <= 1); then no bit was shifted out
+// and S has at most `bits` significant bits, so it is exact and only
+// normalised.  Returns false (the caller takes the general path) for a zero
+// sum or an exponent E0 + p - 126 that is not normal before or after rounding.
 MPIX_SDEV bool round_top(u128 S, int64_t E0, int bits, u128 *m, int64_t *e)
 {
+    if (!(S >> 125)) {
+        if (S == 0)
+            return false;
+        const int p = 127 - clz128(S);
+        const int64_t E = E0 + p - 126;
+        if (E < 1)
+            return false;
+        const int sh = p - (bits - 1);
+        *m = sh >= 0 ? S >> sh : S << -sh;
+        *e = E;
+        return true;
+    }
     const int p = (S >> 127) ? 127 : ((S >> 126) ? 126 : 125);
     int64_t E = E0 + p - 126;
     if (E < 1)
@@ -191,35 +205,31 @@ MPIX_SDEV bool round_top(u128 S, int64_t E0, int bits, u128 *m, int64_t *e)
     return true;
 }
 
-// FAST: the normal-operand path first (kept out of the complex combiners, whose
-// two or more adds per unit then ran slower: more registers, fewer waves)
+// a + b (sub: a - b), as fldt a; fldt b; faddp (fsubp); the result keeps a's
+// padding.  FAST: both operands normal -> round_top, the rest the general path.
 template <bool FAST = true>
 MPIX_SDEV X87 x87_add(const X87 &a, const X87 &b, bool sub)
 {
     const uint32_t ea = (uint32_t) a.se & 0x7fff, eb = (uint32_t) b.se & 0x7fff;
     if (FAST && ea - 1u < 0x7ffeu && eb - 1u < 0x7ffeu && (a.m >> 63) && (b.m >> 63)) {
-        // both normal; unless the operands nearly cancel (opposite effective
-        // signs, exponents within 1), the exact sum's leading bit is at 125..127
-        // and the rounding cut sits at one of three fixed places
+        // both normal: order by magnitude, align, round_top
         const bool swap = ea < eb || (ea == eb && a.m < b.m);
         const bool sa0 = (a.se >> 15) & 1, sb0 = ((b.se >> 15) & 1) ^ (sub ? 1 : 0);
         const bool sa = swap ? sb0 : sa0, sb = swap ? sa0 : sb0;
         const uint64_t ma = swap ? b.m : a.m, mb = swap ? a.m : b.m;
         const int64_t xa = swap ? eb : ea, d = swap ? (int64_t) eb - ea : (int64_t) ea - eb;
-        if (sa == sb || d >= 2) {
-            const u128 A = (u128) ma << 63;
-            u128 B = 1;
-            if (d < 128) {
-                const u128 full = (u128) mb << 63;
-                B = full >> (int) d;
-                if (d > 0 && (full & (((u128) 1 << (int) d) - 1)))
-                    B |= 1;
-            }
-            u128 m;
-            int64_t e;
-            if (round_top(sa == sb ? A + B : A - B, xa, 64, &m, &e))
-                return x87_make(a, sa, (uint32_t) e, (uint64_t) m);
+        const u128 A = (u128) ma << 63;
+        u128 B = 1;
+        if (d < 128) {
+            const u128 full = (u128) mb << 63;
+            B = full >> (int) d;
+            if (d > 0 && (full & (((u128) 1 << (int) d) - 1)))
+                B |= 1;
         }
+        u128 m;
+        int64_t e;
+        if (round_top(sa == sb ? A + B : A - B, xa, 64, &m, &e))
+            return x87_make(a, sa, (uint32_t) e, (uint64_t) m);
     }
     const int ca = x87_class(a.m, ea), cb = x87_class(b.m, eb);
     if (ca == kX87Bad || cb == kX87Bad)
@@ -385,21 +395,19 @@ MPIX_SDEV Quad quad_add(const Quad &x, const Quad &y, bool sub)
         const uint64_t bh = swap ? hy : hx, bl = swap ? y.lo : x.lo;
         const uint64_t th = swap ? hx : hy, tl = swap ? x.lo : y.lo;
         const int64_t xa = (int64_t) (bh >> 48), d = xa - (int64_t) (th >> 48);
-        if (sa == sb || d >= 2) {
-            const uint64_t lead = 1ull << 48, f48 = 0xffffffffffffull;
-            const u128 A = ((((u128) ((bh & f48) | lead)) << 64) | bl) << 14;
-            u128 B = 1;
-            if (d < 128) {
-                const u128 full = ((((u128) ((th & f48) | lead)) << 64) | tl) << 14;
-                B = full >> (int) d;
-                if (d > 0 && (full & (((u128) 1 << (int) d) - 1)))
-                    B |= 1;
-            }
-            u128 m;
-            int64_t e;
-            if (round_top(sa == sb ? A + B : A - B, xa, 113, &m, &e))
-                return quad_make(sa, (uint32_t) e, m & (((u128) 1 << 112) - 1));
+        const uint64_t lead = 1ull << 48, f48 = 0xffffffffffffull;
+        const u128 A = ((((u128) ((bh & f48) | lead)) << 64) | bl) << 14;
+        u128 B = 1;
+        if (d < 128) {
+            const u128 full = ((((u128) ((th & f48) | lead)) << 64) | tl) << 14;
+            B = full >> (int) d;
+            if (d > 0 && (full & (((u128) 1 << (int) d) - 1)))
+                B |= 1;
         }
+        u128 m;
+        int64_t e;
+        if (round_top(sa == sb ? A + B : A - B, xa, 113, &m, &e))
+            return quad_make(sa, (uint32_t) e, m & (((u128) 1 << 112) - 1));
     }
     const int cx = quad_class(x), cy = quad_class(y);
     if (cx == kX87Nan || cy == kX87Nan)
@@ -538,8 +546,8 @@ struct QuadCSum {
     static MPIX_SDEV QuadC apply(QuadC a, QuadC b, const Params &)
     {
         QuadC r;
-        r.re = quad_add<false>(a.re, b.re, false);
-        r.im = quad_add<false>(a.im, b.im, false);
+        r.re = quad_add(a.re, b.re, false);
+        r.im = quad_add(a.im, b.im, false);
         return r;
     }
 };
@@ -548,8 +556,8 @@ struct QuadCProd {
     static MPIX_SDEV QuadC apply(QuadC c, QuadC b, const Params &)
     {
         QuadC r;
-        r.re = quad_add<false>(quad_mul(c.re, b.re), quad_mul(c.im, b.im), true);
-        r.im = quad_add<false>(quad_mul(c.im, b.re), quad_mul(c.re, b.im), false);
+        r.re = quad_add(quad_mul(c.re, b.re), quad_mul(c.im, b.im), true);
+        r.im = quad_add(quad_mul(c.im, b.re), quad_mul(c.re, b.im), false);
         return r;
     }
 };
@@ -583,7 +591,7 @@ struct X87CProd {
     {
         X87 a = x.re, b = x.im, c = y.re, d = y.im;
         const X87 ac = x87_mul(a, c), bd = x87_mul(b, d), ad = x87_mul(a, d), bc = x87_mul(b, c);
-        X87 re = x87_add<false>(ac, bd, true), im = x87_add<false>(ad, bc, false);
+        X87 re = x87_add(ac, bd, true), im = x87_add(ad, bc, false);
         if (x87_isnan(re) && x87_isnan(im)) {
             bool recalc = false;
             if (x87_isinf(a) || x87_isinf(b)) {
@@ -611,8 +619,8 @@ struct X87CProd {
                 X87 inf;
                 inf.m = 1ull << 63;
                 inf.se = 0x7fff;
-                re = x87_mul(inf, x87_add<false>(x87_mul(a, c), x87_mul(b, d), true));
-                im = x87_mul(inf, x87_add<false>(x87_mul(a, d), x87_mul(b, c), false));
+                re = x87_mul(inf, x87_add(x87_mul(a, c), x87_mul(b, d), true));
+                im = x87_mul(inf, x87_add(x87_mul(a, d), x87_mul(b, c), false));
             }
         }
         X87C r;     // stored with fstpt: each part keeps inout's padding
@@ -626,8 +634,8 @@ struct X87CSum {
     static MPIX_SDEV X87C apply(X87C a, X87C b, const Params &)
     {
         X87C r;
-        r.re = x87_add<false>(a.re, b.re, false);
-        r.im = x87_add<false>(a.im, b.im, false);
+        r.re = x87_add(a.re, b.re, false);
+        r.im = x87_add(a.im, b.im, false);
         return r;
     }
 };
