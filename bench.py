@@ -672,6 +672,88 @@ def single_gpu(args, dev):
     print(json.dumps(result, default=str), flush=True)
 
 
+# ---------------------------------------------------------------- config 3 inputs
+# SURVEY §8(d) C3 on the device (torch's seeded Philox generator): ints
+# uniform over the full range (30 % zero elements, the logical ops' false),
+# floats uniform [-1, 1) plus 1 % specials (+-0, +-Inf, NaN) and fp32
+# subnormals, bf16 with ties-away cases, Fortran logicals .TRUE./.FALSE. and
+# other values, pairs with values in 0..15 (ties) and NaNs, random pair
+# padding.  tests/test_c3_full.py draws its parity operands from the same
+# generator; the config-3 throughput rows below time on them.
+C3_FDT = {2: torch.float16, 4: torch.float32, 8: torch.float64}
+C3_IDT = {1: torch.int8, 2: torch.int16, 4: torch.int32, 8: torch.int64}
+C3_TYPES = (('MPI_INT8_T', 'int', 1), ('MPI_INT16_T', 'int', 2), ('MPI_INT32_T', 'int', 4),
+            ('MPI_INT64_T', 'int', 8), ('MPI_INTEGER16', 'int', 16), ('MPIX_C_FLOAT16', 'fp', 2),
+            ('MPIX_BFLOAT16', 'bf16', 2), ('MPI_FLOAT', 'fp', 4), ('MPI_DOUBLE', 'fp', 8),
+            ('MPI_COMPLEX4', 'cplx', 2), ('MPI_C_FLOAT_COMPLEX', 'cplx', 4),
+            ('MPI_C_DOUBLE_COMPLEX', 'cplx', 8), ('MPI_C_BOOL', 'int', 1), ('MPI_LOGICAL', 'flog', 4),
+            ('MPI_BYTE', 'int', 1), ('MPI_2INT', ('pair', '<i4', '<i4', 8, 4), None),
+            ('MPI_FLOAT_INT', ('pair', '<f4', '<i4', 8, 4), None),
+            ('MPI_DOUBLE_INT', ('pair', '<f8', '<i4', 16, 8), None),
+            ('MPI_SHORT_INT', ('pair', '<i2', '<i4', 8, 4), None))
+
+
+def _c3_bytes(g, nbytes):
+    return torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device='cuda', generator=g)
+
+
+def _c3_u(g, n, dt=torch.float32):
+    return torch.rand(n, dtype=dt, device='cuda', generator=g)
+
+
+def _c3_fp(g, n, size):
+    x = (_c3_u(g, n, torch.float64 if size == 8 else torch.float32) * 2 - 1).to(C3_FDT[size])
+    sp = torch.tensor([0.0, -0.0, float('inf'), float('-inf'), float('nan')], dtype=C3_FDT[size],
+                      device='cuda')
+    k = _c3_u(g, n) < 0.01
+    x[k] = sp[torch.randint(0, 5, (int(k.sum()),), device='cuda', generator=g)]
+    if size == 4:       # subnormals must not be flushed
+        d = _c3_u(g, n) < 0.003
+        x[d] = ((_c3_u(g, int(d.sum())) * 2 - 1) * 1e-39).to(torch.float32)
+    return x.view(torch.uint8)
+
+
+def c3_operand(g, kind, size, n):
+    """one config-3 operand of n elements of `kind` as a device uint8 tensor"""
+    if kind == 'int':
+        a = _c3_bytes(g, n * size).view(n, size)
+        a[_c3_u(g, n) < 0.3] = 0                # logical-false elements
+        return a.reshape(-1)
+    if kind == 'flog':
+        vals = torch.tensor([0, 1, -1, 5, 0], dtype=torch.int64, device='cuda')
+        v = vals[torch.randint(0, 5, (n,), device='cuda', generator=g)]
+        if size <= 8:
+            return v.to(C3_IDT[size]).view(torch.uint8)
+        return torch.stack([v, torch.where(v < 0, -1, 0)], 1).view(torch.uint8).reshape(-1)
+    if kind == 'fp':
+        return _c3_fp(g, n, size)
+    if kind == 'cplx':
+        return _c3_fp(g, 2 * n, size)
+    if kind == 'bf16':
+        f = _c3_u(g, n) * 8 - 4
+        k = _c3_u(g, n) < 0.01
+        sp = torch.tensor([float('inf'), float('-inf'), 0.0, -0.0], device='cuda')
+        f[k] = sp[torch.randint(0, 4, (int(k.sum()),), device='cuda', generator=g)]
+        b = (f.view(torch.int32) >> 16).to(torch.int32) & 0xffff
+        b ^= torch.randint(0, 2, (n,), dtype=torch.int32, device='cuda', generator=g)
+        nan = ((b & 0x7f80) == 0x7f80) & ((b & 0x7f) != 0)
+        b[nan] = 0x3f80
+        return b.to(torch.int16).view(torch.uint8)
+    vdt, ldt, ext, loff = kind[1:]
+    buf = _c3_bytes(g, n * ext).view(n, ext)    # random padding
+    vs, ls = np.dtype(vdt).itemsize, np.dtype(ldt).itemsize
+    v = torch.randint(0, 16, (n,), device='cuda', generator=g)
+    if vdt.startswith('<f'):
+        v = v.to(C3_FDT[vs])
+        v[_c3_u(g, n) < 0.02] = float('nan')
+    else:
+        v = v.to(C3_IDT[vs])
+    lv = torch.randint(-1000, 1000, (n,), device='cuda', generator=g).to(C3_IDT[ls])
+    buf[:, :vs] = v.view(torch.uint8).view(n, vs)
+    buf[:, loff:loff + ls] = lv.view(torch.uint8).view(n, ls)
+    return buf.reshape(-1)
+
+
 def fill_soft_slots(buf8, enc, seed):
     """buf8 (a multiple of 16 bytes) as 16-byte slots, each a uniform [-1, 1)
     double widened exactly to `enc`: 'x87' (64-bit significand with its
@@ -705,17 +787,20 @@ def other_configs(inb, inout, n, stream):
     nbytes = 4 * n
     a8 = inout.view(torch.uint8)
     b8 = inb.view(torch.uint8)
-    a8.view(torch.int8).random_(0, 3)      # small values: no NaN/Inf, no data-dependent paths
-    b8.view(torch.int8).random_(0, 3)
-    torch.cuda.synchronize()
     rows = []
-    for tn in ('MPI_INT8_T', 'MPI_INT16_T', 'MPI_INT32_T', 'MPI_INT64_T', 'MPI_INTEGER16',
-               'MPIX_C_FLOAT16', 'MPIX_BFLOAT16', 'MPI_FLOAT', 'MPI_DOUBLE', 'MPI_COMPLEX4',
-               'MPI_C_FLOAT_COMPLEX', 'MPI_C_DOUBLE_COMPLEX', 'MPI_C_BOOL', 'MPI_LOGICAL', 'MPI_BYTE',
-               'MPI_2INT', 'MPI_FLOAT_INT', 'MPI_DOUBLE_INT', 'MPI_SHORT_INT'):
+    g = torch.Generator(device='cuda')
+    for tn, kind, size in C3_TYPES:
         dt = getattr(H, tn)
         ext = redop.datatype_extent(dt)
         m = nbytes // ext
+        # the C3 distributions (c3_operand), drawn per type; the timed calls
+        # then fold into inout again and again, which moves the values but
+        # not the kernel's work (no data-dependent paths in these combiners)
+        g.manual_seed((0x5EED0003 * 31 + dt) & 0xffffffff)
+        a8[:m * ext].copy_(c3_operand(g, kind, size, m))
+        b8[:m * ext].copy_(c3_operand(g, kind, size, m))
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
         for on, op in H.OPS.items():
             if op in (H.MPI_REPLACE, H.MPI_NO_OP) or not redop.is_supported(op, dt):
                 continue
@@ -763,6 +848,7 @@ def other_configs(inb, inout, n, stream):
                                                       stream)), 10, stream)
     return dict(
         config3_per_pair_1GiB=dict(pairs=len(rows), min_GBs=gbs[0], median_GBs=gbs[len(gbs) // 2],
+                                   values='SURVEY 8(d) C3 distributions per type (bench.c3_operand)',
                                    max_GBs=gbs[-1], min_frac=round(gbs[0] / HBM_PEAK_GBS, 4),
                                    slowest=[dict(GBs=g, type=t, op=o) for g, t, o in rows[:3]]),
         x87_binary128_1GiB=soft,

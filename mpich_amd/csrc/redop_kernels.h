@@ -240,15 +240,15 @@ contig_body(const typename C::unit *__restrict__ in, typename C::unit *__restric
                 for (int u = 0; u < U; ++u)
                     r[u] = combine16_fast<C>(a[u], b[u], prm, need);
                 if (__builtin_expect(need, 0)) {
-                    // the rare full form: one packet at a time from memory
-                    // again (inout is not written yet), so the tile's
-                    // registers are dead here and the slow path cannot push
-                    // the kernel past the 128-VGPR cap into scratch
-#pragma unroll 1
-                    for (int u = 0; u < U; ++u) {
-                        const uint64_t k = i + u * nt;
-                        st(vio + k, combine16<C>(ld16<NTL>(vio + k), ldin(k), prm));
-                    }
+                    // the full form on the packets already in registers (one
+                    // packet per lane since round 5, so they fit): with NaNs
+                    // in the data (config 3's 1 % specials, absorbing under
+                    // repeated folds) many waves come here, and re-reading the
+                    // packets from memory and calling the recovery cost
+                    // 20 % of the rate (profiles/r05_c3_inputs.json)
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+                        st(vio + i + u * nt, combine16<C>(a[u], b[u], prm));
                 } else {
 #pragma unroll
                     for (int u = 0; u < U; ++u)

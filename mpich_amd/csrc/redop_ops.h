@@ -266,7 +266,7 @@ template <typename R> struct CProdAnnexG {
         need |= __builtin_isnan(z.re) & __builtin_isnan(z.im);
         return z;
     }
-    static __device__ __noinline__ unit recover(R a, R b, R c, R d, R ac, R bd, R ad, R bc, unit z)
+    static MPIX_DEV unit recover(R a, R b, R c, R d, R ac, R bd, R ad, R bc, unit z)
     {
         bool recalc = false;
         const R one = 1, zero = 0;

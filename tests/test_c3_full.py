@@ -3,15 +3,15 @@ path (the 170 cases of test_gpu_parity's sweep) on 256 MiB per operand, the
 HIP result bit for bit against the oracle (MPI_SUM/PROD on fp: a NaN need only
 be a NaN, arithmetic NaN payloads are unpinned -- test_gpu_parity's rule).
 
-At that size the operands are drawn on the GPU (torch's seeded Philox
-generator, the same value distributions as test_gpu_parity's numpy
-generators: logical zeros, fp specials and subnormals, bf16 ties-away cases,
-pair ties and NaNs, random pair padding), the oracle runs on 8 host threads
+At that size the operands are drawn on the GPU (bench.c3_operand: torch's
+seeded Philox generator, the same value distributions as test_gpu_parity's
+numpy generators: logical zeros, fp specials and subnormals, bf16 ties-away
+cases, pair ties and NaNs, random pair padding; the bench's config-3 rows time
+on the same generator), the oracle runs on 8 host threads
 and the comparison runs on the device, so the 170 cases fit the GPU suite.
 MPIX_C3_BYTES overrides the per-operand size."""
 import os
 
-import numpy as np
 import pytest
 import torch
 
@@ -38,69 +38,8 @@ def H():
     return handles
 
 
-FDT = {2: torch.float16, 4: torch.float32, 8: torch.float64}
-IDT = {1: torch.int8, 2: torch.int16, 4: torch.int32, 8: torch.int64}
-
-
-def _bytes(g, nbytes):
-    return torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device='cuda', generator=g)
-
-
-def _u(g, n, dt=torch.float32):
-    return torch.rand(n, dtype=dt, device='cuda', generator=g)
-
-
-def _fp(g, n, size):
-    x = (_u(g, n, torch.float64 if size == 8 else torch.float32) * 2 - 1).to(FDT[size])
-    sp = torch.tensor([0.0, -0.0, float('inf'), float('-inf'), float('nan')], dtype=FDT[size],
-                      device='cuda')
-    k = _u(g, n) < 0.01
-    x[k] = sp[torch.randint(0, 5, (int(k.sum()),), device='cuda', generator=g)]
-    if size == 4:       # subnormals must not be flushed
-        d = _u(g, n) < 0.003
-        x[d] = ((_u(g, int(d.sum())) * 2 - 1) * 1e-39).to(torch.float32)
-    return x.view(torch.uint8)
-
-
-def operand(g, kind, size, n):
-    """one operand of n elements as a device uint8 tensor"""
-    if kind == 'int':
-        a = _bytes(g, n * size).view(n, size)
-        a[_u(g, n) < 0.3] = 0                   # logical-false elements
-        return a.reshape(-1)
-    if kind == 'flog':
-        vals = torch.tensor([0, 1, -1, 5, 0], dtype=torch.int64, device='cuda')
-        v = vals[torch.randint(0, 5, (n,), device='cuda', generator=g)]
-        if size <= 8:
-            return v.to(IDT[size]).view(torch.uint8)
-        return torch.stack([v, torch.where(v < 0, -1, 0)], 1).view(torch.uint8).reshape(-1)
-    if kind == 'fp':
-        return _fp(g, n, size)
-    if kind == 'cplx':
-        return _fp(g, 2 * n, size)
-    if kind == 'bf16':
-        f = _u(g, n) * 8 - 4
-        k = _u(g, n) < 0.01
-        sp = torch.tensor([float('inf'), float('-inf'), 0.0, -0.0], device='cuda')
-        f[k] = sp[torch.randint(0, 4, (int(k.sum()),), device='cuda', generator=g)]
-        b = (f.view(torch.int32) >> 16).to(torch.int32) & 0xffff
-        b ^= torch.randint(0, 2, (n,), dtype=torch.int32, device='cuda', generator=g)
-        nan = ((b & 0x7f80) == 0x7f80) & ((b & 0x7f) != 0)
-        b[nan] = 0x3f80
-        return b.to(torch.int16).view(torch.uint8)
-    vdt, ldt, ext, loff = kind[1:]
-    buf = _bytes(g, n * ext).view(n, ext)       # random padding
-    vs, ls = np.dtype(vdt).itemsize, np.dtype(ldt).itemsize
-    v = torch.randint(0, 16, (n,), device='cuda', generator=g)
-    if vdt.startswith('<f'):
-        v = v.to(FDT[vs])
-        v[_u(g, n) < 0.02] = float('nan')
-    else:
-        v = v.to(IDT[vs])
-    lv = torch.randint(-1000, 1000, (n,), device='cuda', generator=g).to(IDT[ls])
-    buf[:, :vs] = v.view(torch.uint8).view(n, vs)
-    buf[:, loff:loff + ls] = lv.view(torch.uint8).view(n, ls)
-    return buf.reshape(-1)
+from bench import C3_FDT as FDT  # noqa: E402
+from bench import c3_operand as operand  # noqa: E402
 
 
 def _nan(t, kind, size):
