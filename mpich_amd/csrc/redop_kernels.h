@@ -156,35 +156,6 @@ template <class C> __device__ __forceinline__ v4u combine16(v4u a, v4u b, const 
     return __builtin_bit_cast(v4u, pa);
 }
 
-// Combiners with a rare slow case (C99 Annex G complex product: recovery only
-// when both parts come out NaN) may provide apply_fast(a, b, prm, need), the
-// common-case result plus a flag; the tile then runs the fast form over all
-// its packets and re-runs the full apply only if some element of this lane
-// raised the flag -- one (almost never taken) branch per tile instead of one
-// per element, so the tile's loads, combines and stores stay one block.
-template <class C, class = void> struct HasFast {
-    static constexpr bool value = false;
-};
-template <class C>
-struct HasFast<C, decltype((void) C::apply_fast(typename C::unit(), typename C::unit(),
-                                               *(const Params *) nullptr, *(bool *) nullptr))> {
-    static constexpr bool value = true;
-};
-
-template <class C>
-__device__ __forceinline__ v4u combine16_fast(v4u a, v4u b, const Params &prm, bool &need)
-{
-    using T = typename C::unit;
-    constexpr int E = 16 / sizeof(T);
-    struct alignas(16) Pk { T u[E]; };
-    Pk pa = __builtin_bit_cast(Pk, a);
-    Pk pb = __builtin_bit_cast(Pk, b);
-#pragma unroll
-    for (int e = 0; e < E; ++e)
-        pa.u[e] = C::apply_fast(pa.u[e], pb.u[e], prm, need);
-    return __builtin_bit_cast(v4u, pa);
-}
-
 // AIN: `in` has the same 16-byte phase as `io` (packet loads); otherwise it
 // is only element-aligned and its packets are read with unaligned loads
 // (still one dwordx4 per lane; the lines are shared with the neighbours').
@@ -233,32 +204,9 @@ contig_body(const typename C::unit *__restrict__ in, typename C::unit *__restric
             // (1-byte ints, fp16 complex) below the first packet's combine, so
             // fewer bytes are in flight per wave (tools/isa_seq.py)
             __builtin_amdgcn_sched_barrier(0);
-            if constexpr (HasFast<C>::value) {
-                v4u r[U];
-                bool need = false;
 #pragma unroll
-                for (int u = 0; u < U; ++u)
-                    r[u] = combine16_fast<C>(a[u], b[u], prm, need);
-                if (__builtin_expect(need, 0)) {
-                    // the full form on the packets already in registers (one
-                    // packet per lane since round 5, so they fit): with NaNs
-                    // in the data (config 3's 1 % specials, absorbing under
-                    // repeated folds) many waves come here, and re-reading the
-                    // packets from memory and calling the recovery cost
-                    // 20 % of the rate (profiles/r05_c3_inputs.json)
-#pragma unroll
-                    for (int u = 0; u < U; ++u)
-                        st(vio + i + u * nt, combine16<C>(a[u], b[u], prm));
-                } else {
-#pragma unroll
-                    for (int u = 0; u < U; ++u)
-                        st(vio + i + u * nt, r[u]);
-                }
-            } else {
-#pragma unroll
-                for (int u = 0; u < U; ++u)
-                    st(vio + i + u * nt, combine16<C>(a[u], b[u], prm));
-            }
+            for (int u = 0; u < U; ++u)
+                st(vio + i + u * nt, combine16<C>(a[u], b[u], prm));
         } else {
             for (int u = 0; u < U; ++u) {
                 uint64_t k = i + u * nt;

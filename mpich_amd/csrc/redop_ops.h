@@ -257,15 +257,6 @@ template <typename R> struct CProdAnnexG {
             z = recover(a, b, c, d, ac, bd, ad, bc, z);
         return z;
     }
-    // the plain product, and whether apply() would have to recover it
-    static MPIX_DEV unit apply_fast(unit x, unit y, const Params &, bool &need)
-    {
-        unit z;
-        z.re = x.re * y.re - x.im * y.im;
-        z.im = x.re * y.im + x.im * y.re;
-        need |= __builtin_isnan(z.re) & __builtin_isnan(z.im);
-        return z;
-    }
     static MPIX_DEV unit recover(R a, R b, R c, R d, R ac, R bd, R ad, R bc, unit z)
     {
         bool recalc = false;

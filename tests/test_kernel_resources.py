@@ -8,8 +8,7 @@ headline and the config-3 rows -- must stay well under the 128-VGPR cap of
 `__launch_bounds__(1024)`: the Annex G complex product sat at 128 with 32
 bytes of scratch at four packets per lane until its slow path stopped reusing
 the tile's registers ("Store policy"); at one packet per lane
-(round 5) the slow path runs on the registers again, its recovery inlined,
-at 45 VGPRs."""
+(round 5) it is the plain per-element form again, its recovery inlined."""
 import os
 import re
 import shutil
