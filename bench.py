@@ -850,7 +850,8 @@ def other_configs(inb, inout, n, stream):
         config3_per_pair_1GiB=dict(pairs=len(rows), min_GBs=gbs[0], median_GBs=gbs[len(gbs) // 2],
                                    values='SURVEY 8(d) C3 distributions per type (bench.c3_operand)',
                                    max_GBs=gbs[-1], min_frac=round(gbs[0] / HBM_PEAK_GBS, 4),
-                                   slowest=[dict(GBs=g, type=t, op=o) for g, t, o in rows[:3]]),
+                                   slowest=[dict(GBs=g, type=t, op=o) for g, t, o in rows[:3]],
+                                   every_row=[[t, o, g] for g, t, o in rows]),
         x87_binary128_1GiB=soft,
         x87_binary128_values='every 16-byte slot a uniform [-1, 1) double widened exactly to the '
                              'x87 / binary128 encoding (bench.fill_soft_slots)',
