@@ -136,6 +136,9 @@ int main(int argc, char **argv)
         {"k4_slots4x2_b64_wt", 4, wt<tree<4, 2, 64>>, "k4_slots4x2"}, {"k4_rec4x1_b64_wt", 4, wt<rec<4, 1, 64>>, "k4_slots4x2"},
         {"k8_rec8x1_b64_wt", 8, wt<rec<8, 1, 64>>, "k8_slots8x2"}, {"k16_rec16x1_b64_wt", 16, wt<rec<16, 1, 64>>, "k16_slots16x1"},
         {"k8_multi7_u1_b64_wt", 8, wt<multi<1, 64>>, nullptr}, {"k16_multi15_u1_b64_wt", 16, wt<multi<1, 64>>, nullptr},
+        // one-wave blocks at two packets per lane (2 KiB per stream per wave)
+        {"k8_multi7_u2_b64_wt", 8, wt<multi<2, 64>>, nullptr}, {"k8_rec8x2_b64_wt", 8, wt<rec<8, 2, 64>>, "k8_slots8x2"},
+        {"k4_multi3_u2_b64_wt", 4, wt<multi<2, 64>>, nullptr}, {"k4_multi3_u1_b64_wt", 4, wt<multi<1, 64>>, nullptr},
     };
     std::vector<int> same(vs.size(), -1);
     std::vector<float> h_ref(n), h_got(n);
