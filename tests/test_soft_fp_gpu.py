@@ -99,3 +99,33 @@ def test_entry_points(R, oracle):
     h = a.copy()
     assert R.MPI_Reduce_local(bs[0].copy(), h, n, S.LD, S.MPI_SUM) == 0
     assert np.array_equal(h, orc(bs[0], a.copy()))
+
+
+@pytest.mark.parametrize('name,dt,op,short,ba,bb', [
+    ('x87 PROD ties', S.LD, S.MPI_PROD, S._short_x87, 32, 34),
+    ('quad PROD ties', S.REAL16, S.MPI_PROD, S._short_quad, 57, 58),
+    ('x87 SUM ties', S.LD, S.MPI_SUM, S._short_x87, 40, 40),
+    ('quad SUM ties', S.REAL16, S.MPI_SUM, S._short_quad, 80, 80)])
+def test_fast_path_rounding_ties(R, oracle, name, dt, op, short, ba, bb):
+    """the normal-operand fast paths (round 5) on gfx950: short significands
+    whose products and sums land on rounding ties, carries and (sums with
+    exponents close together) near-cancellations -- the sets
+    tests/test_soft_fp.py checks on the host build, here through the AMDGPU
+    code generation of the same 128-bit arithmetic"""
+    rng = np.random.default_rng(0x5EED0930 + ba + op)
+    n = 200000
+    a, b = short(rng, n, ba), short(rng, n, bb)
+    if op == S.MPI_SUM:         # exponents of b within +-8 of a's: carries and cancellations
+        if dt == S.LD:
+            ea = a[:, 8:10].copy().view(np.uint16).reshape(-1) & 0x7fff
+            eb = np.clip(ea.astype(np.int64) + rng.integers(-8, 9, n), 1, 0x7ffe).astype(np.uint16)
+            sb = b[:, 8:10].copy().view(np.uint16).reshape(-1) & 0x8000
+            b[:, 8:10] = (sb | eb).view(np.uint8).reshape(n, 2)
+        else:
+            ha = a[:, 8:].copy().view(np.uint64).reshape(-1)
+            hb = b[:, 8:].copy().view(np.uint64).reshape(-1)
+            ea = ((ha >> np.uint64(48)) & np.uint64(0x7fff)).astype(np.int64)
+            eb = np.clip(ea + rng.integers(-8, 9, n), 1, 0x7ffe).astype(np.uint64)
+            hb = (hb & ~np.uint64(0x7fff << 48)) | (eb << np.uint64(48))
+            b[:, 8:] = hb.view(np.uint8).reshape(n, 8)
+    _gpu_vs_oracle(R, oracle, dt, op, a, b, 16)
