@@ -275,10 +275,10 @@ int MPIX_Comm_set_max_message(MPIX_Comm comm, MPIX_Aint bytes);
 
 /* Smallest half-step (bytes) whose combine MPIX_RSB_RECURSIVE_HALVING cuts
  * along the next step's split and runs under the next exchange (see
- * MPIX_RSB_RECURSIVE_HALVING): 0 = never, -1 = the default of the
- * communicator's kind (1 MiB on RCCL communicators, off on the others).  A
- * communicator starts with env MPIX_COLL_RH_OVERLAP (read once, at creation)
- * or that default.  Local, not collective: every rank of a communicator must
+ * MPIX_RSB_RECURSIVE_HALVING): 0 = never, -1 = the value the communicator
+ * was created with.  A communicator starts with env MPIX_COLL_RH_OVERLAP (read
+ * once, at creation) or, without it, its kind's default (1 MiB on RCCL
+ * communicators, off on the others).  Local, not collective: every rank of a communicator must
  * set the same value before the collective (the split changes only which
  * stream runs a combine, never the bits). */
 int MPIX_Comm_set_rh_overlap(MPIX_Comm comm, MPIX_Aint min_bytes);

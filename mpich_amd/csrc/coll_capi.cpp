@@ -119,6 +119,7 @@ struct MPIX_Comm_s {
     int same_node = -1;                // every rank on this host (IPC possible): -1 not yet asked
     size_t max_msg = 0;                // MPIX_Comm_set_max_message: split above this (0: never)
     size_t rh_min = 0;                 // MPIX_Comm_set_rh_overlap (rh_overlap_default at creation)
+    size_t rh_created = 0;             // that creation-time value: what -1 restores
     struct Nonce { int rank, attempt; uint64_t n0, n1; };
     std::vector<Nonce> nonce_hist;     // every window nonce published (MPIX_COLL_TRACE)
     struct Shared {                    // MPIX_Comm_alloc_shared windows
@@ -2410,7 +2411,7 @@ MPIX_Comm new_comm(int rank, int size, Kind kind)
     c->kind = kind;
     c->send_seq.assign(size, 0);
     c->recv_seq.assign(size, 0);
-    c->rh_min = rh_overlap_default(kind);
+    c->rh_min = c->rh_created = rh_overlap_default(kind);
     return c;
 }
 
@@ -2548,7 +2549,9 @@ int MPIX_Comm_set_rh_overlap(MPIX_Comm comm, MPIX_Aint min_bytes)
 {
     if (!comm || min_bytes < -1)
         return MPIX_REDOP_ERR_ARG;
-    comm->rh_min = min_bytes == -1 ? (comm->kind == K_CCL ? size_t(1) << 20 : 0) : (size_t) min_bytes;
+    // -1: the value the communicator was created with (the kind's default,
+    // or MPIX_COLL_RH_OVERLAP as it read then)
+    comm->rh_min = min_bytes == -1 ? comm->rh_created : (size_t) min_bytes;
     return MPIX_REDOP_SUCCESS;
 }
 

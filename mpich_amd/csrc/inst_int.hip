@@ -76,7 +76,7 @@ k_equal(const unsigned char *__restrict__ in, unsigned char *__restrict__ io, ui
 hipError_t launch_equal(const void *in, void *io, uint64_t n, hipStream_t s)
 {
     uint64_t npk = (n - 8) / 16;
-    unsigned grid = grid_for(256ull * 4, npk, 0);
+    unsigned grid = grid_for(256ull * 4, npk, 0, 256);
     hipLaunchKernelGGL(k_equal, dim3(grid), dim3(256), 0, s,
                        static_cast<const unsigned char *>(in), static_cast<unsigned char *>(io), n);
     return hipGetLastError();
@@ -135,7 +135,7 @@ hipError_t launch_copy_multi(const void *const *srcs, void *const *dsts, const u
         most = bytes[q] > most ? bytes[q] : most;
     }
     // about 2048 workgroups in all: each segment's share of the 256 CUs
-    unsigned gx = grid_for(256ull * 16 * 4, most, (int) (2048 / (unsigned) n));
+    unsigned gx = grid_for(256ull * 16 * 4, most, (int) (2048 / (unsigned) n), 256);
     hipLaunchKernelGGL(k_copy_multi, dim3(gx, (unsigned) n), dim3(256), 0, s, sg, wt_xcd & 0xffu);
     return hipGetLastError();
 }

@@ -58,6 +58,27 @@ struct Entry {
                         const Params &, const LaunchCfg &, hipStream_t);
 };
 
+// Most blocks one dispatch of `block`-thread workgroups may have: HIP caps a
+// dispatch at UINT32_MAX work-items (gridDim.x * blockDim.x), so with one-wave
+// blocks that is 2^26 - 1 blocks, not 2^31.  Every kernel
+// launched through grid_for strides over the rest.
+constexpr uint64_t max_blocks(uint64_t block)
+{
+    return 0xffffffffull / (block ? block : 1);
+}
+
+inline unsigned grid_for(uint64_t work_per_block_units, uint64_t n, int max_grid, uint64_t block)
+{
+    uint64_t g = (n + work_per_block_units - 1) / work_per_block_units;
+    if (g == 0)
+        g = 1;
+    if (max_grid > 0 && g > (uint64_t) max_grid)
+        g = (uint64_t) max_grid;
+    if (g > max_blocks(block))
+        g = max_blocks(block);
+    return (unsigned) g;
+}
+
 constexpr int kMaxBatchSegs = 64;       // MPIX_BATCH_MAX
 
 constexpr int kMaxMultiInputs = 16;

@@ -834,18 +834,6 @@ k_iov(const typename C::unit *__restrict__ in, typename C::unit *__restrict__ io
     }
 }
 
-static inline unsigned grid_for(uint64_t work_per_block_units, uint64_t n, int max_grid)
-{
-    uint64_t g = (n + work_per_block_units - 1) / work_per_block_units;
-    if (g == 0)
-        g = 1;
-    if (max_grid > 0 && g > (uint64_t) max_grid)
-        g = (uint64_t) max_grid;
-    if (g > 0x7fffffffull)
-        g = 0x7fffffffull;
-    return (unsigned) g;
-}
-
 // The store policy (LaunchCfg::wt_*) of a launch of `grid` blocks.
 inline void set_store_policy(Params &p, const LaunchCfg &cfg, unsigned grid)
 {
@@ -887,7 +875,7 @@ hipError_t launch_contig(const void *in, void *io, uint64_t count, const Params 
         // element-wise
         if (((ai | ao) & 15) == 0) {
             constexpr int U32 = MPIX_REDOP_UNROLL32;
-            unsigned grid = grid_for((uint64_t) kContig32Block * U32, count, cfg.max_grid);
+            unsigned grid = grid_for((uint64_t) kContig32Block * U32, count, cfg.max_grid, kContig32Block);
             Params p = prm;
             p.done = nullptr;
             set_store_policy(p, cfg, grid);
@@ -895,7 +883,7 @@ hipError_t launch_contig(const void *in, void *io, uint64_t count, const Params 
                                dim3(grid), dim3(kContig32Block), 0, s, tin, tio, tio, count, p, grid,
                                kContig32Block);
         } else {
-            unsigned grid = grid_for((uint64_t) cfg.block * 4, count, cfg.max_grid);
+            unsigned grid = grid_for((uint64_t) cfg.block * 4, count, cfg.max_grid, cfg.block);
             hipLaunchKernelGGL((k_elem<C>), dim3(grid), dim3(cfg.block), 0, s, tin, tio, count,
                                prm, grid, (uint32_t) cfg.block);
         }
@@ -907,7 +895,7 @@ hipError_t launch_contig(const void *in, void *io, uint64_t count, const Params 
         uint64_t tail_start = head + npk * E;
         uint32_t ntail = (uint32_t) (count - tail_start);
         const uint64_t tile = (uint64_t) cfg.block * MPIX_REDOP_UNROLL;
-        unsigned grid = grid_for(tile, npk, cfg.max_grid);
+        unsigned grid = grid_for(tile, npk, cfg.max_grid, cfg.block);
         // up to kSignalMaxGrid workgroups (64 KiB per operand at the defaults): the
         // kernel stores the completion word itself (Params::done)
         Params p = prm;
@@ -926,7 +914,7 @@ hipError_t launch_contig(const void *in, void *io, uint64_t count, const Params 
                 dim3(grid), dim3(cfg.block), 0, s, tin, tio, head, npk, tail_start, ntail, p,
                 grid, (uint32_t) cfg.block);
     } else {
-        unsigned grid = grid_for((uint64_t) cfg.block * 4, count, cfg.max_grid);
+        unsigned grid = grid_for((uint64_t) cfg.block * 4, count, cfg.max_grid, cfg.block);
         hipLaunchKernelGGL((k_elem<C>), dim3(grid), dim3(cfg.block), 0, s, tin, tio, count, prm,
                            grid, (uint32_t) cfg.block);
     }
@@ -963,14 +951,14 @@ hipError_t launch_multi(const void *const *ins, int k, void *io, uint64_t count,
         // 1 GiB, store policy on) against 6.04 / 5.83 with two; 4 measured no
         // better than 2 (tools/tree8_probe.hip, tools/multi_probe.py)
         constexpr int U = 1;
-        unsigned grid = grid_for((uint64_t) cfg.block * U, npk, cfg.max_grid);
+        unsigned grid = grid_for((uint64_t) cfg.block * U, npk, cfg.max_grid, cfg.block);
         Params p = prm;
         set_store_policy(p, cfg, grid);
         if constexpr (sizeof(T) <= 16)
             hipLaunchKernelGGL((k_contig_multi<C, U>), dim3(grid), dim3(cfg.block), 0, s, mi, k,
                                tio, head, npk, tail_start, ntail, p, grid, (uint32_t) cfg.block);
     } else {
-        unsigned grid = grid_for((uint64_t) cfg.block * 4, count, cfg.max_grid);
+        unsigned grid = grid_for((uint64_t) cfg.block * 4, count, cfg.max_grid, cfg.block);
         hipLaunchKernelGGL((k_elem_multi<C>), dim3(grid), dim3(cfg.block), 0, s, mi, k, tio, count,
                            prm, grid, (uint32_t) cfg.block);
     }
@@ -1005,7 +993,7 @@ hipError_t launch_tree(const void *const *ins, int k, void *out, uint64_t count,
             ((ao | reinterpret_cast<uintptr_t>(ins[0]) | reinterpret_cast<uintptr_t>(ins[1])) & 15) ==
                 0) {
             constexpr int U32 = MPIX_REDOP_UNROLL32;
-            const unsigned grid = grid_for((uint64_t) kContig32Block * U32, count, cfg.max_grid);
+            const unsigned grid = grid_for((uint64_t) kContig32Block * U32, count, cfg.max_grid, kContig32Block);
             Params p = prm;
             p.done = nullptr;
             set_store_policy(p, cfg, grid);
@@ -1042,18 +1030,21 @@ hipError_t launch_tree(const void *const *ins, int k, void *out, uint64_t count,
         // / 16 at 6.84-6.96 / 6.48-6.61 / 6.58-6.67 / 6.06-6.45 TB/s against
         // 6.64-6.76 / 6.36-6.43 / 6.25-6.28 / 5.82-6.43 with 256 threads
         // (r05_tree_forms.json, last run).
+        // The public entry takes k = 2, 4, 8, 16 only (the collectives pad an odd
+        // world's fold with absent slots); a k between them runs the next
+        // larger form, whose uniform branches skip the slots >= k.
         constexpr unsigned kTreeBlock = 64;
-        const unsigned per = (k == 2 || k == 4) ? kTreeBlock * 2 : kTreeBlock;
-        const unsigned grid = grid_for(per, npk, 0);
+        const unsigned per = k <= 4 ? kTreeBlock * 2 : kTreeBlock;
+        const unsigned grid = grid_for(per, npk, 0, kTreeBlock);
         set_store_policy(p, cfg, grid);
         if constexpr (sizeof(T) <= 16) {
-            if (k == 2)     // out = a OP b (recursive halving's combine_to)
+            if (k <= 2)     // out = a OP b (recursive halving's combine_to)
                 hipLaunchKernelGGL((k_contig_tree_rec<C, 2, 2>), dim3(grid), dim3(kTreeBlock), 0, s,
                                    mi, k, pres, tout, head, npk, tail_start, ntail, p);
-            else if (k == 4)
+            else if (k <= 4)
                 hipLaunchKernelGGL((k_contig_tree<C, 4, 2>), dim3(grid), dim3(kTreeBlock), 0, s, mi,
                                    k, pres, tout, head, npk, tail_start, ntail, p);
-            else if (k == 8)    // the P = 8 pull's fold
+            else if (k <= 8)    // the P = 8 pull's fold
                 hipLaunchKernelGGL((k_contig_tree_rec<C, 8, 1>), dim3(grid), dim3(kTreeBlock), 0, s,
                                    mi, k, pres, tout, head, npk, tail_start, ntail, p);
             else
@@ -1061,7 +1052,7 @@ hipError_t launch_tree(const void *const *ins, int k, void *out, uint64_t count,
                                    0, s, mi, k, pres, tout, head, npk, tail_start, ntail, p);
         }
     } else {
-        hipLaunchKernelGGL((k_elem_tree<C>), dim3(grid_for(256 * 4, count, 0)), dim3(256), 0, s,
+        hipLaunchKernelGGL((k_elem_tree<C>), dim3(grid_for(256 * 4, count, 0, 256)), dim3(256), 0, s,
                            mi, k, pres, tout, count, prm);
     }
     return hipGetLastError();
@@ -1077,14 +1068,14 @@ hipError_t launch_vector(const void *in, void *io, uint64_t count, uint64_t bl, 
         return hipSuccess;
     if (bl == st)       // contiguous after all
         return launch_contig<C>(in, io, n, prm, cfg, s);
-    unsigned grid = grid_for((uint64_t) cfg.block * 4, n, cfg.max_grid);
+    unsigned grid = grid_for((uint64_t) cfg.block * 4, n, cfg.max_grid, cfg.block);
     bool s2 = false;
     if constexpr (sizeof(T) <= 16)
         s2 = bl == 1 && st == 2 && (reinterpret_cast<uintptr_t>(io) % (2 * sizeof(T))) == 0;
     if (s2) {
         if constexpr (sizeof(T) <= 16) {
             constexpr unsigned kVb = MPIX_REDOP_VBLOCK;
-            const unsigned g2 = grid_for(kVb, n, cfg.max_grid);
+            const unsigned g2 = grid_for(kVb, n, cfg.max_grid, kVb);
             hipLaunchKernelGGL((k_vector_s2<C>), dim3(g2), dim3(kVb), 0, s,
                                static_cast<const T *>(in), static_cast<T *>(io), n, prm, g2, kVb);
         }
@@ -1107,7 +1098,7 @@ hipError_t launch_iov(const void *in, void *io, const int64_t *d_seg_off, const 
     using T = typename C::unit;
     if (total == 0 || nseg == 0)
         return hipSuccess;
-    unsigned grid = grid_for(256ull * 4, total, cfg.max_grid);
+    unsigned grid = grid_for(256ull * 4, total, cfg.max_grid, 256);
     hipLaunchKernelGGL((k_iov<C>), dim3(grid), dim3(256), 0, s, static_cast<const T *>(in),
                        static_cast<T *>(io), d_seg_off, d_prefix, d_src_off, nseg, total, prm, grid);
     return hipGetLastError();
@@ -1156,13 +1147,13 @@ hipError_t launch_batch(const void *const *ins, void *const *ios, const uint64_t
                 continue;
             }
             const uint64_t nb = (count + tile - 1) / tile;
-            if (nb > 0x7fffffffull) {       // more tiles than one grid holds: a call of its own
+            if (nb > max_blocks(kContig32Block)) {   // more tiles than one grid holds: a call of its own
                 hipError_t e = launch_contig<C>(ins[i], ios[i], count, p, cfg, s);
                 if (e != hipSuccess)
                     return e;
                 continue;
             }
-            if (blocks + nb > 0x7fffffffull) {
+            if (blocks + nb > max_blocks(kContig32Block)) {
                 hipError_t e = flush();
                 if (e != hipSuccess)
                     return e;
@@ -1211,13 +1202,13 @@ hipError_t launch_batch(const void *const *ins, void *const *ios, const uint64_t
             uint64_t nb = (npk + tile - 1) / tile;
             if (nb == 0)
                 nb = 1;         // a segment of head / tail elements only
-            if (nb > 0x7fffffffull) {       // more tiles than one grid holds: launch_contig
+            if (nb > max_blocks(cfg.block)) {    // more tiles than one grid holds: launch_contig
                 hipError_t e = launch_contig<C>(ins[i], ios[i], count, p, cfg, s);   // loops
                 if (e != hipSuccess)
                     return e;
                 continue;
             }
-            if (blocks + nb > 0x7fffffffull) {
+            if (blocks + nb > max_blocks(cfg.block)) {
                 hipError_t e = flush();
                 if (e != hipSuccess)
                     return e;

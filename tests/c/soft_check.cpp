@@ -24,8 +24,20 @@ static void run(const void *in, void *inout, long n)
     }
 }
 
+// the sums through the general path only (x87_add / quad_add with FAST =
+// false): the normal-operand fast paths must give the same bits
+struct X87SumGeneral {
+    using unit = X87;
+    static X87 apply(X87 a, X87 b, const Params &) { return x87_add<false>(a, b, false); }
+};
+struct QuadSumGeneral {
+    using unit = Quad;
+    static Quad apply(Quad a, Quad b, const Params &) { return quad_add<false>(a, b, false); }
+};
+
 // which: 0 x87 SUM, 1 x87 PROD, 2 binary128 SUM, 3 binary128 PROD,
-// 4 binary128 complex SUM, 5 binary128 complex PROD, 6 x87 complex SUM, 7 x87 complex PROD
+// 4 binary128 complex SUM, 5 binary128 complex PROD, 6 x87 complex SUM, 7 x87 complex PROD,
+// 8 x87 SUM general path only, 9 binary128 SUM general path only
 extern "C" int soft_reduce(int which, const void *in, void *inout, long n)
 {
     switch (which) {
@@ -37,6 +49,8 @@ extern "C" int soft_reduce(int which, const void *in, void *inout, long n)
         case 5: run<QuadCProd>(in, inout, n); return 0;
         case 6: run<X87CSum>(in, inout, n); return 0;
         case 7: run<X87CProd>(in, inout, n); return 0;
+        case 8: run<X87SumGeneral>(in, inout, n); return 0;
+        case 9: run<QuadSumGeneral>(in, inout, n); return 0;
     }
     return -1;
 }

@@ -313,7 +313,7 @@ def test_rh_overlap_setting_per_communicator(monkeypatch):
         assert comms[0].rh_overlap() == 0           # not re-read after creation
         comms[0].set_rh_overlap(1 << 20)
         assert comms[0].rh_overlap() == 1 << 20 and comms[1].rh_overlap() == 0
-        comms[0].set_rh_overlap(-1)                 # the kind's default
+        comms[0].set_rh_overlap(-1)                 # the creation-time value
         assert comms[0].rh_overlap() == 0
         with pytest.raises(redop.RedopError):
             comms[0].set_rh_overlap(-2)
@@ -323,6 +323,11 @@ def test_rh_overlap_setting_per_communicator(monkeypatch):
     comms = ccl.comm_create_local(2)                # created with the env set
     try:
         assert [c.rh_overlap() for c in comms] == [4096, 4096]
+        # -1 restores what the communicator was created with (the
+        # env's 4096 here), not the kind's compiled default
+        comms[0].set_rh_overlap(0)
+        comms[0].set_rh_overlap(-1)
+        assert comms[0].rh_overlap() == 4096
     finally:
         for c in comms:
             c.free()

@@ -129,3 +129,95 @@ def test_large_count_every_entry_matches_oracle(R, oracle, name, dt, ext, count,
     s.synchronize()
     bad['multi'] = _bytes_equal(io, exp2)
     assert all(v is None for v in bad.values()), bad
+
+
+# ---------------------------------------------------------------- 2^32 packets
+# with one 16-byte packet per lane in one-wave blocks, an operand
+# of 2^32 packets (64 GiB) needs 2^26 blocks of 64 lanes -- exactly where a
+# dispatch passes UINT32_MAX work-items.  grid_for caps the grid at
+# floor((2^32 - 1) / block) blocks (tests/test_grid_cap.py checks the rule on
+# the host); here the capped kernels run on the GPU and stride over the rest.
+# 64 GiB per operand: the operands are closed-form byte patterns made and
+# checked chunk by chunk on the device (in[i] = 7i + 3, inout[i] = 13i + 1,
+# mod 256; MPI_INT8_T SUM wraps mod 256, so the result is 20i + 4, and the
+# two-input fold inout + in + in is 27i + 7) -- an oracle pass over 128 GiB of
+# host memory would take minutes.
+HUGE = (1 << 36) + 4099             # elements (bytes) per operand, > 2^32 packets
+CHUNK = 1 << 28
+
+
+def _pattern(t, a, b, start=0):
+    """t[j] = (a * (start + j) + b) mod 256, made in CHUNK pieces"""
+    for s in range(0, t.numel(), CHUNK):
+        e = min(t.numel(), s + CHUNK)
+        i = torch.arange(start + s, start + e, dtype=torch.int64, device='cuda')
+        t[s:e].copy_(((i * a + b) & 0xff).to(torch.uint8))
+        del i
+
+
+def _pattern_mismatch(t, a, b):
+    for s in range(0, t.numel(), CHUNK):
+        e = min(t.numel(), s + CHUNK)
+        i = torch.arange(s, e, dtype=torch.int64, device='cuda')
+        want = ((i * a + b) & 0xff).to(torch.uint8)
+        if not torch.equal(t[s:e], want):
+            bad = torch.nonzero(t[s:e] != want)
+            return 'chunk at %d: %d bytes differ, first at %d' % (s, bad.numel(), s + int(bad[0]))
+    return None
+
+
+@pytest.mark.timeout(900)
+def test_past_2_32_packets_every_entry(R):
+    free, _ = torch.cuda.mem_get_info()
+    if free < 2 * HUGE + (16 << 30):
+        pytest.skip('needs ~144 GiB of free device memory (have %d GiB)' % (free >> 30))
+    off = 3                         # inout and in off the 16-byte grid, same phase
+    io_buf = torch.empty(HUGE + 64, dtype=torch.uint8, device='cuda')
+    in_buf = torch.empty(HUGE + 64, dtype=torch.uint8, device='cuda')
+    io = io_buf[off:off + HUGE]
+    src = in_buf[off:off + HUGE]
+    io_buf[:off].fill_(0xA5)
+    io_buf[off + HUGE:].fill_(0xA5)
+    _pattern(src, 7, 3)
+    s = torch.cuda.current_stream()
+    bad = {}
+
+    def reset():
+        _pattern(io, 13, 1)
+        torch.cuda.synchronize()
+
+    reset()
+    assert R.lib().MPIX_Reduce_local(src.data_ptr(), io.data_ptr(), HUGE, MPI_INT8_T, MPI_SUM) == 0
+    bad['sync'] = _pattern_mismatch(io, 20, 4)
+    reset()
+    assert R.reduce_local_async(src.data_ptr(), io.data_ptr(), HUGE, MPI_INT8_T, MPI_SUM, s) == 0
+    s.synchronize()
+    bad['async'] = _pattern_mismatch(io, 20, 4)
+    # batch: a small segment beside the huge one (the huge one exceeds one
+    # grid's blocks, so it goes as a capped launch of its own)
+    reset()
+    small_io = torch.zeros(4099 + 64, dtype=torch.uint8, device='cuda')
+    small_in = torch.full((4099 + 64,), 5, dtype=torch.uint8, device='cuda')
+    ins = (ctypes.c_void_p * 2)(small_in.data_ptr() + 4, src.data_ptr())
+    ios = (ctypes.c_void_p * 2)(small_io.data_ptr() + 4, io.data_ptr())
+    cnt = (ctypes.c_ssize_t * 2)(4099, HUGE)
+    assert R.lib().MPIX_Reduce_local_batch_async(ins, ios, cnt, 2, MPI_INT8_T, MPI_SUM,
+                                                 s.cuda_stream) == 0
+    s.synchronize()
+    bad['batch'] = _pattern_mismatch(io, 20, 4)
+    bad['batch_small'] = None if bool(torch.all(small_io[4:4 + 4099] == 5)) and \
+        bool(torch.all(small_io[:4] == 0)) and bool(torch.all(small_io[4 + 4099:] == 0)) \
+        else 'small segment wrong'
+    # multi-input k = 2, the same input twice: inout + in + in
+    reset()
+    arr = (ctypes.c_void_p * 2)(src.data_ptr(), src.data_ptr())
+    assert R.lib().MPIX_Reduce_local_multi_async(arr, 2, io.data_ptr(), HUGE, MPI_INT8_T, MPI_SUM,
+                                                 s.cuda_stream) == 0
+    s.synchronize()
+    bad['multi'] = _pattern_mismatch(io, 27, 7)
+    # the bytes around inout never written
+    bad['guard'] = None if bool(torch.all(io_buf[:off] == 0xA5)) and \
+        bool(torch.all(io_buf[off + HUGE:] == 0xA5)) else 'bytes outside inout written'
+    del io_buf, in_buf, io, src
+    torch.cuda.empty_cache()
+    assert all(v is None for v in bad.values()), bad

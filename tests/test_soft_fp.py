@@ -290,3 +290,27 @@ def test_sum_rounding_ties(soft, oracle, which, dt, ext_bits, spread):
         hb = (hb & ~np.uint64(0x7fff << 48)) | (eb << np.uint64(48))
         b[:, 8:] = hb.view(np.uint8).reshape(n, 8)
     _check(soft, oracle, which, dt, MPI_SUM, a, b, 16)
+
+
+@pytest.mark.parametrize('fast,general,dt,ext_bits', [(0, 8, LD, 40), (2, 9, REAL16, 80)])
+@pytest.mark.parametrize('kind', ['wide', 'close', 'ties'])
+def test_sum_fast_path_equals_general_path(soft, oracle, fast, general, dt, ext_bits, kind):
+    """x87_add / quad_add's FAST = false instantiation (the general
+    path alone) against the shipped fast path, bit for bit, on normal
+    operands -- wide exponents, close ones (cancellation, carries) and short
+    significands on rounding ties -- and both against the oracle"""
+    rng = np.random.default_rng(0x5EED0890 + fast + len(kind))
+    n = 200000
+    if kind == 'ties':
+        make = _short_x87 if fast == 0 else _short_quad
+        a, b = make(rng, n, ext_bits), make(rng, n, ext_bits)
+    else:
+        make = x87_random if fast == 0 else quad_random
+        a, b = make(rng, n, close=kind == 'close'), make(rng, n, close=kind == 'close')
+    got = {}
+    for which in (fast, general):
+        r = a.reshape(-1).copy()
+        assert soft.soft_reduce(which, b.reshape(-1).ctypes.data, r.ctypes.data, n) == 0
+        got[which] = r
+    assert np.array_equal(got[fast], got[general])
+    _check(soft, oracle, general, dt, MPI_SUM, a, b, 16)
