@@ -50,6 +50,7 @@ METRIC_RSB = ("GB/s MPI_Reduce_scatter_block bus bandwidth (fp32 SUM, 4 GiB vect
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 XGMI_LINK_GBS = 153.0       # one xGMI link, one direction (task brief: 7 x ~153 GB/s per GPU)
 GIB = float(1 << 30)
+EXIT_PARITY = 3             # a rank's result failed a bit / closed-form check
 
 
 def parse(argv=None):
@@ -400,29 +401,28 @@ def cpu_baseline(seconds, count, crossover_rows):
     phys = topo['physical']
     alg = 3 * count * 4
 
-    def leg(kind, cpus, budget, n=count):
-        if kind == 'reduce':
-            best, med, passes, span = orc.bench_reduce(n, H.MPI_FLOAT, H.MPI_SUM, cpus, budget)
-        else:
-            best, med, passes, span = orc.bench_triad(n, cpus, budget)
+    def leg(cpus, budget, n=count):
+        """the reduce and the host triad in the same passes (oracle_bench_pair):
+        same pinned threads, same first-touched slices, same quota windows"""
+        best, med, passes, span, tbest, tmed, ratio = orc.bench_pair(n, H.MPI_FLOAT, H.MPI_SUM,
+                                                                     cpus, budget)
         nb = 3 * n * 4
         return dict(gibs=round(nb / GIB / med, 3), best=round(nb / GIB / best, 3),
                     sustained=round(passes * nb / GIB / span, 3) if span > 0 else None,
-                    reps=passes, threads=len(cpus))
+                    reps=passes, threads=len(cpus), triad_gibs=round(nb / GIB / tmed, 3),
+                    frac=round(tmed / med, 4), frac_per_pass=round(1.0 / ratio, 4) if ratio else None)
 
     quota = topo['cgroup_cpu_quota']
     nq = max(1, min(len(phys), int(quota))) if quota else len(phys)
-    one = leg('reduce', phys[:1], seconds * 0.25)
-    allc = leg('reduce', phys, seconds * 0.15)
-    tri_all = leg('triad', phys, seconds * 0.1)
-    tri_one = leg('triad', phys[:1], seconds * 0.1)
-    c1 = leg('reduce', phys[:1], seconds * 0.1, n=4194304)
+    one = leg(phys[:1], seconds * 0.35)
+    allc = leg(phys, seconds * 0.25)
+    c1 = leg(phys[:1], seconds * 0.1, n=4194304)
     quota_leg = None
     if nq < len(phys):
-        q = leg('reduce', phys[:nq], seconds * 0.1)
-        tq = leg('triad', phys[:nq], seconds * 0.1)
+        q = leg(phys[:nq], seconds * 0.2)
         quota_leg = dict(threads=nq, value=q['gibs'], sustained=q['sustained'],
-                         host_triad_gibs=tq['gibs'], frac_of_host_triad=round(q['gibs'] / tq['gibs'], 4),
+                         host_triad_gibs=q['triad_gibs'], frac_of_host_triad=q['frac'],
+                         frac_of_host_triad_per_pass=q['frac_per_pass'],
                          note='as many pinned threads as the cgroup quota grants CPUs, spread '
                               'over both sockets: what this process can sustain')
     if crossover_rows:
@@ -441,11 +441,17 @@ def cpu_baseline(seconds, count, crossover_rows):
                'operand, host-resident) through oracle/redop_oracle.c, 1 pinned thread, %d calls, '
                'median' % (count, count * 4 >> 20, one['reps']),
         best=one['best'],
-        host_triad_1core_gibs=tri_one['gibs'],
-        frac_of_host_triad_1core=round(one['gibs'] / tri_one['gibs'], 4),
+        host_triad_1core_gibs=one['triad_gibs'],
+        frac_of_host_triad_1core=one['frac'],
+        frac_of_host_triad_1core_per_pass=one['frac_per_pass'],
+        host_triad_timing='each pass runs the reduce, a barrier, then the triad (a += 0.5 b) on '
+                          'the same pinned threads and first-touched slices, so both are read in '
+                          'the same quota windows; frac = triad median / reduce median time, '
+                          'frac_per_pass = median over passes of triad / reduce time',
         allcores=dict(value=allc['gibs'], threads=allc['threads'], reps=allc['reps'],
-                      sustained=allc['sustained'], host_triad_gibs=tri_all['gibs'],
-                      frac_of_host_triad=round(allc['gibs'] / tri_all['gibs'], 4),
+                      sustained=allc['sustained'], host_triad_gibs=allc['triad_gibs'],
+                      frac_of_host_triad=allc['frac'],
+                      frac_of_host_triad_per_pass=allc['frac_per_pass'],
                       note='one pinned thread per physical core of this process (%d sockets), '
                            'each first-touching its own slice of both operands (NUMA-local); '
                            'value = median pass; host triad = a += 0.5 b on the same threads '
@@ -778,6 +784,26 @@ def fill_soft_slots(buf8, enc, seed):
     del d
 
 
+def fresh_event_time(launch, prep, reps, stream):
+    """median duration of `launch()` with every launch on fresh operands:
+    `prep()` (enqueued on `stream`, outside the event pair) restores them
+    first, so a data-dependent combiner is timed on the distribution it
+    claims rather than on values its own repeated folds moved"""
+    per = []
+    with torch.cuda.stream(stream):
+        for _ in range(reps):
+            prep()
+            s0 = torch.cuda.Event(enable_timing=True)
+            s1 = torch.cuda.Event(enable_timing=True)
+            s0.record(stream)
+            launch()
+            s1.record(stream)
+            s1.synchronize()
+            per.append(s0.elapsed_time(s1))
+    per.sort()
+    return per[len(per) // 2]
+
+
 def other_configs(inb, inout, n, stream):
     """BASELINE configs 3 and 5 on the same buffers (kernel-only, HIP events):
     every supported (op, type) pair at 1 GiB per operand (past the 256 MB
@@ -793,25 +819,34 @@ def other_configs(inb, inout, n, stream):
         dt = getattr(H, tn)
         ext = redop.datatype_extent(dt)
         m = nbytes // ext
-        # the C3 distributions (c3_operand), drawn per type; the timed calls
-        # then fold into inout again and again, which moves the values but
-        # not the kernel's work (no data-dependent paths in these combiners)
+        # the C3 distributions (c3_operand), drawn per type; inout is restored
+        # from a0 before each op's calls (the repeated in-place
+        # folds move the values -- PROD drives them to 0 / subnormal / Inf /
+        # NaN).  The complex products have a data-dependent path (the C99
+        # Annex G recovery, per lane when both parts come out NaN), so their
+        # rows restore inout before every timed launch; the other combiners
+        # have no data-dependent path and are timed back to back.
         g.manual_seed((0x5EED0003 * 31 + dt) & 0xffffffff)
-        a8[:m * ext].copy_(c3_operand(g, kind, size, m))
+        a0 = c3_operand(g, kind, size, m)
         b8[:m * ext].copy_(c3_operand(g, kind, size, m))
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
         for on, op in H.OPS.items():
             if op in (H.MPI_REPLACE, H.MPI_NO_OP) or not redop.is_supported(op, dt):
                 continue
-            redop.check(redop.reduce_local_async(b8, a8, m, dt, op, stream))
-            # median of three batches of five: one disturbed batch (seen once
-            # at 0.62 of the row's rate, profiles/r04_bench_n1.json) does not
-            # set the row
-            _, med, _ = event_time_per_launch(
-                lambda: redop.check(redop.reduce_local_async(b8, a8, m, dt, op, stream)), 5, stream,
-                rounds=3)
+            a8[:m * ext].copy_(a0)
+            call = lambda: redop.check(redop.reduce_local_async(b8, a8, m, dt, op, stream))  # noqa
+            if kind == 'cplx' and op == H.MPI_PROD:
+                torch.cuda.synchronize()
+                med = fresh_event_time(call, lambda: a8[:m * ext].copy_(a0), 7, stream)
+            else:
+                call()
+                # median of three batches of five: one disturbed batch (seen
+                # once at 0.62 of the row's rate, profiles/r04_bench_n1.json)
+                # does not set the row
+                _, med, _ = event_time_per_launch(call, 5, stream, rounds=3)
             rows.append((round(3 * m * ext / (med * 1e-3) / 1e9, 1), tn, on))
+        del a0
     rows.sort()
     gbs = [r[0] for r in rows]
     # beyond config 3's types: the x87 / binary128 families (software
@@ -822,8 +857,8 @@ def other_configs(inb, inout, n, stream):
     soft = []
     for tn in ('MPI_LONG_DOUBLE', 'MPI_REAL16', 'MPI_C_LONG_DOUBLE_COMPLEX', 'MPI_COMPLEX32',
                'MPI_LONG_DOUBLE_INT'):
-        fill_soft_slots(a8, 'x87' if 'LONG_DOUBLE' in tn else 'binary128', 0x5EED0003)
-        fill_soft_slots(b8, 'x87' if 'LONG_DOUBLE' in tn else 'binary128', 0x5EED0004)
+        enc = 'x87' if 'LONG_DOUBLE' in tn else 'binary128'
+        fill_soft_slots(b8, enc, 0x5EED0004)
         torch.cuda.synchronize()
         dt = getattr(H, tn)
         ext = redop.datatype_extent(dt)
@@ -831,6 +866,7 @@ def other_configs(inb, inout, n, stream):
         for on, op in H.OPS.items():
             if op in (H.MPI_REPLACE, H.MPI_NO_OP) or not redop.is_supported(op, dt):
                 continue
+            fill_soft_slots(a8, enc, 0x5EED0003)        # every op on the same normal values
             redop.check(redop.reduce_local_async(b8, a8, m, dt, op, stream))
             _, med, _ = event_time_per_launch(
                 lambda: redop.check(redop.reduce_local_async(b8, a8, m, dt, op, stream)), 3, stream,
@@ -848,7 +884,10 @@ def other_configs(inb, inout, n, stream):
                                                       stream)), 10, stream)
     return dict(
         config3_per_pair_1GiB=dict(pairs=len(rows), min_GBs=gbs[0], median_GBs=gbs[len(gbs) // 2],
-                                   values='SURVEY 8(d) C3 distributions per type (bench.c3_operand)',
+                                   values='SURVEY 8(d) C3 distributions per type (bench.c3_operand); '
+                                          'inout restored before each op, and before every '
+                                          'launch for the complex PROD rows (data-dependent '
+                                          'Annex G path)',
                                    max_GBs=gbs[-1], min_frac=round(gbs[0] / HBM_PEAK_GBS, 4),
                                    slowest=[dict(GBs=g, type=t, op=o) for g, t, o in rows[:3]],
                                    every_row=[[t, o, g] for g, t, o in rows]),
@@ -1078,6 +1117,60 @@ def rh_expected_block(sends, rank, recvcount):
     return parts[owner][rank * recvcount:(rank + 1) * recvcount]
 
 
+class ParityError(RuntimeError):
+    """a bit-exactness or closed-form check failed: never a timing problem,
+    so the run fails non-zero even when it happens in a secondary leg"""
+
+
+def rh_expected_block_device(world, rank, recvcount, seed0, dev, own=None):
+    """rh_expected_block at the timed size, on the device: block `rank` of
+    every rank's vector (fill_uniform with seed0 + q, regenerated here one
+    vector at a time; `own` = this rank's send buffer, not regenerated) folded
+    in the schedule's association -- the non-power-of-two fold (odd rank
+    2i+1 adds rank 2i), then per step with mask = pof2/2 .. 1 every new rank
+    adds its partner's partial (one IEEE fp32 add each, commutative, so both
+    members of a pair share one sum tensor).  Peak extra memory: one vector
+    and the P blocks."""
+    total = world * recvcount
+
+    def block(q):
+        if q == rank and own is not None:
+            return own[rank * recvcount:(rank + 1) * recvcount].clone()
+        v = torch.empty(total, dtype=torch.float32, device=dev)
+        fill_uniform(v, seed0 + q)
+        b = v[rank * recvcount:(rank + 1) * recvcount].clone()
+        del v
+        return b
+    pof2 = 1
+    while pof2 * 2 <= world:
+        pof2 *= 2
+    rem = world - pof2
+    parts = []
+    for i in range(rem):
+        odd = block(2 * i + 1)
+        odd += block(2 * i)
+        parts.append(odd)
+    parts += [block(r) for r in range(2 * rem, world)]
+    m = pof2 // 2
+    while m:
+        for q in range(pof2):
+            if q < q ^ m:
+                t = parts[q] + parts[q ^ m]
+                parts[q] = parts[q ^ m] = t
+        m //= 2
+    owner = rank // 2 if rank < 2 * rem else rank - rem
+    out = parts[owner]
+    del parts
+    torch.cuda.empty_cache()
+    return out
+
+
+def bits_equal_all_ranks(got, want, dev):
+    """torch.equal on the int32 view (NaN payloads and -0 included), MIN over ranks"""
+    same = bool(torch.equal(got.view(torch.int32), want.view(torch.int32)))
+    return allreduce_scalar(1.0 if same else 0.0, dist.ReduceOp.MIN, dev) == 1.0
+
+
 def rsb_inputs_host(r, P, recvcount):
     return np.random.default_rng(0x5EED0100 + r).uniform(-1, 1, P * recvcount).astype(np.float32)
 
@@ -1130,8 +1223,8 @@ def multi_gpu(args, world, rank, dev):
                 raise RuntimeError('value leg: recursive halving requested, ' + sched['error'])
             ok = dr.cpu().numpy().tobytes() == expected
             if allreduce_scalar(1.0 if ok else 0.0, dist.ReduceOp.MIN, dev) != 1.0:
-                raise RuntimeError('recursive-halving RSB differs from the reference association '
-                                   '(fp32 SUM, recvcount %d, combine overlap %s) on some rank'
+                raise ParityError('recursive-halving RSB differs from the reference association '
+                                  '(fp32 SUM, recvcount %d, combine overlap %s) on some rank'
                                    % (rc_small, 'on every half-step' if mode else 'off'))
     finally:
         cc.set_rh_overlap(shipped_overlap)
@@ -1160,6 +1253,20 @@ def multi_gpu(args, world, rank, dev):
     torch.cuda.synchronize()
     dist.barrier()
     t = allreduce_scalar(time.perf_counter() - t0, dist.ReduceOp.MAX, dev) / args.steps
+    # the timed calls' own result, at the timed size, on every rank (VERDICT
+    # r05 item 1): `send` never changes, so `recv` holds one call's block;
+    # it must equal the recursive-halving association of every rank's seeded
+    # vector regenerated on the device (…recursive_halving.c:164-229)
+    progress(rank, 'value leg: full-size bit check')
+    if os.environ.get('MPIX_BENCH_FAULT_RANK') == str(rank):
+        # test hook (tests/test_bench_gpu.py): one flipped bit in this rank's
+        # timed result must fail the run with EXIT_PARITY
+        recv[recvcount // 2:recvcount // 2 + 1].view(torch.int32).bitwise_xor_(1)
+    expected = rh_expected_block_device(world, rank, recvcount, 0x5EED0100, dev, own=send)
+    if not bits_equal_all_ranks(recv, expected, dev):
+        raise ParityError('the timed recursive-halving RSB result differs from the reference '
+                          'association at the timed size (fp32 SUM, recvcount %d) on some rank'
+                          % recvcount)
     busbytes = (world - 1) / world * total * 4
     pof2 = 1
     while pof2 * 2 <= world:
@@ -1176,7 +1283,14 @@ def multi_gpu(args, world, rank, dev):
     cc.set_rh_overlap(shipped_overlap)
     steps = cc.step_times()
     progress(rank, 'value leg: defaults A/B')
-    ab = None if args.no_ab else defaults_ab(cc, step, recv, dev, args.ab_reps, args.ab_rounds)
+    if not bits_equal_all_ranks(recv, expected, dev):
+        raise ParityError('recursive-halving RSB with the combine overlap off differs from the '
+                          'reference association at the timed size on some rank')
+    ab = None if args.no_ab else defaults_ab(cc, step, recv, expected, dev, args.ab_reps,
+                                             args.ab_rounds)
+    del expected
+    progress(rank, 'value leg: CPU baseline (the reference schedule\'s host work)')
+    cpu = None if args.no_cpu_baseline else rsb_cpu_baseline(world, rank, recvcount, dev)
     comb_ms = sum(s['ms'] for s in steps if s['phase'] == 'combine')
     exch_ms = sum(s['ms'] for s in steps if s['phase'] == 'exchange')
     combined = (pof2 - 1) / pof2 * total            # elements this rank combined (pof2 ranks)
@@ -1190,7 +1304,16 @@ def multi_gpu(args, world, rank, dev):
                 'parallelism': 'rsb%d (one rank per GPU, libmpix_coll over RCCL)' % world},
         parity=dict(checked=True, recvcount=rc_small, bit_exact_all_ranks=True,
                     combine_overlap_checked=['every half-step split', 'none split'],
-                    against='numpy restatement of the recursive-halving association'),
+                    against='numpy restatement of the recursive-halving association',
+                    full_size_bit_exact_all_ranks=True, full_size_recvcount=recvcount,
+                    full_size_checked=['the timed calls\' result (shipped overlap %s)'
+                                       % ('on' if shipped_overlap else 'off'),
+                                       'the step-timing call (overlap off)'] +
+                                      (['every defaults_ab variant'] if ab else []),
+                    full_size_against='the recursive-halving association of every rank\'s '
+                                      'seeded vector regenerated on the device '
+                                      '(bench.rh_expected_block_device), torch.equal on the '
+                                      'int32 view, MIN over ranks'),
         schedule_ran=sched['schedule_ran'],
         combine_overlap=overlap_note(shipped_overlap),
         roofline={'bound': 'hbm', 'unit': 'GB/s',
@@ -1207,28 +1330,110 @@ def multi_gpu(args, world, rank, dev):
         steps_rank0=steps,
         step_split_rank0=dict(exchange_ms=round(exch_ms, 3), combine_ms=round(comb_ms, 3)),
         defaults_ab=ab)
+    if cpu is not None:
+        result['cpu_baseline'] = dict(value=round(busbytes / cpu.pop('value_s') / 1e9, 3), **cpu)
     del send, recv, ws
     torch.cuda.empty_cache()
     return result
+
+
+def host_memory_budget():
+    """bytes this node's ranks may still take: MemAvailable, and the cgroup's
+    memory.max less its current use when one is set"""
+    avail = None
+    try:
+        for line in open('/proc/meminfo'):
+            if line.startswith('MemAvailable:'):
+                avail = int(line.split()[1]) * 1024
+                break
+    except (OSError, ValueError):
+        pass
+    try:
+        mx = open('/sys/fs/cgroup/memory.max').read().strip()
+        if mx != 'max':
+            cur = int(open('/sys/fs/cgroup/memory.current').read())
+            left = int(mx) - cur
+            avail = left if avail is None else min(avail, left)
+    except (OSError, ValueError):
+        pass
+    return avail
+
+
+def rsb_cpu_baseline(world, rank, recvcount, dev, reps=3):
+    """The N > 1 line's CPU baseline:
+    the reference's own host work for this collective -- recursive halving
+    keeps the vector in host temporaries (…recursive_halving.c:80-88), copies
+    the send buffer in (:91-96), combines each step's received half with
+    MPIR_Reduce_local (:219-221; log2(P) combines of n/2, n/4, ... elements)
+    and copies its block out (:232-235) -- timed with the oracle's op_fns.c
+    loop (oracle/host_bench.c oracle_bench_rsb_rank) on one pinned core per
+    rank, all ranks at once between barriers, the max over ranks.  The
+    exchange is not the CPU's work and is not in it, so `value` (bus bytes /
+    that time, GB/s) is the most the reference's CPU path could reach with a
+    free network.  When the node's host memory cannot hold every rank's
+    three full-size host vectors the sample is scaled down by a power of two
+    and the times scaled back up (the work is linear streams); `sample` says
+    which."""
+    from oracle import oracle as orc
+    orc.build()
+    topo = host_topology()
+    phys = topo['physical']
+    cpu = phys[rank % len(phys)]
+    total = world * recvcount
+    need = world * (3 * total + recvcount) * 4
+    budget = host_memory_budget()
+    scale = 1
+    while budget is not None and need // scale > 0.6 * budget and recvcount // (2 * scale) >= 1024:
+        scale *= 2
+    scale = int(allreduce_scalar(float(scale), dist.ReduceOp.MAX, dev))
+    rc = recvcount // scale
+    dist.barrier()
+    r = orc.bench_rsb_rank(rc, world, rank, cpu, reps, H.MPI_FLOAT, H.MPI_SUM)
+    dist.barrier()
+    worst = {k: allreduce_scalar(r[k] * scale, dist.ReduceOp.MAX, dev)
+             for k in ('copy_in_s', 'combine_s', 'copy_out_s', 'total_s')}
+    comb = r['combined_elements'] * scale
+    return dict(
+        value_s=worst['total_s'], unit='GB/s', cores=world, kind='port',
+        cores_per_rank=1,
+        sample='MPICH recursive-halving reduce-scatter-block host work per rank (copy in, the '
+               'log2(P) MPIR_Reduce_local combines through oracle/redop_oracle.c, copy out) on '
+               '%s fp32 per rank, one pinned core per rank, all %d ranks at once, median of %d '
+               'calls per rank, max over ranks%s'
+               % ('%d x %d' % (world, rc), world, reps,
+                  '' if scale == 1 else '; 1/%d of the timed vector (host memory), times x %d'
+                  % (scale, scale)),
+        ms_per_call=round(worst['total_s'] * 1e3, 3),
+        copy_in_ms=round(worst['copy_in_s'] * 1e3, 3),
+        combine_ms=round(worst['combine_s'] * 1e3, 3),
+        copy_out_ms=round(worst['copy_out_s'] * 1e3, 3),
+        combined_elements_per_rank=comb,
+        combine_GiBs_rank=round(3 * comb * 4 / GIB / (r['combine_s'] * scale), 3)
+        if r['combine_s'] > 0 else None,
+        scaled_down_by=scale, host_cpu=topo['model'], nproc=os.cpu_count(),
+        affinity_cpus=len(topo['affinity']), physical_cores=len(phys), sockets=topo['sockets'],
+        cgroup_cpu_quota=topo['cgroup_cpu_quota'],
+        note='value = (P-1)/P x vector bytes / the slowest rank\'s host call time: the bus '
+             'bandwidth MPICH\'s CPU schedule could not exceed even with a free network')
 
 
 AB_VARIANTS = ('overlap_on_policy_on', 'overlap_off_policy_on', 'overlap_on_policy_off',
                'overlap_off_policy_off')
 
 
-def defaults_ab(cc, step, recv, dev, reps=3, rounds=2):
+def defaults_ab(cc, step, recv, expected, dev, reps=3, rounds=2):
     """The value leg's two defaults that no earlier run could measure, timed
     against their alternatives on the same buffers, interleaved: the
     recursive-halving combine overlap (1 MiB half-steps and up, the RCCL
     communicators' default, vs off) x libmpix_redop's store policy (the
     default XCD write-through mask vs all non-temporal stores).  Every variant
     first runs one untimed call whose result must equal, bit for bit on every
-    rank, the result of the shipped default's timed calls (same association,
-    so the same bits); then `reps` calls between barrier + synchronize, max
+    rank, `expected` -- the reference association regenerated on the device
+    (rh_expected_block_device), not the shipped default's own output; then
+    `reps` calls between barrier + synchronize, max
     over ranks.  `rounds` passes, the order rotated each pass; ms_per_step is
     the median over the passes.  The line's `value` stays on the shipped
     default; this only says whether the defaults gain or cost."""
-    ref = recv.clone()
     torch.cuda.synchronize()
     shipped_overlap = cc.rh_overlap()
     pol = redop.get_store_policy()
@@ -1247,10 +1452,9 @@ def defaults_ab(cc, step, recv, dev, reps=3, rounds=2):
                 recv.fill_(float('nan'))
                 step()
                 torch.cuda.synchronize()
-                same = bool(torch.equal(recv.view(torch.int32), ref.view(torch.int32)))
-                if not allreduce_scalar(1.0 if same else 0.0, dist.ReduceOp.MIN, dev):
-                    raise RuntimeError('defaults A/B: %s differs from the shipped default\'s bits '
-                                       'on some rank' % name)
+                if not bits_equal_all_ranks(recv, expected, dev):
+                    raise ParityError('defaults A/B: %s differs from the reference association '
+                                      'at the timed size on some rank' % name)
                 parity[name] = True
                 dist.barrier()
                 torch.cuda.synchronize()
@@ -1268,7 +1472,7 @@ def defaults_ab(cc, step, recv, dev, reps=3, rounds=2):
                          'policy_on' if pol['xcd_mask'] > 0 else 'policy_off')
     out = {k: dict(ms_per_step=round(1e3 * float(np.median(v)), 4),
                    ms_each_round=[round(1e3 * x, 4) for x in v],
-                   bit_identical_to_shipped_all_ranks=parity.get(k, False))
+                   bit_exact_vs_association_all_ranks=parity.get(k, False))
            for k, v in times.items()}
     best = min(AB_VARIANTS, key=lambda k: out[k]['ms_per_step'])
     out.update(shipped=shipped, fastest=best, reps=reps, rounds=rounds,
@@ -1337,7 +1541,7 @@ def rsb_secondary(args, world, rank, dev, out):
         ok = allreduce_scalar(1 if bool(torch.all(o == world * rank + world * (world - 1) // 2))
                               else 0, dist.ReduceOp.MIN, dev)
         if not ok:
-            raise RuntimeError('%s RSB fails the redscatblk3 closed form' % algo)
+            raise ParityError('%s RSB fails the redscatblk3 closed form' % algo)
 
         def once():
             redop.check(ccl.reduce_scatter_block(src, recv, recvcount, H.MPI_FLOAT, H.MPI_SUM, cc,
@@ -1353,7 +1557,7 @@ def rsb_secondary(args, world, rank, dev, out):
         elif name in same_as:
             same = bool(torch.equal(recv.view(torch.int32), refs[same_as[name]].view(torch.int32)))
             if not allreduce_scalar(1 if same else 0, dist.ReduceOp.MIN, dev):
-                raise RuntimeError('%s RSB differs from %s at the timed size' % (name, same_as[name]))
+                raise ParityError('%s RSB differs from %s at the timed size' % (name, same_as[name]))
             bits = same_as[name]
         reps = max(3, min(10, args.steps))
         dist.barrier()
@@ -1407,7 +1611,7 @@ def allreduce_secondary(args, world, rank, dev, res):
     redop.check(ccl.allreduce(x, y, m, H.MPI_INT, H.MPI_SUM, cc, 'reduce_scatter_allgather'),
                 'MPIX_Allreduce')
     if not allreduce_scalar(1 if bool(torch.all(y == x * world)) else 0, dist.ReduceOp.MIN, dev):
-        raise RuntimeError('allreduce fails the allred.c sum_test_1 closed form')
+        raise ParityError('allreduce fails the allred.c sum_test_1 closed form')
     n = min(1 << 28, args.rsb_bytes // 4)          # 1 GiB per rank at the default size
     send = torch.empty(n, dtype=torch.float32, device=dev)
     fill_uniform(send, 0x5EED0200 + rank)
@@ -1456,7 +1660,7 @@ def allreduce_secondary(args, world, rank, dev, res):
             got = sh_out if name == 'c_pull_shared' else recv
             same = bool(torch.equal(got.view(torch.int32), ref.view(torch.int32)))
             if not allreduce_scalar(1 if same else 0, dist.ReduceOp.MIN, dev):
-                raise RuntimeError('%s allreduce differs from reduce_scatter_allgather' % name)
+                raise ParityError('%s allreduce differs from reduce_scatter_allgather' % name)
             res['%s_bit_identical_all_ranks' % name[2:]] = True
         reps = max(3, min(10, args.steps))
         dist.barrier()
@@ -1523,6 +1727,29 @@ def _watchdog(seconds, emit, note=True, code=0):
     t.daemon = True
     t.start()
     return t
+
+
+def run_secondary(result, legs):
+    """Run the secondary legs ((key, fn(part)) pairs) in order into
+    result[key], stopping at the first that raises (the peers may be stuck
+    in that leg: no further collective).  Returns (failure or None, exit
+    code): an exception or timing trouble in an extra keeps the checked
+    value and exits 0 (`extras_error`); a ParityError -- a wrong result is
+    never an extra -- also sets the top-level `error` and exits
+    EXIT_PARITY."""
+    for key, fn in legs:
+        part = result[key] = {}
+        try:
+            fn(part)
+        except Exception as e:
+            part['error'] = '%s: %s' % (type(e).__name__, e)
+            failed = '%s: %s' % (key, part['error'])
+            result['extras_error'] = failed
+            if isinstance(e, ParityError):
+                result['error'] = 'secondary leg failed its parity check: ' + failed
+                return failed, EXIT_PARITY
+            return failed, 0
+    return None, 0
 
 
 def world_plan(args, env=None):
@@ -1652,22 +1879,34 @@ def launch_ranks(n, argv):
     return 0
 
 
-def dry_run(world, rank):
+def dry_run(world, rank, args=None):
     """the launch path without a GPU: ranks rendezvous over gloo, count
-    themselves with an all-reduce, and rank 0 prints the line's skeleton"""
+    themselves with an all-reduce, run the N > 1 line's CPU baseline (the
+    reference schedule's host work, unless --no-cpu-baseline) and rank 0
+    prints the line's skeleton"""
     seen = 1
+    cpu = None
     if world > 1:
         dist.init_process_group('gloo')
         t = torch.ones(1)
         dist.all_reduce(t)
         seen = int(t.item())
         dist.barrier()
+        if args is not None and not args.no_cpu_baseline:
+            total = (args.rsb_bytes // 4) // world * world
+            cpu = rsb_cpu_baseline(world, rank, total // world, None)
+            cpu = dict(value=round((world - 1) / world * total * 4 / cpu.pop('value_s') / 1e9, 3),
+                       **cpu)
     if rank == 0:
-        print(json.dumps({'metric': METRIC_RSB if world > 1 else METRIC, 'value': None,
-                          'n_gpus': world, 'ranks_seen': seen, 'dry_run': True,
-                          'defaults_ab': ({k: None for k in AB_VARIANTS} if world > 1 else None),
-                          'launcher': 'bench.py' if os.environ.get('MPIX_BENCH_LAUNCHED')
-                          else ('external' if world > 1 else None)}), flush=True)
+        line = {'metric': METRIC_RSB if world > 1 else METRIC, 'value': None,
+                'n_gpus': world, 'ranks_seen': seen, 'dry_run': True,
+                'defaults_ab': ({k: None for k in AB_VARIANTS} if world > 1 else None),
+                'launcher': 'bench.py' if os.environ.get('MPIX_BENCH_LAUNCHED')
+                else ('external' if world > 1 else None)}
+        if world > 1:
+            line['parity'] = {'full_size_bit_exact_all_ranks': None}
+            line['cpu_baseline'] = cpu
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
     return 0 if seen == world else 1
@@ -1684,7 +1923,7 @@ def main(argv=None):
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     if args.dry_run:
-        return dry_run(world, rank)
+        return dry_run(world, rank, args)
     # rehearsal knobs for a 1-GPU box (never set by the driver): every rank on
     # device 0 and a gloo control plane + transport; RCCL refuses two ranks on
     # one device (profiles/r01_rccl_probe.txt)
@@ -1715,7 +1954,7 @@ def main(argv=None):
         first.result = dict(failed_line, error='%s: %s' % (type(e).__name__, e))
         first.emit()
         sys.stdout.flush()
-        os._exit(1)
+        os._exit(EXIT_PARITY if isinstance(e, ParityError) else 1)
     dog0.cancel()
     with first.lock:            # the watchdog fired meanwhile: its line stands
         if first.done:
@@ -1724,29 +1963,16 @@ def main(argv=None):
     emit = _Emitter(rank, result)
     dog = _watchdog(args.extras_timeout, emit)
     result['extras_timeout_s'] = args.extras_timeout
-    failed = None
-    if not args.no_extras:
-        for key, fn in (('reduce_scatter_block_other', rsb_secondary),
-                        ('allreduce', allreduce_secondary)):
-            part = result[key] = {}
-            try:
-                fn(args, world, rank, dev, part)
-            except Exception as e:
-                part['error'] = '%s: %s' % (type(e).__name__, e)
-                failed = '%s: %s' % (key, part['error'])
-                break       # the peers may be stuck in that leg: stop issuing collectives
-    if failed:
-        # a secondary leg failed (its error is in its part of the line): the
-        # value leg passed its parity gate and was timed, so the line stands
-        # and the run succeeds; the peers may be stuck in that leg, so no
-        # teardown collective follows
-        result['extras_error'] = failed
+    failed, code = (None, 0) if args.no_extras else run_secondary(
+        result, ((k, lambda part, fn=fn: fn(args, world, rank, dev, part))
+                 for k, fn in (('reduce_scatter_block_other', rsb_secondary),
+                               ('allreduce', allreduce_secondary))))
     emit.emit()
     if failed:
         sys.stdout.flush()
         sys.stderr.write('bench.py: secondary leg failed: %s\n' % failed)
         sys.stderr.flush()
-        os._exit(0)
+        os._exit(code)
     dist.barrier()
     if dist.get_backend() == 'nccl':
         _CCL.pop('comm').free()

@@ -240,6 +240,38 @@ def bench_reduce(count, datatype, op, cpus, seconds):
                   float(seconds))
 
 
+def bench_pair(count, datatype, op, cpus, seconds):
+    """MPI_Reduce_local(datatype, op) and the host triad in the same passes
+    (host_bench.c oracle_bench_pair): (reduce best, reduce median, passes,
+    span, triad best, triad median, median per-pass reduce / triad time)"""
+    L = lib()
+    arr = (ctypes.c_int * len(cpus))(*cpus)
+    best, med, passes, span = ctypes.c_double(), ctypes.c_double(), ctypes.c_int(), \
+        ctypes.c_double()
+    pair = (ctypes.c_double * 3)()
+    rc = L.oracle_bench_pair(ctypes.c_long(count), _i32(datatype), _i32(op), len(cpus), arr,
+                             ctypes.c_double(seconds), ctypes.byref(best), ctypes.byref(med),
+                             ctypes.byref(passes), ctypes.byref(span), pair)
+    if rc:
+        raise RuntimeError('host bench failed (%d)' % rc)
+    return best.value, med.value, passes.value, span.value, pair[0], pair[1], pair[2]
+
+
+def bench_rsb_rank(recvcount, P, rank, cpu, reps, datatype, op):
+    """one rank's host work in MPICH's recursive-halving reduce-scatter-block
+    (copy in, the log2(P) combines, copy out) on one pinned core
+    (host_bench.c oracle_bench_rsb_rank): dict of median seconds and the
+    elements combined per call"""
+    L = lib()
+    out = (ctypes.c_double * 5)()
+    rc = L.oracle_bench_rsb_rank(ctypes.c_long(recvcount), int(P), int(rank), int(cpu), int(reps),
+                                 _i32(datatype), _i32(op), out)
+    if rc:
+        raise RuntimeError('host RSB bench failed (%d)' % rc)
+    return dict(copy_in_s=out[0], combine_s=out[1], copy_out_s=out[2], total_s=out[3],
+                combined_elements=int(out[4]))
+
+
 def bench_triad(count, cpus, seconds):
     """host STREAM triad on `count` fp32 (12 bytes each) over pinned threads"""
     arr = (ctypes.c_int * len(cpus))(*cpus)

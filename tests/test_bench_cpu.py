@@ -355,3 +355,115 @@ def test_launcher_counts_devices_in_a_child(monkeypatch):
     with pytest.raises(SystemExit):
         bench.check_devices(2, {})
     bench.check_devices(4, {'MPIX_BENCH_SAME_DEVICE': '1'})
+
+
+# ------------------------------------------------- round 6
+@pytest.mark.parametrize('world', [2, 3, 4, 8])
+def test_rh_expected_block_device_matches_numpy_restatement(world):
+    """the full-size check's expected block (built with torch, on the device
+    in the bench; here on the CPU, same generator calls) equals the numpy
+    restatement the parity gate uses, itself pinned to the oracle above"""
+    import torch
+    import bench
+    rc = 1031
+    sends = []
+    for r in range(world):
+        v = torch.empty(world * rc, dtype=torch.float32)
+        bench.fill_uniform(v, 0x5EED0100 + r)
+        sends.append(v.numpy().copy())
+    own = torch.from_numpy(sends[1].copy())
+    for r in range(world):
+        got = bench.rh_expected_block_device(world, r, rc, 0x5EED0100, 'cpu',
+                                             own=own if r == 1 else None)
+        assert got.numpy().tobytes() == bench.rh_expected_block(sends, r, rc).tobytes(), r
+
+
+def test_secondary_parity_failure_fails_the_run():
+    """a secondary leg whose closed form / bit check fails sets
+    the top-level error and exits EXIT_PARITY; an ordinary exception in an
+    extra keeps the value (exit 0); later legs do not run after a failure"""
+    import bench
+    ran = []
+
+    def ok(part):
+        ran.append('ok')
+        part['ms'] = 1.0
+
+    def bad_bits(part):
+        raise bench.ParityError('pairwise RSB differs from the oracle')
+
+    def boom(part):
+        raise RuntimeError('timed out')
+
+    r = {'value': 1.0}
+    failed, code = bench.run_secondary(r, [('a', ok), ('b', bad_bits), ('c', ok)])
+    assert code == bench.EXIT_PARITY != 0 and 'parity' in r['error'] and 'b' in failed
+    assert ran == ['ok'] and 'c' not in r and r['value'] == 1.0
+    r = {'value': 1.0}
+    failed, code = bench.run_secondary(r, [('a', boom), ('b', ok)])
+    assert code == 0 and 'error' not in r and r['extras_error'].startswith('a:')
+    r = {'value': 1.0}
+    assert bench.run_secondary(r, [('a', ok), ('b', ok)]) == (None, 0)
+    assert 'extras_error' not in r
+
+
+@pytest.mark.parametrize('launch', ['bench', 'torchrun'])
+def test_dry_run_line_carries_the_rsb_cpu_baseline(launch):
+    """the N > 1 line carries a cpu_baseline -- MPICH's
+    recursive-halving host work (copy in, log2(P) combines through the oracle
+    loop, copy out) on one pinned core per rank, max over ranks"""
+    import json
+    args = ['--gpus', '2', '--dry-run', '--no-extras', '--rsb-bytes', str(16 << 20)]
+    p = _bench(args) if launch == 'bench' else _torchrun(2, args)
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith('{')][0])
+    c = d['cpu_baseline']
+    assert c['kind'] == 'port' and c['unit'] == 'GB/s' and c['cores'] == 2, c
+    assert c['value'] > 0 and c['ms_per_call'] > 0 and c['combine_ms'] > 0, c
+    assert c['combined_elements_per_rank'] == (16 << 20) // 4 // 2, c     # P = 2: half the vector
+    assert 'full_size_bit_exact_all_ranks' in d['parity'], d
+
+
+@pytest.mark.parametrize('P', [2, 3, 4, 5, 8])
+def test_rsb_host_work_combines_what_the_schedule_combines(oracle, P):
+    """oracle_bench_rsb_rank runs the reference's index arithmetic: a rank of a
+    power-of-two world combines (P-1)/P of the vector; with rem = P - pof2
+    the odd ranks below 2 rem also fold the whole vector first and the even
+    ones combine nothing"""
+    from oracle import oracle as orc
+    rc = 4096
+    pof2 = 1
+    while pof2 * 2 <= P:
+        pof2 *= 2
+    rem = P - pof2
+    for r in range(P):
+        got = orc.bench_rsb_rank(rc, P, r, -1, 1, 0x4c00040a, 0x58000003)['combined_elements']
+        if r < 2 * rem and r % 2 == 0:
+            want = 0
+        else:
+            nr = r // 2 if r < 2 * rem else r - rem
+            cnts = [2 * rc if (i * 2 + 1 if i < rem else i + rem) < 2 * rem else rc
+                    for i in range(pof2)]
+            want = P * rc if r < 2 * rem else 0
+            lo, hi, m = 0, pof2, pof2 // 2
+            while m:            # the half of [lo, hi) that stays with nr
+                if nr < (nr ^ m):
+                    hi = lo + m
+                else:
+                    lo = lo + m
+                want += sum(cnts[lo:hi])
+                m //= 2
+        assert got == want, (P, r, got, want)
+
+
+def test_cpu_baseline_reads_reduce_and_triad_from_the_same_passes(oracle):
+    """the host-triad denominator is timed in the same
+    passes as the reduce (same threads, slices and quota windows); the line
+    carries both the ratio of medians and the median per-pass ratio"""
+    import bench
+    c = bench.cpu_baseline(1.0, 1 << 22, None)
+    for k in ('frac_of_host_triad_1core', 'frac_of_host_triad_1core_per_pass',
+              'host_triad_1core_gibs', 'host_triad_timing'):
+        assert k in c, k
+    assert 'frac_of_host_triad_per_pass' in c['allcores']
+    assert 0 < c['frac_of_host_triad_1core'] < 3 and 0 < c['allcores']['frac_of_host_triad'] < 3

@@ -22,7 +22,7 @@ def test_bench_gpus_2_self_launched_line():
     env.update(MPIX_BENCH_SAME_DEVICE='1', MPIX_BENCH_BACKEND='gloo')
     p = subprocess.run([sys.executable, os.path.join(ROOT, 'bench.py'), '--gpus', '2',
                         '--steps', '2', '--warmup', '1', '--count', str(1 << 22),
-                        '--rsb-bytes', str(16 << 20), '--no-extras', '--no-cpu-baseline'],
+                        '--rsb-bytes', str(16 << 20), '--no-extras'],
                        cwd=ROOT, capture_output=True, text=True, timeout=100, env=env)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith('{')]
@@ -30,12 +30,38 @@ def test_bench_gpus_2_self_launched_line():
     d = json.loads(lines[0])
     assert d['n_gpus'] == 2 and d['schedule_ran'] == 'recursive_halving', d
     assert d['parity']['bit_exact_all_ranks'] and d['value'] > 0, d
-    # the overlap x store-policy defaults timed beside the
-    # shipped one, every variant first bit-identical on every rank
+    # the timed result itself, at the timed size, on every rank
+    assert d['parity']['full_size_bit_exact_all_ranks'], d['parity']
+    assert d['parity']['full_size_recvcount'] == (16 << 20) // 4 // 2, d['parity']
+    # the overlap x store-policy defaults
+    # timed beside the shipped one, every variant first bit-exact on every
+    # rank against the association (not against the default's own output)
     ab = d['defaults_ab']
     for k in ('overlap_on_policy_on', 'overlap_off_policy_on', 'overlap_on_policy_off',
               'overlap_off_policy_off'):
-        assert ab[k]['bit_identical_to_shipped_all_ranks'] and ab[k]['ms_per_step'] > 0, ab
+        assert ab[k]['bit_exact_vs_association_all_ranks'] and ab[k]['ms_per_step'] > 0, ab
+    # the reference schedule's host work as the baseline
+    c = d['cpu_baseline']
+    assert c['kind'] == 'port' and c['cores'] == 2 and c['value'] > 0, c
+
+
+@pytest.mark.gpu
+def test_bench_full_size_check_catches_a_flipped_bit():
+    """the full-size check is live: one bit flipped in rank 1's timed result
+    (MPIX_BENCH_FAULT_RANK, a test hook) fails the run with EXIT_PARITY and a
+    top-level error naming the timed size"""
+    sys.path.insert(0, ROOT)
+    import bench
+    env = {k: v for k, v in os.environ.items()
+           if k not in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_PORT')}
+    env.update(MPIX_BENCH_SAME_DEVICE='1', MPIX_BENCH_BACKEND='gloo', MPIX_BENCH_FAULT_RANK='1')
+    p = subprocess.run([sys.executable, os.path.join(ROOT, 'bench.py'), '--gpus', '2',
+                        '--steps', '2', '--warmup', '1', '--count', str(1 << 22),
+                        '--rsb-bytes', str(16 << 20), '--no-extras', '--no-cpu-baseline',
+                        '--no-ab'], cwd=ROOT, capture_output=True, text=True, timeout=100, env=env)
+    assert p.returncode == bench.EXIT_PARITY, (p.returncode, p.stderr[-3000:])
+    d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith('{')][0])
+    assert d['value'] is None and 'timed size' in d['error'], d
 
 
 @pytest.mark.gpu
@@ -64,4 +90,5 @@ def test_bench_gpus_2_under_torchrun_line():
     assert d['schedule_ran'] == 'recursive_halving' and d['parity']['bit_exact_all_ranks'], d
     for k in ('overlap_on_policy_on', 'overlap_off_policy_on', 'overlap_on_policy_off',
               'overlap_off_policy_off'):
-        assert d['defaults_ab'][k]['bit_identical_to_shipped_all_ranks'], d['defaults_ab']
+        assert d['defaults_ab'][k]['bit_exact_vs_association_all_ranks'], d['defaults_ab']
+    assert d['parity']['full_size_bit_exact_all_ranks'], d['parity']
