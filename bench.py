@@ -537,12 +537,25 @@ def reduce_local_leg(args, world, rank, dev):
     kreps = max(10, min(args.steps, 50))
     call = lambda: redop.check(redop.reduce_local_async(inb, inout, n, H.MPI_FLOAT, H.MPI_SUM,  # noqa
                                                          stream))
-    # the kernel as the timed loop runs it: each launch from an idle GPU
-    k_avg, k_med, k_min = isolated_event_time(call, 3 * kreps, stream)
-    # and back to back (a stream-ordered caller's steady state)
+    # the kernel as the timed loop runs it: each launch from an idle GPU, with
+    # the synchronous entry's store policy (its own XCD mask since round 6)
+    pol = redop.get_store_policy()
+    sync_mask = redop.get_sync_store_policy()
+    redop.check(redop.set_store_policy(sync_mask, pol['every'], pol['phase'], pol['tail_blocks']))
+    try:
+        k_avg, k_med, k_min = isolated_event_time(call, 3 * kreps, stream)
+    finally:
+        # back to the default (-1) unless the environment fixed a mask: an
+        # explicit mask would become the synchronous entry's too
+        env_mask = os.environ.get('MPIX_REDOP_WT_XCD')
+        redop.check(redop.set_store_policy(-1 if env_mask is None else pol['xcd_mask'],
+                                           pol['every'], pol['phase'], pol['tail_blocks']))
+    # and back to back with the stream-ordered entries' policy (a
+    # stream-ordered caller's steady state)
     b_avg, b_med, b_min = event_time_per_launch(call, kreps, stream)
     return dict(t=t, k_avg=k_avg, k_med=k_med, k_min=k_min, kreps=kreps, inb=inb, inout=inout,
-                stream=stream, b_avg=b_avg, b_med=b_med, b_min=b_min)
+                stream=stream, b_avg=b_avg, b_med=b_med, b_min=b_min, sync_mask=sync_mask,
+                async_mask=redop.get_store_policy()['xcd_mask'])
 
 
 def single_gpu(args, dev):
@@ -571,6 +584,8 @@ def single_gpu(args, dev):
             'count': n, 'bytes_per_operand': 4 * n, 'algorithmic_bytes_per_step': nbytes_alg,
             'parallelism': 'single GPU',
             'launch': redop.get_launch(),
+            'store_policy_xcd_mask': {'synchronous_entry': leg['sync_mask'],
+                                      'stream_ordered_entries': leg['async_mask']},
         },
         'roofline': {
             'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
@@ -584,15 +599,16 @@ def single_gpu(args, dev):
             'kernel_timing': 'HIP events around each launch on its stream, every launch started '
                              'from an idle GPU as in the timed synchronous loop (a short spin '
                              'kernel holds the stream while the events and the launch are '
-                             'enqueued)',
+                             'enqueued), with the synchronous entry\'s store policy',
             'algorithmic_bytes_per_launch': nbytes_alg,
             'back_to_back': {'kernel_ms_avg': round(leg['b_avg'], 4),
                              'achieved': round(nbytes_alg / (leg['b_avg'] * 1e-3) / 1e9, 1),
                              'frac': round(nbytes_alg / (leg['b_avg'] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                              'launches': 3 * kreps,
                              'note': 'one event pair around batches of launches issued back to '
-                                     'back (a stream-ordered caller); an idle-start launch runs '
-                                     'longer with the one-wave blocks (DESIGN.md §8)'},
+                                     'back (a stream-ordered caller, with the stream-ordered '
+                                     'entries\' store policy); an idle-start launch runs longer '
+                                     'with the one-wave blocks (DESIGN.md §8)'},
         },
     }
     if traced and traced.get('avg_duration_ns'):
@@ -1467,7 +1483,8 @@ def defaults_ab(cc, step, recv, expected, dev, reps=3, rounds=2):
                                                     dev) / reps)
     finally:
         cc.set_rh_overlap(shipped_overlap)
-        redop.set_store_policy(pol['xcd_mask'], pol['every'], pol['phase'], pol['tail_blocks'])
+        redop.set_store_policy(-1 if os.environ.get('MPIX_REDOP_WT_XCD') is None
+                               else pol['xcd_mask'], pol['every'], pol['phase'], pol['tail_blocks'])
     shipped = '%s_%s' % ('overlap_on' if shipped_overlap else 'overlap_off',
                          'policy_on' if pol['xcd_mask'] > 0 else 'policy_off')
     out = {k: dict(ms_per_step=round(1e3 * float(np.median(v)), 4),

@@ -409,6 +409,17 @@ int MPIX_Redop_get_launch(int *block_threads, int *unroll, int *max_grid);
 int MPIX_Redop_set_store_policy(int xcd_mask, int every, int phase, int tail_blocks);
 int MPIX_Redop_get_store_policy(int *xcd_mask, int *every, int *phase, int *tail_blocks);
 
+/* The synchronous entry's own XCD mask (MPIX_Reduce_local on device or
+ * page-locked operands: the MPIR_Reduce_local drop-in, whose kernels start
+ * from an idle GPU call after call).  Default (-1): the mask set with
+ * MPIX_Redop_set_store_policy / MPIX_REDOP_WT_XCD if any, else 0x22 on
+ * 8-XCD devices (XCDs 1 and 5: the faster synchronous call,
+ * profiles/r05_sync_xcd_masks.json), 0 otherwise; env MPIX_REDOP_WT_XCD_SYNC
+ * at first use.  get reports the mask the next synchronous launch uses (-1
+ * while the default is unsettled).  No HIP call. */
+int MPIX_Redop_set_sync_store_policy(int xcd_mask);
+int MPIX_Redop_get_sync_store_policy(int *xcd_mask);
+
 /* ---- large pageable host operands (performance knob) ----
  * threads > 0: pageable operands of at least 2 * chunk_bytes go through that many
  * host threads (the caller is one of them).  Default form, "wave": the

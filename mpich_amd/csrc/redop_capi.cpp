@@ -278,6 +278,15 @@ std::atomic<int> g_zc_grid{kZcAuto};
 // predicates, never start the HIP runtime).
 constexpr int kWtAuto = -1;
 std::atomic<int> g_wt_tail{0}, g_wt_every{0}, g_wt_phase{0}, g_wt_xcd{kWtAuto};
+// The synchronous entry's own mask (MPIX_Redop_set_sync_store_policy, env
+// MPIX_REDOP_WT_XCD_SYNC): MPIX_Reduce_local -- the MPIR_Reduce_local drop-in
+// -- is timed by its callers call by call, each kernel starting from an idle
+// GPU, and there XCDs 1 and 5 writing through (0x22) beat XCDs 3 and 7 (0x88)
+// by 1.7-3.2 % per call on three boxes although the kernel alone is 2 %
+// slower with it (profiles/r05_sync_xcd_masks.json).  The
+// stream-ordered entries, whose kernels run back to back, keep g_wt_xcd.
+// kWtAuto: an explicit g_wt_xcd if one was set, else the sync default.
+std::atomic<int> g_wt_xcd_sync{kWtAuto};
 std::once_flag g_wt_once;
 // completion wait of the synchronous calls: 0 block (hipStreamSynchronize),
 // 1 spin on an event, 2 spin on a pinned host word that a one-workgroup
@@ -366,6 +375,8 @@ void read_env()
         g_wt_phase = g_wt_phase % g_wt_every;
     if (const char *s = getenv("MPIX_REDOP_WT_XCD"))
         g_wt_xcd = (int) (strtol(s, nullptr, 0) & 0xff);
+    if (const char *s = getenv("MPIX_REDOP_WT_XCD_SYNC"))
+        g_wt_xcd_sync = (int) (strtol(s, nullptr, 0) & 0xff);
     if (const char *s = getenv("MPIX_REDOP_MAXGRID"))
         g_max_grid = atoi(s) > 0 ? atoi(s) : 0;
     if (const char *s = getenv("MPIX_REDOP_ZC_GRID"))
@@ -555,8 +566,8 @@ void env()
 // 3 and 7 write through when every visible device has 8 XCDs (SPX), else
 // none.  While g_wt_xcd is kWtAuto (no MPIX_REDOP_WT_XCD, no explicit mask
 // from MPIX_Redop_set_store_policy, or -1 set there) the launches use it.
-std::atomic<int> g_wt_default{kWtAuto};
-int wt_default()
+std::atomic<int> g_wt_default{kWtAuto}, g_wt_sync_default{kWtAuto};
+int wt_default(bool sync = false)
 {
     std::call_once(g_wt_once, [] {
         int ndev = 0;
@@ -568,25 +579,31 @@ int wt_default()
         }
         (void) hipGetLastError();
         g_wt_default = spx ? 0x88 : 0;
+        g_wt_sync_default = spx ? 0x22 : 0;
     });
-    return g_wt_default.load();
+    return sync ? g_wt_sync_default.load() : g_wt_default.load();
 }
 
-// Launch geometry and store policy of a kernel about to be enqueued.
-LaunchCfg launch_cfg()
+// Launch geometry and store policy of a kernel about to be enqueued (sync:
+// for the synchronous entry, g_wt_xcd_sync).
+LaunchCfg launch_cfg(bool zero_copy = false, bool sync = false)
 {
     env();
     int wt = g_wt_xcd.load();
+    if (sync) {
+        const int ws = g_wt_xcd_sync.load();
+        if (ws != kWtAuto)
+            wt = ws;
+        else if (wt == kWtAuto)
+            wt = wt_default(true);
+    }
     if (wt == kWtAuto)
         wt = wt_default();
-    return LaunchCfg{g_block.load(), g_max_grid.load(), g_wt_tail.load(), g_wt_every.load(),
-                     g_wt_phase.load(), wt};
-}
-
-// ... of one whose operand(s) include page-locked host memory (g_zc_grid)
-LaunchCfg launch_cfg(bool zero_copy)
-{
-    LaunchCfg c = launch_cfg();
+    LaunchCfg c{g_block.load(), g_max_grid.load(), g_wt_tail.load(), g_wt_every.load(),
+                g_wt_phase.load(), wt};
+    if (!zero_copy)
+        return c;
+    // ... of one whose operand(s) include page-locked host memory (g_zc_grid)
     int z = g_zc_grid.load();
     if (z == kZcAuto)
         z = kZcLanes / (c.block > 0 ? c.block : 64);
@@ -715,7 +732,7 @@ int validate(const void *in, const void *io, MPIX_Aint count, uint32_t dt, uint3
 // workgroup counter, NULL = one workgroup only).
 int enqueue(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext, uint32_t op,
             hipStream_t s, uint32_t *done = nullptr, uint32_t *ctr = nullptr, uint32_t seq = 0,
-            bool *signalled = nullptr, bool zero_copy = false)
+            bool *signalled = nullptr, bool zero_copy = false, bool sync = false)
 {
     if (signalled)
         *signalled = false;
@@ -734,7 +751,7 @@ int enqueue(const void *in, void *io, uint64_t count, uint32_t it, uint64_t ext,
     prm.done = done;
     prm.done_ctr = ctr;
     prm.done_seq = seq;
-    int rc = hip_err(e->contig(in, io, count, prm, launch_cfg(zero_copy), s));
+    int rc = hip_err(e->contig(in, io, count, prm, launch_cfg(zero_copy, sync), s));
     if (signalled)
         *signalled = done && rc == MPIX_REDOP_SUCCESS;
     return rc;
@@ -754,13 +771,14 @@ int run_sync(DevState *d, const void *in, void *io, uint64_t count, uint32_t it,
         const uint32_t seq = ++d->seq;
         bool signalled = false;
         int rc = enqueue(in, io, count, it, ext, op, d->s[0], (uint32_t *) d->flag, d->flag_ctr,
-                         seq, &signalled, zero_copy);
+                         seq, &signalled, zero_copy, true);
         if (signalled)      // the kernel stores the word itself
             return spin_on_flag(d, d->s[0], seq);
         int rc2 = wait_stream(d, d->s[0]);
         return rc ? rc : rc2;
     }
-    int rc = enqueue(in, io, count, it, ext, op, d->s[0], nullptr, nullptr, 0, nullptr, zero_copy);
+    int rc = enqueue(in, io, count, it, ext, op, d->s[0], nullptr, nullptr, 0, nullptr, zero_copy,
+                     true);
     int rc2 = wait_stream(d, d->s[0]);
     return rc ? rc : rc2;
 }
@@ -2424,6 +2442,27 @@ int MPIX_Redop_set_store_policy(int xcd_mask, int every, int phase, int tail_blo
     g_wt_every = every;
     g_wt_phase = phase;
     g_wt_tail = tail_blocks;
+    return MPIX_REDOP_SUCCESS;
+}
+
+int MPIX_Redop_set_sync_store_policy(int xcd_mask)
+{
+    env();
+    if (xcd_mask < kWtAuto || xcd_mask > 0xff)
+        return MPIX_REDOP_ERR_ARG;
+    g_wt_xcd_sync = xcd_mask;
+    return MPIX_REDOP_SUCCESS;
+}
+
+int MPIX_Redop_get_sync_store_policy(int *xcd_mask)
+{
+    env();
+    if (!xcd_mask)
+        return MPIX_REDOP_ERR_ARG;
+    // as launch_cfg(…, sync = true) resolves it; -1 while the default is
+    // not settled (no launch so far)
+    const int ws = g_wt_xcd_sync.load(), x = g_wt_xcd.load();
+    *xcd_mask = ws != kWtAuto ? ws : x != kWtAuto ? x : g_wt_sync_default.load();
     return MPIX_REDOP_SUCCESS;
 }
 

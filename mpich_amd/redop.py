@@ -75,6 +75,8 @@ def lib():
             'MPIX_Redop_get_launch': ([ctypes.POINTER(i32)] * 3, i32),
             'MPIX_Redop_set_store_policy': ([i32, i32, i32, i32], i32),
             'MPIX_Redop_get_store_policy': ([ctypes.POINTER(i32)] * 4, i32),
+            'MPIX_Redop_set_sync_store_policy': ([i32], i32),
+            'MPIX_Redop_get_sync_store_policy': ([ctypes.POINTER(i32)], i32),
             'MPIX_Redop_set_pageable': ([i32, aint], i32),
             'MPIX_Redop_get_pageable': ([ctypes.POINTER(i32), ctypes.POINTER(aint)], i32),
             'MPIX_Redop_last_error': ([], i32),
@@ -429,6 +431,17 @@ def get_store_policy():
     check(lib().MPIX_Redop_get_store_policy(ctypes.byref(x), ctypes.byref(e), ctypes.byref(p),
                                             ctypes.byref(t)))
     return dict(xcd_mask=x.value, every=e.value, phase=p.value, tail_blocks=t.value)
+
+
+def set_sync_store_policy(xcd_mask=-1):
+    """the synchronous entry's own XCD mask (-1: the default)"""
+    return lib().MPIX_Redop_set_sync_store_policy(xcd_mask)
+
+
+def get_sync_store_policy():
+    x = ctypes.c_int()
+    check(lib().MPIX_Redop_get_sync_store_policy(ctypes.byref(x)))
+    return x.value
 
 
 def error_string(code):

@@ -86,6 +86,10 @@ def test_queries_and_knobs_make_no_hip_call(shim):
         'assert x[0].value == -1, x[0].value          # default not settled before a launch',
         'assert L.MPIX_Redop_set_store_policy(0x81, 0, 0, 0) == 0',
         'assert L.MPIX_Redop_set_store_policy(-1, 0, 0, 0) == 0',
+        'assert L.MPIX_Redop_get_sync_store_policy(ctypes.byref(x[0])) == 0',
+        'assert x[0].value == -1, x[0].value          # sync default unsettled too',
+        'assert L.MPIX_Redop_set_sync_store_policy(0x22) == 0',
+        'assert L.MPIX_Redop_set_sync_store_policy(-1) == 0',
         'assert L.MPIX_Redop_get_support(ctypes.byref(x[0]), *[ctypes.byref(v) for v in y]) == 0',
         'L.MPIX_Redop_set_support.argtypes = [i, a, a, a]',
         'assert L.MPIX_Redop_set_support(x[0], y[0], y[1], y[2]) == 0',

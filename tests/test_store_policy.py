@@ -27,6 +27,32 @@ def test_store_policy_arguments():
                                       old['tail_blocks']) == 0
 
 
+def test_sync_store_policy_resolution():
+    """the synchronous entry has its own mask.  Unset
+    (-1) it follows an explicit MPIX_Redop_set_store_policy mask, else its
+    own default (0x22 on 8-XCD devices, settled at the first launch; -1 until
+    then); set, it wins for the synchronous entry only"""
+    from mpich_amd import redop
+    old = redop.get_store_policy()
+    old_sync = redop.get_sync_store_policy()
+    try:
+        for bad in (-2, 0x100):
+            assert redop.set_sync_store_policy(bad) != 0, bad
+        assert redop.set_sync_store_policy(-1) == 0
+        assert redop.set_store_policy(0x81, 0, 0, 0) == 0
+        assert redop.get_sync_store_policy() == 0x81           # the explicit mask
+        assert redop.set_sync_store_policy(0x22) == 0
+        assert redop.get_sync_store_policy() == 0x22
+        assert redop.get_store_policy()['xcd_mask'] == 0x81    # the others keep theirs
+        assert redop.set_sync_store_policy(-1) == 0
+        assert redop.set_store_policy(-1, 0, 0, 0) == 0
+        assert redop.get_sync_store_policy() in (-1, 0, 0x22)
+    finally:
+        assert redop.set_store_policy(old['xcd_mask'], old['every'], old['phase'],
+                                      old['tail_blocks']) == 0
+        assert redop.set_sync_store_policy(-1 if old_sync in (-1, 0x22) else old_sync) == 0
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize('dtname,opname', [('MPI_FLOAT', 'MPI_SUM'), ('MPI_INT64_T', 'MPI_BXOR'),
                                            ('MPI_2INT', 'MPI_MAXLOC'), ('MPIX_C_FLOAT16', 'MPI_MAX')])
@@ -58,6 +84,9 @@ def test_every_store_policy_same_bits(oracle, dtname, opname):
     try:
         for pol in POLICIES:
             assert redop.set_store_policy(*pol) == 0
+            # the synchronous entry's own mask: the same masks in turn, and
+            # the default (-1) for the first policy
+            assert redop.set_sync_store_policy(pol[0] if pol != POLICIES[0] else -1) == 0
             d = torch.from_numpy(a.copy()).cuda()
             redop.check(redop.MPI_Reduce_local(dbs[0], d, n, dt, op))
             assert np.array_equal(d.cpu().numpy(), want1), ('contig', pol)
@@ -71,3 +100,4 @@ def test_every_store_policy_same_bits(oracle, dtname, opname):
             assert np.array_equal(out.cpu().numpy(), want_tree), ('tree', pol)
     finally:
         redop.set_store_policy(old['xcd_mask'], old['every'], old['phase'], old['tail_blocks'])
+        redop.set_sync_store_policy(-1)
