@@ -1489,6 +1489,31 @@ struct DeviceGuard {
     }
 };
 
+// ------------------------------------------- split combiners' fixup words
+// One buffer per (device, stream) for the words k_contig32 writes for a split
+// combiner (redop_kernels.h is_split): stream order serialises its users on
+// one stream, and no two streams share one.
+struct FixupBuf {
+    int dev;
+    uintptr_t stream;
+    void *ptr;
+    size_t bytes;
+};
+std::mutex g_fixup_mu;
+std::vector<FixupBuf> g_fixup;
+
+void free_fixup_buffers()
+{
+    std::lock_guard<std::mutex> l(g_fixup_mu);
+    for (FixupBuf &f : g_fixup) {
+        DeviceGuard g(f.dev);
+        (void) hipStreamSynchronize((hipStream_t) f.stream);
+        (void) hipFree(f.ptr);
+    }
+    g_fixup.clear();
+    (void) hipGetLastError();
+}
+
 // ------------------------------------------- peer access between devices
 // A kernel on device `dev` may dereference another device's hipMalloc memory
 // only once peer access dev -> owner is enabled.  The reference's HIP backend
@@ -1729,6 +1754,42 @@ int enqueue_runs(const void *inbuf, void *inoutbuf, const std::vector<Run> &runs
 
 }  // namespace
 
+namespace mpix {
+uint64_t *fixup_buffer(hipStream_t s, size_t bytes)
+{
+    int dev = 0;
+    if (hipStreamGetDevice(s, &dev) != hipSuccess)
+        return nullptr;
+    std::lock_guard<std::mutex> l(g_fixup_mu);
+    FixupBuf *f = nullptr;
+    for (FixupBuf &e : g_fixup)
+        if (e.dev == dev && e.stream == (uintptr_t) s)
+            f = &e;
+    if (!f) {
+        g_fixup.push_back(FixupBuf{dev, (uintptr_t) s, nullptr, 0});
+        f = &g_fixup.back();
+    }
+    if (f->bytes < bytes) {
+        DeviceGuard g(dev);
+        if (f->ptr) {       // enqueued work on this stream may still read the old one
+            if (hipStreamSynchronize(s) != hipSuccess)
+                return nullptr;
+            (void) hipFree(f->ptr);
+            f->ptr = nullptr;
+            f->bytes = 0;
+        }
+        size_t want = bytes < ((size_t) 64 << 10) ? (size_t) 64 << 10 : bytes;
+        if (hipMalloc(&f->ptr, want) != hipSuccess) {
+            (void) hipGetLastError();
+            f->ptr = nullptr;
+            return nullptr;
+        }
+        f->bytes = want;
+    }
+    return static_cast<uint64_t *>(f->ptr);
+}
+}  // namespace mpix
+
 extern "C" {
 
 int MPIX_Redop_init(void)
@@ -1777,6 +1838,7 @@ static void free_states(DevState *arr)
 
 int MPIX_Redop_finalize(void)
 {
+    free_fixup_buffers();
     std::vector<DevState *> pooled;
     {
         std::lock_guard<std::mutex> l(g_pool_mu);

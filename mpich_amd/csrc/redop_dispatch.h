@@ -28,6 +28,9 @@ struct Params {
     uint32_t wt_every = 0;      // and blocks b with b % wt_every == wt_phase (0 = none)
     uint32_t wt_phase = 0;
     uint32_t wt_xcd = 0;        // and every block running on an XCD whose bit is set
+    // split combiners (is_split, redop_kernels.h): one 64-bit word per 64
+    // units, bit j set when unit 64 w + j left its fast path (fixup_buffer)
+    uint64_t *fixup = nullptr;
 };
 
 constexpr unsigned kSignalMaxGrid = 64;     // 64 tiles of 64 x 1 packets: 64 KiB per operand
@@ -94,6 +97,12 @@ const Entry *lookup_pair(int raw, int opi);
 hipError_t launch_equal(const void *in, void *io, uint64_t n, hipStream_t s);
 
 // up to kMaxMultiInputs independent device copies in one launch
+// A device buffer of at least `bytes` for the split combiners' fixup words,
+// one per (device, stream): stream order serialises its users; grown (after
+// synchronising the stream) when a larger call comes; freed by
+// MPIX_Redop_finalize.  nullptr when it cannot be allocated.
+uint64_t *fixup_buffer(hipStream_t s, size_t bytes);
+
 hipError_t launch_copy_multi(const void *const *srcs, void *const *dsts, const uint64_t *bytes,
                              int n, hipStream_t s, unsigned wt_xcd = 0);
 

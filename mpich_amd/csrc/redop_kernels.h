@@ -25,6 +25,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "redop_ops.h"
 
 #ifndef MPIX_REDOP_UNROLL
@@ -319,34 +321,23 @@ k_contig_multi(MultiIn<typename C::unit> ins, int k, typename C::unit *__restric
     const uint64_t tile = nt * U;
     const uint64_t stride = (uint64_t) nblk * tile;
     const bool wt = wt_block(prm);
-    // input q + 1's packets are loaded before input q's are combined, so two
-    // inputs' worth stay in flight through the fold (one at a time: 5.86 TB/s
-    // at k = 7, tools/multi_probe.py)
-    auto load = [&](int q, v4u *b, uint64_t i) {
-        const v4u *__restrict__ vin = reinterpret_cast<const v4u *>(ins.p[q] + head);
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (i + u * nt < npk)
-                b[u] = ld16<true>(vin + i + u * nt);
-    };
+    // one input packet live beside the accumulator: input q is loaded, then
+    // combined, then input q + 1 (round 6; the round-5 form loaded q + 1
+    // before combining q, and its copy forced a full wait anyway), with the
+    // launch capping the waves per SIMD (launch_multi, kMultiLds)
+    // (tools/multi_fold_probe.hip, profiles/r06_multi_fold_caps2.json)
     for (uint64_t i = (uint64_t) blockIdx.x * tile + threadIdx.x; i < npk; i += stride) {
-        v4u acc[U], b[U], nb[U];
+        v4u acc[U];
 #pragma unroll
         for (int u = 0; u < U; ++u)
             if (i + u * nt < npk)
                 acc[u] = ld16<true>(vio + i + u * nt);
-        if (k > 0)
-            load(0, b, i);
         for (int q = 0; q < k; ++q) {
-            if (q + 1 < k)
-                load(q + 1, nb, i);
+            const v4u *__restrict__ vin = reinterpret_cast<const v4u *>(ins.p[q] + head);
 #pragma unroll
             for (int u = 0; u < U; ++u)
                 if (i + u * nt < npk)
-                    acc[u] = combine16<C>(acc[u], b[u], prm);
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                b[u] = nb[u];
+                    acc[u] = combine16<C>(acc[u], ld16<true>(vin + i + u * nt), prm);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -596,6 +587,34 @@ struct alignas(16) Pk32 {
     v4u lo, hi;
 };
 
+// Split combiners (C::kSplit, the soft complex products): C::apply_fast(a, b,
+// prm, ok) runs only the normal-operand fast paths and returns a unchanged
+// with ok false when any of them declines; the contiguous 32-byte kernel then
+// records the unit in Params::fixup (one 64-bit word per 64 units, written
+// for every group) and k_fixup32 combines the recorded units with the full
+// C::apply in a second launch.  The general paths stay out of the streaming
+// kernel, whose registers -- and so its waves per SIMD -- are the fast path's
+// (QuadCProd: 107 VGPRs with the general paths inline, 79 without; it is
+// VALU- and latency-bound).
+template <class C, class = void> struct is_split : std::false_type {};
+template <class C> struct is_split<C, std::void_t<decltype(C::kSplit)>>
+    : std::integral_constant<bool, C::kSplit> {};
+
+// the 64-bit lane mask of contig32's gathered layout (lane 2m holds unit m of
+// the run, lane 2m + 1 unit 32 + m) in unit order
+__device__ __forceinline__ uint64_t lanes_to_units(uint64_t m)
+{
+    auto even = [](uint64_t x) {
+        x &= 0x5555555555555555ull;
+        x = (x | (x >> 1)) & 0x3333333333333333ull;
+        x = (x | (x >> 2)) & 0x0f0f0f0f0f0f0f0full;
+        x = (x | (x >> 4)) & 0x00ff00ff00ff00ffull;
+        x = (x | (x >> 8)) & 0x0000ffff0000ffffull;
+        return (x | (x >> 16)) & 0x00000000ffffffffull;
+    };
+    return even(m) | (even(m >> 1) << 32);
+}
+
 // v from the other lane of each adjacent pair (quad_perm [1,0,3,2])
 __device__ __forceinline__ v4u swap_pair(v4u v)
 {
@@ -620,9 +639,21 @@ __device__ __forceinline__ void contig32_tile(const typename C::unit *in, const 
     const v4u *vin = reinterpret_cast<const v4u *>(in);
     const v4u *vio = reinterpret_cast<const v4u *>(io);     // the inout role (read)
     v4u *vout = reinterpret_cast<v4u *>(out);               // io itself, or the tree's output
+    constexpr bool split = is_split<C>::value;
+    bool ok = true;
     auto f = [&](const Pk32 &a, const Pk32 &b) {
-        return __builtin_bit_cast(Pk32, C::apply(__builtin_bit_cast(T, a),
-                                                 __builtin_bit_cast(T, b), prm));
+        if constexpr (split)
+            return __builtin_bit_cast(Pk32, C::apply_fast(__builtin_bit_cast(T, a),
+                                                          __builtin_bit_cast(T, b), prm, ok));
+        else
+            return __builtin_bit_cast(Pk32, C::apply(__builtin_bit_cast(T, a),
+                                                     __builtin_bit_cast(T, b), prm));
+    };
+    // one fixup word per 64 units (every group written: the buffer is reused)
+    auto record = [&](uint64_t unit0, uint64_t mask) {
+        if constexpr (split)
+            if ((threadIdx.x & 63) == 0)
+                prm.fixup[unit0 >> 6] = mask;
     };
     const uint64_t tile = nt * U;
     if ((t + 1) * tile <= n) {
@@ -655,6 +686,8 @@ __device__ __forceinline__ void contig32_tile(const typename C::unit *in, const 
             const uint64_t q = 2 * (t * tile + u * nt + wave * 64) + lane;
             st16_pol<NTS>(vout + q, odd ? y : r.lo, wt);
             st16_pol<NTS>(vout + q + 64, odd ? r.hi : y, wt);
+            if constexpr (split)
+                record(t * tile + u * nt + wave * 64, lanes_to_units(__ballot(!ok)));
         }
     } else {
         for (uint64_t k = t * tile + threadIdx.x; k < n; k += nt) {
@@ -662,6 +695,8 @@ __device__ __forceinline__ void contig32_tile(const typename C::unit *in, const 
                              Pk32{ld16<NTL>(vin + 2 * k), ld16<NTL>(vin + 2 * k + 1)});
             st16_pol<NTS>(vout + 2 * k, r.lo, wt);
             st16_pol<NTS>(vout + 2 * k + 1, r.hi, wt);
+            if constexpr (split)        // a unit per lane: the mask is in unit order
+                record(k - (threadIdx.x & 63), __ballot(!ok));
         }
     }
 }
@@ -676,6 +711,26 @@ k_contig32(const typename C::unit *in, const typename C::unit *io, typename C::u
     const bool wt = wt_block(prm);
     for (uint64_t t = blockIdx.x; t < ntiles; t += nblk)
         contig32_tile<C, U, NTL, NTS>(in, io, out, n, t, nthreads, wt, prm);
+}
+
+// The second launch of a split combiner: every unit the fast kernel recorded
+// in the fixup words (it left them unchanged in `out`), combined with the full
+// C::apply from the untouched operands (`io` is `out` in place, or the tree's
+// separate inout role).  Rare units, a word per lane.
+template <class C>
+__global__ void __launch_bounds__(256)
+k_fixup32(const typename C::unit *in, const typename C::unit *io, typename C::unit *out, uint64_t n,
+          Params prm, uint32_t nblk)
+{
+    const uint64_t nw = (n + 63) / 64;
+    for (uint64_t w = (uint64_t) blockIdx.x * 256 + threadIdx.x; w < nw; w += (uint64_t) nblk * 256) {
+        uint64_t m = prm.fixup[w];
+        while (m) {
+            const uint64_t u = w * 64 + (uint64_t) __builtin_ctzll(m);
+            m &= m - 1;
+            out[u] = C::apply(io[u], in[u], prm);
+        }
+    }
 }
 
 // The batch entry's form for 32-byte units: segment s owns blocks [blk0,
@@ -857,6 +912,34 @@ inline void set_store_policy(Params &p, const LaunchCfg &cfg, unsigned grid)
 #endif
 constexpr unsigned kContig32Block = MPIX_REDOP_BLOCK32;
 
+// k_contig32 over 16-byte-aligned 32-byte units (`io` read in the inout
+// role, the result to `out`: io itself, or the tree's output); a split
+// combiner adds its fixup launch
+template <class C>
+hipError_t launch_contig32(const typename C::unit *in, const typename C::unit *io,
+                           typename C::unit *out, uint64_t count, const Params &prm,
+                           const LaunchCfg &cfg, hipStream_t s)
+{
+    constexpr int U32 = MPIX_REDOP_UNROLL32;
+    const unsigned grid = grid_for((uint64_t) kContig32Block * U32, count, cfg.max_grid,
+                                   kContig32Block);
+    Params p = prm;
+    p.done = nullptr;
+    set_store_policy(p, cfg, grid);
+    if constexpr (is_split<C>::value) {
+        p.fixup = fixup_buffer(s, (count + 63) / 64 * sizeof(uint64_t));
+        if (!p.fixup)
+            return hipErrorOutOfMemory;
+    }
+    hipLaunchKernelGGL((k_contig32<C, U32, MPIX_REDOP_NT_LOAD, MPIX_REDOP_NT_STORE>), dim3(grid),
+                       dim3(kContig32Block), 0, s, in, io, out, count, p, grid, kContig32Block);
+    if constexpr (is_split<C>::value) {
+        const unsigned g2 = grid_for(256, (count + 63) / 64, 1024, 256);
+        hipLaunchKernelGGL((k_fixup32<C>), dim3(g2), dim3(256), 0, s, in, io, out, count, p, g2);
+    }
+    return hipGetLastError();
+}
+
 // Contiguous launcher: chooses the packet or the element-wise kernel.
 template <class C>
 hipError_t launch_contig(const void *in, void *io, uint64_t count, const Params &prm,
@@ -874,14 +957,9 @@ hipError_t launch_contig(const void *in, void *io, uint64_t count, const Params 
         // flight as k_contig's four packets; operands off the 16-byte grid go
         // element-wise
         if (((ai | ao) & 15) == 0) {
-            constexpr int U32 = MPIX_REDOP_UNROLL32;
-            unsigned grid = grid_for((uint64_t) kContig32Block * U32, count, cfg.max_grid, kContig32Block);
-            Params p = prm;
-            p.done = nullptr;
-            set_store_policy(p, cfg, grid);
-            hipLaunchKernelGGL((k_contig32<C, U32, MPIX_REDOP_NT_LOAD, MPIX_REDOP_NT_STORE>),
-                               dim3(grid), dim3(kContig32Block), 0, s, tin, tio, tio, count, p, grid,
-                               kContig32Block);
+            hipError_t e = launch_contig32<C>(tin, tio, tio, count, prm, cfg, s);
+            if (e != hipSuccess)
+                return e;
         } else {
             unsigned grid = grid_for((uint64_t) cfg.block * 4, count, cfg.max_grid, cfg.block);
             hipLaunchKernelGGL((k_elem<C>), dim3(grid), dim3(cfg.block), 0, s, tin, tio, count,
@@ -924,6 +1002,10 @@ hipError_t launch_contig(const void *in, void *io, uint64_t count, const Params 
     return e;
 }
 
+// LDS per 64 threads of a multi-input fold block: 160 KiB per CU / 6656 B =
+// 24 one-wave blocks = 6 waves per SIMD (the kernel itself uses no LDS)
+constexpr unsigned kMultiLds = 6656;
+
 template <class C>
 hipError_t launch_multi(const void *const *ins, int k, void *io, uint64_t count, const Params &prm,
                         const LaunchCfg &cfg, hipStream_t s)
@@ -954,8 +1036,21 @@ hipError_t launch_multi(const void *const *ins, int k, void *io, uint64_t count,
         unsigned grid = grid_for((uint64_t) cfg.block * U, npk, cfg.max_grid, cfg.block);
         Params p = prm;
         set_store_policy(p, cfg, grid);
+        // k >= 2 inputs: unused LDS per block caps the waves per SIMD at 6
+        // (24 one-wave blocks per CU): with k + 2 streams per wave fewer
+        // waves in flight run faster -- 256 MiB fp32, one-wave blocks, store
+        // policy on: k = 3 6.53 -> 6.91, k = 7 6.53 -> 6.92, k = 15 6.38 ->
+        // 6.65 TB/s against the round-5 form; the headline kernel (k = 1)
+        // loses with any cap (7.04 -> 6.73) and keeps none
+        // (profiles/r06_multi_fold_caps2.json)
+        size_t lds = 0;
+        if (k >= 2) {
+            lds = (size_t) kMultiLds * ((unsigned) cfg.block / 64u);
+            if (lds > 65536)
+                lds = 0;
+        }
         if constexpr (sizeof(T) <= 16)
-            hipLaunchKernelGGL((k_contig_multi<C, U>), dim3(grid), dim3(cfg.block), 0, s, mi, k,
+            hipLaunchKernelGGL((k_contig_multi<C, U>), dim3(grid), dim3(cfg.block), lds, s, mi, k,
                                tio, head, npk, tail_start, ntail, p, grid, (uint32_t) cfg.block);
     } else {
         unsigned grid = grid_for((uint64_t) cfg.block * 4, count, cfg.max_grid, cfg.block);
@@ -992,15 +1087,7 @@ hipError_t launch_tree(const void *const *ins, int k, void *out, uint64_t count,
         if (k == 2 && pres == 3u &&
             ((ao | reinterpret_cast<uintptr_t>(ins[0]) | reinterpret_cast<uintptr_t>(ins[1])) & 15) ==
                 0) {
-            constexpr int U32 = MPIX_REDOP_UNROLL32;
-            const unsigned grid = grid_for((uint64_t) kContig32Block * U32, count, cfg.max_grid, kContig32Block);
-            Params p = prm;
-            p.done = nullptr;
-            set_store_policy(p, cfg, grid);
-            hipLaunchKernelGGL((k_contig32<C, U32, MPIX_REDOP_NT_LOAD, MPIX_REDOP_NT_STORE>),
-                               dim3(grid), dim3(kContig32Block), 0, s, mi.p[1], mi.p[0], tout, count,
-                               p, grid, kContig32Block);
-            return hipGetLastError();
+            return launch_contig32<C>(mi.p[1], mi.p[0], tout, count, prm, cfg, s);
         }
     }
     if (aligned) {
@@ -1115,7 +1202,17 @@ hipError_t launch_batch(const void *const *ins, void *const *ios, const uint64_t
     using T = typename C::unit;
     Params p = prm;
     p.done = nullptr;
-    if constexpr (sizeof(T) > 16) {
+    if constexpr (is_split<C>::value) {
+        // a split combiner: each triple its own launches (launch_contig: the
+        // fast kernel and its fixup)
+        for (int i = 0; i < k; ++i)
+            if (counts[i]) {
+                hipError_t e = launch_contig<C>(ins[i], ios[i], counts[i], p, cfg, s);
+                if (e != hipSuccess)
+                    return e;
+            }
+        return hipSuccess;
+    } else if constexpr (sizeof(T) > 16) {
         // 32-byte units: the 16-byte-aligned triples as one k_batch32 launch,
         // the others element-wise one launch each
         constexpr int U32 = MPIX_REDOP_UNROLL32;

@@ -32,6 +32,12 @@
 
 #include <stdint.h>
 
+// the complex product's fast path with quad_mul_fast_wide's products (1) or
+// quad_mul_fast's digits (0)
+#ifndef MPIX_QUAD_CMUL_WIDE
+#define MPIX_QUAD_CMUL_WIDE 0
+#endif
+
 #include "redop_dispatch.h"
 
 // MPIX_SOFT_HOST: the same functions as plain host C++, for the CPU test that
@@ -206,33 +212,23 @@ MPIX_SDEV uint32_t shr128_lost(uint32_t v[4], uint32_t d)
     return lost;
 }
 
-// v <<= s (s in 0..127)
-MPIX_SDEV void shl128(uint32_t v[4], uint32_t s)
-{
-    const bool b64 = (s & 64) != 0, b32 = (s & 32) != 0;
-    const uint32_t t3 = b64 ? v[1] : v[3], t2 = b64 ? v[0] : v[2];
-    const uint32_t t1 = b64 ? 0u : v[1], t0 = b64 ? 0u : v[0];
-    const uint32_t u3 = b32 ? t2 : t3, u2 = b32 ? t1 : t2, u1 = b32 ? t0 : t1, u0 = b32 ? 0u : t0;
-    const uint32_t r = s & 31;
-    v[3] = funnel_l(u3, u2, r);
-    v[2] = funnel_l(u2, u1, r);
-    v[1] = funnel_l(u1, u0, r);
-    v[0] = u0 << r;
-}
-
 // The sum of two normal operands, A (the larger magnitude) and B, both with
 // their leading bit at 126 of a 128-bit limb vector, B's exponent d below A's
 // (d clamped to 127: B then only leaves its sticky bit, as it did before it
 // moved out of range).  B is aligned by d with the bits shifted out folded
 // into its lowest bit (a sticky bit below every rounding position), added or
-// (sub) subtracted, the exact sum normalised to bit 127 and rounded to BITS
-// bits (RNE) at bit 128 - BITS: round_exact's normal-result case.  *q = the
-// significand (limbs, leading bit at BITS - 1 of the 128-bit value), *E its
-// biased exponent for A's biased exponent xa.  Returns false for a zero sum
-// or a result that is not normal (the general path decides those).
+// (sub) subtracted, and the exact sum S rounded to BITS bits (RNE) at its
+// leading bit: the cut sits lz bits lower than for a leading bit at 127, so
+// the significand is S shifted right by 128 - BITS - lz, a funnel shift per
+// limb -- no normalising shift.  A sum whose leading bit is not in the top
+// limb (lz > 31: opposite signs cancelling 30 bits or more; for binary128
+// lz > 15, where the significand would need a left shift) goes to the
+// general path, as do a zero sum and a result that is not normal.  *q = the
+// significand (limbs, leading bit at BITS - 1), *E its biased exponent for
+// A's biased exponent xa.  round_exact's normal-result case.
 template <int BITS>
-MPIX_SDEV bool add_normal_limbs(const uint32_t A[4], uint32_t B[4], uint32_t d, bool sub, int64_t xa,
-                                uint32_t q[4], int64_t *E)
+MPIX_SDEV bool add_normal_limbs(const uint32_t A[4], uint32_t B[4], uint32_t d, bool sub, int32_t xa,
+                                uint32_t q[4], int32_t *E)
 {
     if (shr128_lost(B, d))
         B[0] |= 1u;
@@ -245,32 +241,33 @@ MPIX_SDEV bool add_normal_limbs(const uint32_t A[4], uint32_t B[4], uint32_t d, 
         S[i] = (uint32_t) c;
         c >>= 32;
     }
-    const uint32_t lz = S[3] ? clz32(S[3])
-                      : S[2] ? 32u + clz32(S[2])
-                      : S[1] ? 64u + clz32(S[1])
-                      : 96u + clz32(S[0]);
-    if (lz >= 128)
-        return false;                   // exact cancellation: +0, general path
-    shl128(S, lz);
-    constexpr int C = 128 - BITS;       // the cut: bits below it are rounded off
-    // the BITS-bit significand S >> C, its round bit C - 1 and sticky below
+    const uint32_t lz = clz32(S[3]);
     uint32_t rnd, sticky;
-    if constexpr (C == 64) {            // x87: the two high limbs
-        q[0] = S[2];
-        q[1] = S[3];
+    if constexpr (BITS == 64) {
+        // x87: q = S >> (64 - lz), lz in 0..31
+        if (lz > 31)
+            return false;
+        const uint32_t r1 = funnel_l(S[1], S[0], lz);
+        q[0] = funnel_l(S[2], S[1], lz);
+        q[1] = funnel_l(S[3], S[2], lz);
         q[2] = q[3] = 0;
-        rnd = S[1] >> 31;
-        sticky = (S[1] & 0x7fffffffu) | S[0];
+        rnd = r1 >> 31;
+        sticky = (r1 & 0x7fffffffu) | (S[0] << lz);
     } else {
-        static_assert(C > 0 && C < 32, "cut inside the lowest limb");
-        q[0] = funnel_r(S[1], S[0], C);
-        q[1] = funnel_r(S[2], S[1], C);
-        q[2] = funnel_r(S[3], S[2], C);
-        q[3] = S[3] >> C;
-        rnd = (S[0] >> (C - 1)) & 1u;
-        sticky = S[0] & ((1u << (C - 1)) - 1u);
+        static_assert(BITS == 113, "binary128");
+        // q = S >> (15 - lz), lz in 0..15 (the cut in the lowest limb)
+        if (lz > 15)
+            return false;
+        const uint32_t cut = 15u - lz;
+        q[0] = funnel_r(S[1], S[0], cut);
+        q[1] = funnel_r(S[2], S[1], cut);
+        q[2] = funnel_r(S[3], S[2], cut);
+        q[3] = S[3] >> cut;
+        const uint32_t half = (1u << cut) >> 1;         // the round bit (0: none below)
+        rnd = (S[0] & half) != 0;
+        sticky = S[0] & (half - 1u) & (cut ? 0xffffffffu : 0u);
     }
-    int64_t e = xa + 1 - (int64_t) lz;
+    int32_t e = xa + 1 - (int32_t) lz;
     const uint32_t inc = rnd & ((sticky != 0) | (q[0] & 1u));
     uint64_t k = inc;
     for (int i = 0; i < 4; ++i) {
@@ -280,7 +277,7 @@ MPIX_SDEV bool add_normal_limbs(const uint32_t A[4], uint32_t B[4], uint32_t d, 
     }
     // carried out of the significand: it was all ones, it is now 2^BITS
     bool ovf;
-    if constexpr (C == 64)
+    if constexpr (BITS == 64)
         ovf = (q[2] & 1u) != 0;
     else
         ovf = (q[3] >> (BITS - 96)) != 0;
@@ -295,11 +292,14 @@ MPIX_SDEV bool add_normal_limbs(const uint32_t A[4], uint32_t B[4], uint32_t d, 
 
 // a + b (sub: a - b), as fldt a; fldt b; faddp (fsubp); the result keeps a's
 // padding.  FAST: both operands normal -> add_normal_limbs, the rest the general path.
-template <bool FAST = true>
-MPIX_SDEV X87 x87_add(const X87 &a, const X87 &b, bool sub)
+// a + b (sub: a - b) of two normal operands whose sum is normal: *r and true;
+// false for anything else (x87_add's general path decides)
+MPIX_SDEV bool x87_add_fast(const X87 &a, const X87 &b, bool sub, X87 *r)
 {
     const uint32_t ea = (uint32_t) a.se & 0x7fff, eb = (uint32_t) b.se & 0x7fff;
-    if (FAST && ea - 1u < 0x7ffeu && eb - 1u < 0x7ffeu && (a.m >> 63) && (b.m >> 63)) {
+    if (!(ea - 1u < 0x7ffeu && eb - 1u < 0x7ffeu && (a.m >> 63) && (b.m >> 63)))
+        return false;
+    {
         // both normal: order by magnitude, align, add_normal_limbs
         const bool swap = ea < eb || (ea == eb && a.m < b.m);
         const bool sa0 = (a.se >> 15) & 1, sb0 = ((b.se >> 15) & 1) ^ (sub ? 1 : 0);
@@ -312,10 +312,21 @@ MPIX_SDEV X87 x87_add(const X87 &a, const X87 &b, bool sub)
         const uint32_t A[4] = {0u, al << 31, funnel_r(ah, al, 1), ah >> 1};
         uint32_t B[4] = {0u, bl << 31, funnel_r(bh, bl, 1), bh >> 1};
         uint32_t q[4];
-        int64_t e;
-        if (add_normal_limbs<64>(A, B, d < 127u ? d : 127u, sa != sb, xa, q, &e))
-            return x87_make(a, sa, (uint32_t) e, ((uint64_t) q[1] << 32) | q[0]);
+        int32_t e;
+        if (!add_normal_limbs<64>(A, B, d < 127u ? d : 127u, sa != sb, (int32_t) xa, q, &e))
+            return false;
+        *r = x87_make(a, sa, (uint32_t) e, ((uint64_t) q[1] << 32) | q[0]);
+        return true;
     }
+}
+
+template <bool FAST = true>
+MPIX_SDEV X87 x87_add(const X87 &a, const X87 &b, bool sub)
+{
+    const uint32_t ea = (uint32_t) a.se & 0x7fff, eb = (uint32_t) b.se & 0x7fff;
+    X87 r;
+    if (FAST && x87_add_fast(a, b, sub, &r))
+        return r;
     const int ca = x87_class(a.m, ea), cb = x87_class(b.m, eb);
     if (ca == kX87Bad || cb == kX87Bad)
         return x87_indefinite(a);
@@ -353,10 +364,14 @@ MPIX_SDEV X87 x87_add(const X87 &a, const X87 &b, bool sub)
     return x87_from_round(a, sa, S, xa);
 }
 
-MPIX_SDEV X87 x87_mul(const X87 &a, const X87 &b)
+// a * b of two normal operands whose product is normal: *r and true; false
+// for anything else (x87_mul's general path decides)
+MPIX_SDEV bool x87_mul_fast(const X87 &a, const X87 &b, X87 *r)
 {
     const uint32_t ea = (uint32_t) a.se & 0x7fff, eb = (uint32_t) b.se & 0x7fff;
-    if (ea - 1u < 0x7ffeu && eb - 1u < 0x7ffeu && (a.m >> 63) && (b.m >> 63)) {
+    if (!(ea - 1u < 0x7ffeu && eb - 1u < 0x7ffeu && (a.m >> 63) && (b.m >> 63)))
+        return false;
+    {
         // both normal: the product of the significands is in [2^126, 2^128),
         // so its leading bit sits at 126 + top and the rounding cut at a
         // fixed place -- the general path below with its shifts constant.
@@ -377,10 +392,21 @@ MPIX_SDEV X87 x87_mul(const X87 &a, const X87 &b)
                     E += 1;
                 }
             }
-            if (E <= 0x7ffe)
-                return x87_make(a, ((a.se ^ b.se) >> 15) & 1, (uint32_t) E, q);
+            if (E <= 0x7ffe) {
+                *r = x87_make(a, ((a.se ^ b.se) >> 15) & 1, (uint32_t) E, q);
+                return true;
+            }
         }
     }
+    return false;
+}
+
+MPIX_SDEV X87 x87_mul(const X87 &a, const X87 &b)
+{
+    const uint32_t ea = (uint32_t) a.se & 0x7fff, eb = (uint32_t) b.se & 0x7fff;
+    X87 r;
+    if (x87_mul_fast(a, b, &r))
+        return r;
     const int ca = x87_class(a.m, ea), cb = x87_class(b.m, eb);
     if (ca == kX87Bad || cb == kX87Bad)
         return x87_indefinite(a);
@@ -466,11 +492,14 @@ MPIX_SDEV Quad quad_from_round(bool s, u128 S, int64_t E0)
 }
 
 // x + y (sub: x - y): __addtf3 / __subtf3
-template <bool FAST = true>
-MPIX_SDEV Quad quad_add(const Quad &x, const Quad &y, bool sub)
+// x + y (sub: x - y) of two normal operands whose sum is normal: *r and
+// true; false for anything else (quad_add's general path decides)
+MPIX_SDEV bool quad_add_fast(const Quad &x, const Quad &y, bool sub, Quad *r)
 {
     const uint32_t ex = (uint32_t) (x.hi >> 48) & 0x7fff, ey = (uint32_t) (y.hi >> 48) & 0x7fff;
-    if (FAST && ex - 1u < 0x7ffeu && ey - 1u < 0x7ffeu) {
+    if (!(ex - 1u < 0x7ffeu && ey - 1u < 0x7ffeu))
+        return false;
+    {
         // both normal: as x87_add's fast path (magnitudes ordered by the
         // encoding without its sign bit)
         const uint64_t hx = x.hi & ~(1ull << 63), hy = y.hi & ~(1ull << 63);
@@ -489,15 +518,22 @@ MPIX_SDEV Quad quad_add(const Quad &x, const Quad &y, bool sub)
                                funnel_l(a3, a2, 14)};
         uint32_t B[4] = {b0 << 14, funnel_l(b1, b0, 14), funnel_l(b2, b1, 14), funnel_l(b3, b2, 14)};
         uint32_t q[4];
-        int64_t e;
-        if (add_normal_limbs<113>(A, B, d < 127u ? d : 127u, sa != sb, xa, q, &e)) {
-            Quad r;
-            r.lo = ((uint64_t) q[1] << 32) | q[0];
-            r.hi = ((uint64_t) sa << 63) | ((uint64_t) e << 48) |
-                   ((uint64_t) (q[3] & 0xffffu) << 32) | q[2];
-            return r;
-        }
+        int32_t e;
+        if (!add_normal_limbs<113>(A, B, d < 127u ? d : 127u, sa != sb, (int32_t) xa, q, &e))
+            return false;
+        r->lo = ((uint64_t) q[1] << 32) | q[0];
+        r->hi = ((uint64_t) sa << 63) | ((uint64_t) e << 48) | ((uint64_t) (q[3] & 0xffffu) << 32) |
+                q[2];
+        return true;
     }
+}
+
+template <bool FAST = true>
+MPIX_SDEV Quad quad_add(const Quad &x, const Quad &y, bool sub)
+{
+    Quad r;
+    if (FAST && quad_add_fast(x, y, sub, &r))
+        return r;
     const int cx = quad_class(x), cy = quad_class(y);
     if (cx == kX87Nan || cy == kX87Nan)
         return quad_nan(x, cx == kX87Nan, y, cy == kX87Nan, !sub);
@@ -536,43 +572,129 @@ MPIX_SDEV Quad quad_add(const Quad &x, const Quad &y, bool sub)
     return quad_from_round(sa, S, xa);
 }
 
+// x * y of two normal operands whose product is normal, as four 64 x 64-bit
+// partial products: *r and true; false for anything else (quad_mul's general
+// path decides).  The shorter dependency chains of the two forms: the
+// standalone MPI_REAL16 PROD row, bandwidth-bound, runs 6 % faster with it
+// than with quad_mul_fast's digits (7.34-7.38 against 6.87-6.94 TB/s,
+// profiles/r06_soft_rows_ab3.json)
+MPIX_SDEV bool quad_mul_fast_wide(const Quad &x, const Quad &y, Quad *r)
+{
+    const uint32_t ex = (uint32_t) (x.hi >> 48) & 0x7fff, ey = (uint32_t) (y.hi >> 48) & 0x7fff;
+    if (!(ex - 1u < 0x7ffeu && ey - 1u < 0x7ffeu))
+        return false;
+    // significands in [2^112, 2^113), the product in [2^224, 2^226) with its
+    // leading bit at 224 + top, so the cut below the 113-bit result is at a
+    // fixed place (the general path's shifts constant)
+    const uint64_t a0 = x.lo, a1 = (x.hi & 0xffffffffffffull) | (1ull << 48);
+    const uint64_t b0 = y.lo, b1 = (y.hi & 0xffffffffffffull) | (1ull << 48);
+    const u128 p00 = (u128) a0 * b0, p01 = (u128) a0 * b1, p10 = (u128) a1 * b0;
+    const u128 p11 = (u128) a1 * b1;
+    const u128 mid = p01 + p10;     // a1, b1 < 2^49: no carry out
+    const u128 lo = p00 + (mid << 64);
+    const u128 hi = p11 + (mid >> 64) + (lo < p00 ? 1 : 0);
+    const int top = (int) (hi >> 97) & 1;
+    const u128 q112 = (hi << 16) | (lo >> 112);         // P >> 112
+    const u128 rest = lo & (((u128) 1 << 112) - 1);
+    const u128 q0 = top ? q112 >> 1 : q112;
+    const bool rnd = top ? (q112 & 1) != 0 : ((rest >> 111) & 1) != 0;
+    const bool sticky = top ? rest != 0 : (rest & (((u128) 1 << 111) - 1)) != 0;
+    int64_t E = (int64_t) ex + ey - 16383 + top;
+    if (E < 1)
+        return false;
+    u128 q = q0;
+    if (rnd && (sticky || (q & 1))) {
+        q += 1;
+        if (q >> 113) {             // carried out of the significand
+            q >>= 1;
+            E += 1;
+        }
+    }
+    if (E > 0x7ffe)
+        return false;
+    *r = quad_make(((x.hi ^ y.hi) >> 63) & 1, (uint32_t) E, q & (((u128) 1 << 112) - 1));
+    return true;
+}
+
+// x * y of two normal operands whose product is normal: *r and true; false
+// for anything else.  The same product as quad_mul_fast_wide in fewer
+// instructions: 29-bit digits, no carry between the multiply-adds
+MPIX_SDEV bool quad_mul_fast(const Quad &x, const Quad &y, Quad *r)
+{
+    const uint32_t ex = (uint32_t) (x.hi >> 48) & 0x7fff, ey = (uint32_t) (y.hi >> 48) & 0x7fff;
+    if (!(ex - 1u < 0x7ffeu && ey - 1u < 0x7ffeu))
+        return false;
+    {
+        // both normal: significands in [2^112, 2^113), the product in
+        // [2^224, 2^226) with its leading bit at 224 + top, so the cut below
+        // the 113-bit result is at bit 112 + top (the general path's shifts
+        // constant).  The significands as four 29-bit digits: a digit
+        // product is < 2^58, so a column of at most four sums in 64 bits
+        // with no carry between the 16 multiply-adds; one carry pass turns
+        // the columns into digits d0..d7, and the significand is the value
+        // above 2^87 (digits 3..7, V) shifted right by 25 + top -- the digits
+        // below only decide the sticky bit.  A denormal or overflowing result
+        // takes the general path.
+        constexpr uint32_t M29 = (1u << 29) - 1u;
+        const uint32_t x0 = (uint32_t) x.lo, x1 = (uint32_t) (x.lo >> 32), x2 = (uint32_t) x.hi;
+        const uint32_t x3 = ((uint32_t) (x.hi >> 32) & 0xffffu) | 0x10000u;
+        const uint32_t y0 = (uint32_t) y.lo, y1 = (uint32_t) (y.lo >> 32), y2 = (uint32_t) y.hi;
+        const uint32_t y3 = ((uint32_t) (y.hi >> 32) & 0xffffu) | 0x10000u;
+        const uint32_t a[4] = {x0 & M29, funnel_r(x1, x0, 29) & M29, funnel_r(x2, x1, 26) & M29,
+                               funnel_r(x3, x2, 23)};
+        const uint32_t b[4] = {y0 & M29, funnel_r(y1, y0, 29) & M29, funnel_r(y2, y1, 26) & M29,
+                               funnel_r(y3, y2, 23)};
+        uint64_t col[7];
+#pragma unroll
+        for (int c = 0; c < 7; ++c) {
+            uint64_t acc = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (c - i >= 0 && c - i < 4)
+                    acc += (uint64_t) a[i] * b[c - i];
+            col[c] = acc;
+        }
+        uint32_t d[8];
+        uint64_t t = 0;
+#pragma unroll
+        for (int c = 0; c < 7; ++c) {
+            t = col[c] + (t >> 29);
+            d[c] = (uint32_t) t & M29;
+        }
+        d[7] = (uint32_t) (t >> 29);            // < 2^23
+        // V = digits 3..7 as 32-bit words (bits 87.. of the product)
+        const uint32_t v[5] = {d[3] | (d[4] << 29), (d[4] >> 3) | (d[5] << 26),
+                               (d[5] >> 6) | (d[6] << 23), (d[6] >> 9) | (d[7] << 20), d[7] >> 12};
+        const uint32_t top = d[7] >> 22;        // leading bit 225 (1) or 224 (0)
+        const uint32_t c = 25u + top;           // the cut, bit 112 + top of the product
+        uint32_t q[4] = {funnel_r(v[1], v[0], c), funnel_r(v[2], v[1], c), funnel_r(v[3], v[2], c),
+                         funnel_r(v[4], v[3], c)};
+        const uint32_t rnd = (v[0] >> (c - 1u)) & 1u;
+        const uint32_t sticky = (v[0] & ((1u << (c - 1u)) - 1u)) | d[2] | d[1] | d[0];
+        uint64_t k = rnd & ((sticky != 0) | (q[0] & 1u));
+        for (int i = 0; i < 4; ++i) {
+            k += q[i];
+            q[i] = (uint32_t) k;
+            k >>= 32;
+        }
+        int32_t E = (int32_t) (ex + ey + top) - 16383;
+        if (q[3] >> 17) {               // carried out of the significand: 2^113
+            q[3] = 0x10000u;            // (q[0..2] are 0)
+            E += 1;
+        }
+        r->lo = ((uint64_t) q[1] << 32) | q[0];
+        r->hi = (((x.hi ^ y.hi) >> 63) << 63) | ((uint64_t) E << 48) |
+                ((uint64_t) (q[3] & 0xffffu) << 32) | q[2];
+        return E >= 1 && E <= 0x7ffe;
+    }
+}
+
 // x * y: __multf3 (the 226-bit product folded to 128 bits plus a sticky bit)
 MPIX_SDEV Quad quad_mul(const Quad &x, const Quad &y)
 {
-    const uint32_t ex = (uint32_t) (x.hi >> 48) & 0x7fff, ey = (uint32_t) (y.hi >> 48) & 0x7fff;
-    if (ex - 1u < 0x7ffeu && ey - 1u < 0x7ffeu) {
-        // both normal: significands in [2^112, 2^113), the product in
-        // [2^224, 2^226) with its leading bit at 224 + top, so the cut below
-        // the 113-bit result is at a fixed place (the general path's shifts
-        // constant).  A denormal or overflowing result takes the general path.
-        const uint64_t a0 = x.lo, a1 = (x.hi & 0xffffffffffffull) | (1ull << 48);
-        const uint64_t b0 = y.lo, b1 = (y.hi & 0xffffffffffffull) | (1ull << 48);
-        const u128 p00 = (u128) a0 * b0, p01 = (u128) a0 * b1, p10 = (u128) a1 * b0;
-        const u128 p11 = (u128) a1 * b1;
-        const u128 mid = p01 + p10;     // a1, b1 < 2^49: no carry out
-        const u128 lo = p00 + (mid << 64);
-        const u128 hi = p11 + (mid >> 64) + (lo < p00 ? 1 : 0);
-        const int top = (int) (hi >> 97) & 1;
-        const u128 q112 = (hi << 16) | (lo >> 112);         // P >> 112
-        const u128 rest = lo & (((u128) 1 << 112) - 1);
-        const u128 q0 = top ? q112 >> 1 : q112;
-        const bool rnd = top ? (q112 & 1) != 0 : ((rest >> 111) & 1) != 0;
-        const bool sticky = top ? rest != 0 : (rest & (((u128) 1 << 111) - 1)) != 0;
-        int64_t E = (int64_t) ex + ey - 16383 + top;
-        if (E >= 1) {
-            u128 q = q0;
-            if (rnd && (sticky || (q & 1))) {
-                q += 1;
-                if (q >> 113) {         // carried out of the significand
-                    q >>= 1;
-                    E += 1;
-                }
-            }
-            if (E <= 0x7ffe)
-                return quad_make(((x.hi ^ y.hi) >> 63) & 1, (uint32_t) E,
-                                 q & (((u128) 1 << 112) - 1));
-        }
-    }
+    Quad r;
+    if (quad_mul_fast_wide(x, y, &r))
+        return r;
     const int cx = quad_class(x), cy = quad_class(y);
     if (cx == kX87Nan || cy == kX87Nan)
         return quad_nan(x, cx == kX87Nan, y, cy == kX87Nan, true);
@@ -640,14 +762,39 @@ struct QuadCSum {
         return r;
     }
 };
+// The complex products are split combiners (is_split, redop_kernels.h): the
+// contiguous kernel runs apply_fast -- all six operations' normal-operand
+// fast paths, one flag for the lot, the unit left unchanged when any declines
+// -- and a second launch combines those units with apply, each operation's
+// fast path or general path.  The general paths' registers stay out of the
+// streaming kernel.
 struct QuadCProd {
     using unit = QuadC;
+    static constexpr bool kSplit = true;
     static MPIX_SDEV QuadC apply(QuadC c, QuadC b, const Params &)
     {
         QuadC r;
         r.re = quad_add(quad_mul(c.re, b.re), quad_mul(c.im, b.im), true);
         r.im = quad_add(quad_mul(c.im, b.re), quad_mul(c.re, b.im), false);
         return r;
+    }
+    static MPIX_SDEV QuadC apply_fast(QuadC c, QuadC b, const Params &, bool &ok)
+    {
+        QuadC r;
+        Quad p0, p1, p2, p3;
+#if MPIX_QUAD_CMUL_WIDE
+#define MPIX_QMF quad_mul_fast_wide
+#else
+#define MPIX_QMF quad_mul_fast
+#endif
+        ok = MPIX_QMF(c.re, b.re, &p0);
+        ok &= MPIX_QMF(c.im, b.im, &p1);
+        ok &= quad_add_fast(p0, p1, true, &r.re);
+        ok &= MPIX_QMF(c.im, b.re, &p2);
+        ok &= MPIX_QMF(c.re, b.im, &p3);
+#undef MPIX_QMF
+        ok &= quad_add_fast(p2, p3, false, &r.im);
+        return ok ? r : c;
     }
 };
 struct alignas(16) X87C {
@@ -676,6 +823,23 @@ MPIX_SDEV X87 x87_signed(bool one, const X87 &sgn)      // copysign(one ? 1 : 0,
 
 struct X87CProd {
     using unit = X87C;
+    static constexpr bool kSplit = true;
+    // the six fast paths (as QuadCProd): finite results, so the Annex G
+    // recovery of apply can never be needed where they all succeed
+    static MPIX_SDEV X87C apply_fast(X87C x, X87C y, const Params &, bool &ok)
+    {
+        X87 ac, bd, ad, bc, re, im;
+        ok = x87_mul_fast(x.re, y.re, &ac);
+        ok &= x87_mul_fast(x.im, y.im, &bd);
+        ok &= x87_mul_fast(x.re, y.im, &ad);
+        ok &= x87_mul_fast(x.im, y.re, &bc);
+        ok &= x87_add_fast(ac, bd, true, &re);
+        ok &= x87_add_fast(ad, bc, false, &im);
+        X87C r;     // stored with fstpt: each part keeps inout's padding
+        r.re = x87_make(x.re, (re.se >> 15) & 1, (uint32_t) re.se & 0x7fff, re.m);
+        r.im = x87_make(x.im, (im.se >> 15) & 1, (uint32_t) im.se & 0x7fff, im.m);
+        return ok ? r : x;
+    }
     static MPIX_SDEV X87C apply(X87C x, X87C y, const Params &)
     {
         X87 a = x.re, b = x.im, c = y.re, d = y.im;

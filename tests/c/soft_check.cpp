@@ -35,9 +35,34 @@ struct QuadSumGeneral {
     static Quad apply(Quad a, Quad b, const Params &) { return quad_add<false>(a, b, false); }
 };
 
+// a split combiner as the kernels run it: apply_fast, and where it declined
+// (the unit must come back unchanged) the full apply -- returns -2 when a
+// declined unit came back changed
+template <class C>
+static int run_split(const void *in, void *inout, long n)
+{
+    typedef typename C::unit T;
+    const Params prm{1, 0};
+    for (long i = 0; i < n; ++i) {
+        T a, b;
+        memcpy(&a, (const char *) inout + i * sizeof(T), sizeof(T));
+        memcpy(&b, (const char *) in + i * sizeof(T), sizeof(T));
+        bool ok = false;
+        T r = C::apply_fast(a, b, prm, ok);
+        if (!ok) {
+            if (memcmp(&r, &a, sizeof(T)))
+                return -2;
+            r = C::apply(a, b, prm);
+        }
+        memcpy((char *) inout + i * sizeof(T), &r, sizeof(T));
+    }
+    return 0;
+}
+
 // which: 0 x87 SUM, 1 x87 PROD, 2 binary128 SUM, 3 binary128 PROD,
 // 4 binary128 complex SUM, 5 binary128 complex PROD, 6 x87 complex SUM, 7 x87 complex PROD,
-// 8 x87 SUM general path only, 9 binary128 SUM general path only
+// 8 x87 SUM general path only, 9 binary128 SUM general path only,
+// 10 binary128 complex PROD split form, 11 x87 complex PROD split form
 extern "C" int soft_reduce(int which, const void *in, void *inout, long n)
 {
     switch (which) {
@@ -51,6 +76,8 @@ extern "C" int soft_reduce(int which, const void *in, void *inout, long n)
         case 7: run<X87CProd>(in, inout, n); return 0;
         case 8: run<X87SumGeneral>(in, inout, n); return 0;
         case 9: run<QuadSumGeneral>(in, inout, n); return 0;
+        case 10: return run_split<QuadCProd>(in, inout, n);
+        case 11: return run_split<X87CProd>(in, inout, n);
     }
     return -1;
 }

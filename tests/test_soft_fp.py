@@ -169,11 +169,12 @@ def test_quad_random(soft, oracle, which, op, kind):
 
 
 @pytest.mark.parametrize('which,dt,op', [(4, COMPLEX32, MPI_SUM), (5, COMPLEX32, MPI_PROD),
-                                         (6, C_LD_COMPLEX, MPI_SUM), (7, C_LD_COMPLEX, MPI_PROD)])
+                                         (6, C_LD_COMPLEX, MPI_SUM), (7, C_LD_COMPLEX, MPI_PROD),
+                                         (10, COMPLEX32, MPI_PROD), (11, C_LD_COMPLEX, MPI_PROD)])
 def test_complex(soft, oracle, which, dt, op):
     rng = np.random.default_rng(0x5EED0840 + which)
     n = 200000
-    if which in (6, 7):
+    if which in (6, 7, 11):
         parts = [x87_random(rng, n, close=True) for _ in range(4)]
         sp = np.stack(x87_specials())
     else:
@@ -187,13 +188,14 @@ def test_complex(soft, oracle, which, dt, op):
     _check(soft, oracle, which, dt, op, a, b, 32)
 
 
-@pytest.mark.parametrize('which,dt', [(7, C_LD_COMPLEX), (5, COMPLEX32)])
+@pytest.mark.parametrize('which,dt', [(7, C_LD_COMPLEX), (5, COMPLEX32), (11, C_LD_COMPLEX),
+                                      (10, COMPLEX32)])
 def test_complex_prod_special_parts(soft, oracle, which, dt):
     """every (a, b, c, d) of 9 special parts: the Annex G recovery branches
     of __mulxc3 (inf boxed, NaNs zeroed, overflowed products) for x87, the
     plain struct formula for binary128"""
     J = 1 << 63
-    if which == 7:
+    if which in (7, 11):
         parts = [x87(0, 0, 0), x87(1, 0x3fff, J), x87(0, 0x7fff, J), x87(1, 0x7fff, J),
                  x87(0, 0x7fff, J | (1 << 62) | 3), x87(0, 0x7ffe, J), x87(1, 0x3ffe, J | 5),
                  x87(0, 0x3fff, 1 << 62), x87(1, 0, 3)]
@@ -207,7 +209,7 @@ def test_complex_prod_special_parts(soft, oracle, which, dt):
     a = np.concatenate([P[idx[0]], P[idx[1]]], axis=1)
     b = np.concatenate([P[idx[2]], P[idx[3]]], axis=1)
     rng = np.random.default_rng(0x5EED0850 + which)
-    if which == 7:          # random padding in both parts of both operands
+    if which in (7, 11):    # random padding in both parts of both operands
         for X in (a, b):
             X[:, 10:16] = rng.integers(0, 256, (len(X), 6), dtype=np.uint8)
             X[:, 26:32] = rng.integers(0, 256, (len(X), 6), dtype=np.uint8)
@@ -314,3 +316,62 @@ def test_sum_fast_path_equals_general_path(soft, oracle, fast, general, dt, ext_
         got[which] = r
     assert np.array_equal(got[fast], got[general])
     _check(soft, oracle, general, dt, MPI_SUM, a, b, 16)
+
+
+def _with_exponents(rng, base_a, base_b, enc, n=4000):
+    """n copies of one operand pair with random signs and exponent offsets
+    (the same offset on both keeps a sum's alignment; products may reach the
+    ends of the exponent range and leave the fast path)"""
+    a = np.repeat(base_a[None], n, 0).copy()
+    b = np.repeat(base_b[None], n, 0).copy()
+    if enc == 'x87':
+        off = rng.integers(-16000, 16000, n)
+        for X in (a, b):
+            se = X[:, 8:10].copy().view(np.uint16).reshape(-1).astype(np.int64)
+            e = np.clip((se & 0x7fff) + off, 1, 0x7ffe)
+            s = rng.integers(0, 2, n) << 15
+            X[:, 8:10] = (s | e).astype(np.uint16).view(np.uint8).reshape(n, 2)
+    else:
+        off = rng.integers(-16000, 16000, n)
+        for X in (a, b):
+            hi = X[:, 8:].copy().view(np.uint64).reshape(-1)
+            e = np.clip(((hi >> np.uint64(48)) & np.uint64(0x7fff)).astype(np.int64) + off, 1, 0x7ffe)
+            s = rng.integers(0, 2, n).astype(np.uint64) << np.uint64(63)
+            hi = s | (e.astype(np.uint64) << np.uint64(48)) | (hi & np.uint64((1 << 48) - 1))
+            X[:, 8:] = hi.view(np.uint8).reshape(n, 8)
+    return a, b
+
+
+@pytest.mark.parametrize('case', ['quad_prod', 'x87_prod', 'quad_sum', 'x87_sum'])
+def test_rounding_carries_out_of_the_significand(soft, oracle, case):
+    """operands whose exactly rounded result carries out of the significand
+    (all ones + round up -> the next power of two): the 32-bit-limb fast
+    paths' overflow step, against the oracle.  binary128 product: (1 + 2^-112)
+    x (2 - 2^-111) = 2 - 2^-223 -> 2; x87: (1 + 2^-63) x (2 - 2^-62); sums:
+    (2 - ulp) + ulp / 2, a tie to even that rounds up"""
+    rng = np.random.default_rng(0x5EED08A0 + len(case))
+    J = 1 << 63
+    if case == 'quad_prod':
+        a0, b0 = quad(0, 0x3fff, 0, 1), quad(0, 0x3fff, (1 << 48) - 1, (1 << 64) - 2)
+    elif case == 'x87_prod':
+        a0, b0 = x87(0, 0x3fff, J | 1), x87(0, 0x3fff, (1 << 64) - 2)
+    elif case == 'quad_sum':
+        a0, b0 = quad(0, 0x3fff, (1 << 48) - 1, (1 << 64) - 1), quad(0, 0x3fff - 113, 0, 0)
+    else:
+        a0, b0 = x87(0, 0x3fff, (1 << 64) - 1), x87(0, 0x3fff - 64, J)
+    enc = 'x87' if case.startswith('x87') else 'quad'
+    a, b = _with_exponents(rng, a0, b0, enc)
+    if case.endswith('sum'):        # a sum keeps its operands' signs equal (no cancellation)
+        b[:, 9 if enc == 'x87' else 15] = (b[:, 9 if enc == 'x87' else 15] & 0x7f) | \
+            (a[:, 9 if enc == 'x87' else 15] & 0x80)
+    which = {'quad_prod': 3, 'x87_prod': 1, 'quad_sum': 2, 'x87_sum': 0}[case]
+    dt = LD if enc == 'x87' else REAL16
+    op = MPI_PROD if case.endswith('prod') else MPI_SUM
+    _check(soft, oracle, which, dt, op, a, b, 16)
+    # the unscaled pair itself lands on the next power of two
+    r = a0.copy()
+    assert soft.soft_reduce(which, b0.ctypes.data, r.ctypes.data, 1) == 0
+    if enc == 'quad':
+        assert r[:8].view(np.uint64)[0] == 0 and r[8:].view(np.uint64)[0] == (0x4000 << 48), r
+    else:
+        assert r[:8].view(np.uint64)[0] == J and r[8:10].view(np.uint16)[0] == 0x4000, r

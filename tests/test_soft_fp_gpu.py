@@ -129,3 +129,95 @@ def test_fast_path_rounding_ties(R, oracle, name, dt, op, short, ba, bb):
             hb = (hb & ~np.uint64(0x7fff << 48)) | (eb << np.uint64(48))
             b[:, 8:] = hb.view(np.uint8).reshape(n, 8)
     _gpu_vs_oracle(R, oracle, dt, op, a, b, 16)
+
+
+# ------------------------------------------------ split combiners (round 6)
+# The soft complex products run their normal-operand fast paths in the
+# streaming kernel and leave any unit where one declined unchanged, recorded
+# in a per-(device, stream) word buffer; a second launch combines those units
+# with the general paths (redop_kernels.h is_split, k_fixup32).  Every entry
+# that reaches k_contig32 -- the synchronous and stream-ordered calls, the
+# two-slot tree into a separate output (recursive halving's combine_to), the
+# batch -- on ragged counts (a partial last tile), declined units placed at
+# word edges and inside full and partial tiles, and a buffer that grows
+# between calls on one stream.
+def _split_operands(rng, dt, n, special_at):
+    x87 = dt == S.C_LD_COMPLEX
+    gen = (lambda: S.x87_random(rng, n, True)) if x87 else (lambda: S.quad_random(rng, n, True))
+    sp = np.stack(S.x87_specials() if x87 else S.quad_specials())
+    parts = [gen() for _ in range(4)]
+    for i, u in enumerate(special_at):
+        parts[i % 4][u] = sp[rng.integers(0, len(sp))]
+    return np.concatenate(parts[:2], axis=1), np.concatenate(parts[2:], axis=1)
+
+
+def _oracle_prod(oracle, dt, a, b):
+    n = len(a)
+    want = a.reshape(-1).copy()
+    assert oracle.reduce_local(b.reshape(-1).copy(), want, n, dt, S.MPI_PROD) == 0
+    return want
+
+
+def _same(got, want, n, what):
+    bad = np.flatnonzero((got.reshape(n, 32) != want.reshape(n, 32)).any(1))
+    assert bad.size == 0, (what, '%d of %d differ' % (bad.size, n), bad[:6])
+
+
+@pytest.mark.parametrize('dt', [S.COMPLEX32, S.C_LD_COMPLEX], ids=['complex32', 'c_long_double'])
+def test_split_product_every_entry(R, oracle, dt):
+    import ctypes
+    rng = np.random.default_rng(0x5EED0930 + dt)
+    s = torch.cuda.current_stream()
+    for n in (37, 64, 4099, 70001):
+        special_at = sorted({0, 63, 64, n - 1, n // 2, n // 3} | set(rng.integers(0, n, 40).tolist()))
+        special_at = [u for u in special_at if u < n]
+        a, b = _split_operands(rng, dt, n, special_at)
+        want = _oracle_prod(oracle, dt, a, b)
+        # synchronous, in place
+        da, db = dev(a), dev(b)
+        assert R.MPI_Reduce_local(db, da, n, dt, S.MPI_PROD) == 0
+        _same(da.cpu().numpy(), want, n, ('sync', n))
+        # stream-ordered, in place
+        da = dev(a)
+        assert R.reduce_local_async(db, da, n, dt, S.MPI_PROD, s) == 0
+        s.synchronize()
+        _same(da.cpu().numpy(), want, n, ('async', n))
+        # two-slot tree into a separate output: out = slot0 OP slot1 (slot 0
+        # in the inout role), both slots left as they were
+        da = dev(a)
+        out = torch.full_like(da, 0x5A)
+        assert R.reduce_local_tree_async([da, db], out, n, dt, S.MPI_PROD, s) == 0
+        s.synchronize()
+        _same(out.cpu().numpy(), want, n, ('tree', n))
+        assert np.array_equal(da.cpu().numpy(), a.reshape(-1).view(np.uint8)), ('tree slot 0', n)
+        # batch: this call's triple beside a small one of the same type
+        da = dev(a)
+        a2, b2 = _split_operands(rng, dt, 5, [2])
+        want2 = _oracle_prod(oracle, dt, a2, b2)
+        da2, db2 = dev(a2), dev(b2)
+        ins = (ctypes.c_void_p * 2)(db2.data_ptr(), db.data_ptr())
+        ios = (ctypes.c_void_p * 2)(da2.data_ptr(), da.data_ptr())
+        cnt = (ctypes.c_ssize_t * 2)(5, n)
+        assert R.lib().MPIX_Reduce_local_batch_async(ins, ios, cnt, 2, dt, S.MPI_PROD,
+                                                     s.cuda_stream) == 0
+        s.synchronize()
+        _same(da.cpu().numpy(), want, n, ('batch', n))
+        _same(da2.cpu().numpy(), want2, 5, ('batch small', n))
+
+
+def test_split_fixup_buffer_grows_on_a_stream(R, oracle):
+    """a small call, then one needing a larger word buffer on the same
+    stream (the library synchronises the stream and reallocates), then the
+    small one again -- each against the oracle"""
+    rng = np.random.default_rng(0x5EED0940)
+    s = torch.cuda.Stream()
+    dt = S.COMPLEX32
+    for n in (1000, (1 << 20) + 17, 1000):      # the middle one needs > 64 KiB of words
+        special_at = [0, n - 1] + rng.integers(0, n, 16).tolist()
+        a, b = _split_operands(rng, dt, n, special_at)
+        want = _oracle_prod(oracle, dt, a, b)
+        da, db = dev(a), dev(b)
+        with torch.cuda.stream(s):
+            assert R.reduce_local_async(db, da, n, dt, S.MPI_PROD, s) == 0
+        s.synchronize()
+        _same(da.cpu().numpy(), want, n, ('grow', n))

@@ -48,13 +48,13 @@ __global__ void fill(float *p, uint64_t n, uint32_t seed)
 template <int KMAX, int U, unsigned B = 256> void tree(const MultiIn<float> &mi, int k, float *o,
                                                         uint64_t npk, const Params &p, hipStream_t s)
 {
-    hipLaunchKernelGGL((k_contig_tree<C, KMAX, U>), dim3(grid_for(B * U, npk, 0)), dim3(B), 0, s,
+    hipLaunchKernelGGL((k_contig_tree<C, KMAX, U>), dim3(grid_for(B * U, npk, 0, B)), dim3(B), 0, s,
                        mi, k, (1u << k) - 1, o, 0, npk, npk * 4, 0, p);
 }
 template <int KMAX, int U, unsigned B = 256> void rec(const MultiIn<float> &mi, int k, float *o,
                                                        uint64_t npk, const Params &p, hipStream_t s)
 {
-    hipLaunchKernelGGL((k_contig_tree_rec<C, KMAX, U>), dim3(grid_for(B * U, npk, 0)), dim3(B), 0,
+    hipLaunchKernelGGL((k_contig_tree_rec<C, KMAX, U>), dim3(grid_for(B * U, npk, 0, B)), dim3(B), 0,
                        s, mi, k, (1u << k) - 1, o, 0, npk, npk * 4, 0, p);
 }
 template <int U, unsigned B = 256> void multi(const MultiIn<float> &mi, int k, float *o, uint64_t npk,
@@ -64,7 +64,7 @@ template <int U, unsigned B = 256> void multi(const MultiIn<float> &mi, int k, f
     MultiIn<float> m{};
     for (int q = 1; q < k; ++q)
         m.p[q - 1] = mi.p[q];
-    const unsigned g = grid_for(B * U, npk, 0);
+    const unsigned g = grid_for(B * U, npk, 0, B);
     hipLaunchKernelGGL((k_contig_multi<C, U>), dim3(g), dim3(B), 0, s, m, k - 1, o, 0, npk, npk * 4,
                        0, p, g, B);
 }
@@ -73,7 +73,7 @@ template <int U, unsigned B = 256> void multi(const MultiIn<float> &mi, int k, f
 template <int U, unsigned B = 256> void contig(const MultiIn<float> &mi, int, float *o, uint64_t npk,
                                                const Params &p, hipStream_t s)
 {
-    const unsigned g = grid_for(B * U, npk, 0);
+    const unsigned g = grid_for(B * U, npk, 0, B);
     hipLaunchKernelGGL((k_contig<C, U, true, true, true>), dim3(g), dim3(B), 0, s, mi.p[0], o, 0, npk,
                        npk * 4, 0, p, g, B);
 }
