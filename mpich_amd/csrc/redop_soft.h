@@ -630,8 +630,8 @@ MPIX_SDEV bool quad_mul_fast(const Quad &x, const Quad &y, Quad *r)
         // the 113-bit result is at bit 112 + top (the general path's shifts
         // constant).  The significands as four 29-bit digits: a digit
         // product is < 2^58, so a column of at most four sums in 64 bits
-        // with no carry between the 16 multiply-adds; one carry pass turns
-        // the columns into digits d0..d7, and the significand is the value
+        // with no carry between the 16 multiply-adds; each column starts from
+        // the previous one's carry, giving the digits d0..d7; the significand is the value
         // above 2^87 (digits 3..7, V) shifted right by 25 + top -- the digits
         // below only decide the sticky bit.  A denormal or overflowing result
         // takes the general path.
@@ -644,21 +644,17 @@ MPIX_SDEV bool quad_mul_fast(const Quad &x, const Quad &y, Quad *r)
                                funnel_r(x3, x2, 23)};
         const uint32_t b[4] = {y0 & M29, funnel_r(y1, y0, 29) & M29, funnel_r(y2, y1, 26) & M29,
                                funnel_r(y3, y2, 23)};
-        uint64_t col[7];
-#pragma unroll
-        for (int c = 0; c < 7; ++c) {
-            uint64_t acc = 0;
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                if (c - i >= 0 && c - i < 4)
-                    acc += (uint64_t) a[i] * b[c - i];
-            col[c] = acc;
-        }
+        // column c, with the carry of column c - 1 as the first addend of its
+        // multiply-add chain: < 4 x 2^58 + 2^35 < 2^61
         uint32_t d[8];
         uint64_t t = 0;
 #pragma unroll
         for (int c = 0; c < 7; ++c) {
-            t = col[c] + (t >> 29);
+            t >>= 29;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (c - i >= 0 && c - i < 4)
+                    t += (uint64_t) a[i] * b[c - i];
             d[c] = (uint32_t) t & M29;
         }
         d[7] = (uint32_t) (t >> 29);            // < 2^23

@@ -5,7 +5,9 @@ complex products are the slowest rows) for ONE build of libmpix_redop.so, at
 same operands), kernel only by HIP events, median of 3 batches of 3; the
 fp32 SUM row of the same process beside them.  One JSON line.
 
-usage: soft_rows.py LIBPATH LABEL   (run alternately for two builds)"""
+usage: soft_rows.py LIBPATH LABEL [TYPE:OP ...]   (run alternately for two
+builds; TYPE:OP pairs, e.g. MPI_COMPLEX32:MPI_PROD, restrict the rows -- a
+profiler pass over one kernel)"""
 import ctypes
 import json
 import os
@@ -49,6 +51,7 @@ def main():
     _, med, _ = bench.event_time_per_launch(lambda: call(fb, fa, n, H.MPI_FLOAT, H.MPI_SUM, s), 3, s,
                                             rounds=3)
     rows.append(dict(type='MPI_FLOAT', op='MPI_SUM', GBs=round(3 * nbytes / (med * 1e-3) / 1e9, 1)))
+    only = set(sys.argv[3:])
     for tn in ('MPI_LONG_DOUBLE', 'MPI_REAL16', 'MPI_C_LONG_DOUBLE_COMPLEX', 'MPI_COMPLEX32'):
         enc = 'x87' if 'LONG_DOUBLE' in tn else 'binary128'
         bench.fill_soft_slots(b8, enc, 0x5EED0004)
@@ -56,6 +59,8 @@ def main():
         ext = L.MPIX_Datatype_extent(H.as_c_int(dt))
         m = nbytes // ext
         for on in ('MPI_SUM', 'MPI_PROD'):
+            if only and '%s:%s' % (tn, on) not in only:
+                continue
             op = getattr(H, on)
             bench.fill_soft_slots(a8, enc, 0x5EED0003)
             torch.cuda.synchronize()
