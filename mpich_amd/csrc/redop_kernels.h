@@ -934,7 +934,8 @@ hipError_t launch_contig32(const typename C::unit *in, const typename C::unit *i
     hipLaunchKernelGGL((k_contig32<C, U32, MPIX_REDOP_NT_LOAD, MPIX_REDOP_NT_STORE>), dim3(grid),
                        dim3(kContig32Block), 0, s, in, io, out, count, p, grid, kContig32Block);
     if constexpr (is_split<C>::value) {
-        const unsigned g2 = grid_for(256, (count + 63) / 64, 1024, 256);
+        // a word per lane: the scan is one load per lane, mostly of zeros
+        const unsigned g2 = grid_for(256, (count + 63) / 64, 0, 256);
         hipLaunchKernelGGL((k_fixup32<C>), dim3(g2), dim3(256), 0, s, in, io, out, count, p, g2);
     }
     return hipGetLastError();

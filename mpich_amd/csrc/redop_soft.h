@@ -32,11 +32,6 @@
 
 #include <stdint.h>
 
-// the complex product's fast path with quad_mul_fast_wide's products (1) or
-// quad_mul_fast's digits (0)
-#ifndef MPIX_QUAD_CMUL_WIDE
-#define MPIX_QUAD_CMUL_WIDE 0
-#endif
 
 #include "redop_dispatch.h"
 
@@ -492,6 +487,53 @@ MPIX_SDEV Quad quad_from_round(bool s, u128 S, int64_t E0)
 }
 
 // x + y (sub: x - y): __addtf3 / __subtf3
+// A binary128 value in limbs: the significand q (implicit one at bit 112 of
+// the four 32-bit limbs), its biased exponent e and sign s -- a product's
+// result before it is packed, or an operand unpacked, for the sums
+struct QLimbs {
+    uint32_t q[4];
+    uint32_t e, s;
+};
+
+MPIX_SDEV QLimbs quad_limbs(const Quad &x)
+{
+    QLimbs r;
+    r.q[0] = (uint32_t) x.lo;
+    r.q[1] = (uint32_t) (x.lo >> 32);
+    r.q[2] = (uint32_t) x.hi;
+    r.q[3] = ((uint32_t) (x.hi >> 32) & 0xffffu) | 0x10000u;
+    r.e = (uint32_t) (x.hi >> 48) & 0x7fff;
+    r.s = (uint32_t) (x.hi >> 63);
+    return r;
+}
+
+// x + y (sub: x - y) of two normal values in limbs whose sum is normal: *r
+// (packed) and true; false for anything else (quad_add's general path)
+MPIX_SDEV bool quad_add_limbs(const QLimbs &x, const QLimbs &y, bool sub, Quad *r)
+{
+    // magnitudes ordered by (exponent, significand): two 64-bit keys each
+    const uint64_t kx = ((uint64_t) ((x.e << 17) | x.q[3]) << 32) | x.q[2];
+    const uint64_t ky = ((uint64_t) ((y.e << 17) | y.q[3]) << 32) | y.q[2];
+    const uint64_t lx = ((uint64_t) x.q[1] << 32) | x.q[0], ly = ((uint64_t) y.q[1] << 32) | y.q[0];
+    const bool swap = kx < ky || (kx == ky && lx < ly);
+    const uint32_t sy = y.s ^ (sub ? 1u : 0u);
+    const uint32_t sa = swap ? sy : x.s, sb = swap ? x.s : sy;
+    const QLimbs &big = swap ? y : x, &small = swap ? x : y;
+    const uint32_t xa = big.e, d = big.e - small.e;
+    // significand << 14: the leading bit at 126
+    const uint32_t A[4] = {big.q[0] << 14, funnel_l(big.q[1], big.q[0], 14),
+                           funnel_l(big.q[2], big.q[1], 14), funnel_l(big.q[3], big.q[2], 14)};
+    uint32_t B[4] = {small.q[0] << 14, funnel_l(small.q[1], small.q[0], 14),
+                     funnel_l(small.q[2], small.q[1], 14), funnel_l(small.q[3], small.q[2], 14)};
+    uint32_t q[4];
+    int32_t e;
+    if (!add_normal_limbs<113>(A, B, d < 127u ? d : 127u, sa != sb, (int32_t) xa, q, &e))
+        return false;
+    r->lo = ((uint64_t) q[1] << 32) | q[0];
+    r->hi = ((uint64_t) sa << 63) | ((uint64_t) e << 48) | ((uint64_t) (q[3] & 0xffffu) << 32) | q[2];
+    return true;
+}
+
 // x + y (sub: x - y) of two normal operands whose sum is normal: *r and
 // true; false for anything else (quad_add's general path decides)
 MPIX_SDEV bool quad_add_fast(const Quad &x, const Quad &y, bool sub, Quad *r)
@@ -499,33 +541,7 @@ MPIX_SDEV bool quad_add_fast(const Quad &x, const Quad &y, bool sub, Quad *r)
     const uint32_t ex = (uint32_t) (x.hi >> 48) & 0x7fff, ey = (uint32_t) (y.hi >> 48) & 0x7fff;
     if (!(ex - 1u < 0x7ffeu && ey - 1u < 0x7ffeu))
         return false;
-    {
-        // both normal: as x87_add's fast path (magnitudes ordered by the
-        // encoding without its sign bit)
-        const uint64_t hx = x.hi & ~(1ull << 63), hy = y.hi & ~(1ull << 63);
-        const bool swap = hx < hy || (hx == hy && x.lo < y.lo);
-        const bool sx = x.hi >> 63, sy = (bool) (y.hi >> 63) ^ sub;
-        const bool sa = swap ? sy : sx, sb = swap ? sx : sy;
-        const uint64_t bh = swap ? hy : hx, bl = swap ? y.lo : x.lo;
-        const uint64_t th = swap ? hx : hy, tl = swap ? x.lo : y.lo;
-        const uint32_t xa = (uint32_t) (bh >> 48), d = xa - (uint32_t) (th >> 48);
-        // (implicit one | fraction) << 14: the leading bit at 126
-        const uint32_t a0 = (uint32_t) bl, a1 = (uint32_t) (bl >> 32), a2 = (uint32_t) bh;
-        const uint32_t a3 = ((uint32_t) (bh >> 32) & 0xffffu) | 0x10000u;
-        const uint32_t b0 = (uint32_t) tl, b1 = (uint32_t) (tl >> 32), b2 = (uint32_t) th;
-        const uint32_t b3 = ((uint32_t) (th >> 32) & 0xffffu) | 0x10000u;
-        const uint32_t A[4] = {a0 << 14, funnel_l(a1, a0, 14), funnel_l(a2, a1, 14),
-                               funnel_l(a3, a2, 14)};
-        uint32_t B[4] = {b0 << 14, funnel_l(b1, b0, 14), funnel_l(b2, b1, 14), funnel_l(b3, b2, 14)};
-        uint32_t q[4];
-        int32_t e;
-        if (!add_normal_limbs<113>(A, B, d < 127u ? d : 127u, sa != sb, (int32_t) xa, q, &e))
-            return false;
-        r->lo = ((uint64_t) q[1] << 32) | q[0];
-        r->hi = ((uint64_t) sa << 63) | ((uint64_t) e << 48) | ((uint64_t) (q[3] & 0xffffu) << 32) |
-                q[2];
-        return true;
-    }
+    return quad_add_limbs(quad_limbs(x), quad_limbs(y), sub, r);
 }
 
 template <bool FAST = true>
@@ -616,73 +632,96 @@ MPIX_SDEV bool quad_mul_fast_wide(const Quad &x, const Quad &y, Quad *r)
     return true;
 }
 
+// A binary128 operand as four 29-bit digits of its significand (the
+// implicit one included: a[3] has 26 bits), biased exponent and sign
+struct QDigits {
+    uint32_t a[4];
+    uint32_t e, s;
+};
+
+MPIX_SDEV QDigits quad_digits(const Quad &x)
+{
+    constexpr uint32_t M29 = (1u << 29) - 1u;
+    const uint32_t x0 = (uint32_t) x.lo, x1 = (uint32_t) (x.lo >> 32), x2 = (uint32_t) x.hi;
+    const uint32_t x3 = ((uint32_t) (x.hi >> 32) & 0xffffu) | 0x10000u;
+    QDigits r;
+    r.a[0] = x0 & M29;
+    r.a[1] = funnel_r(x1, x0, 29) & M29;
+    r.a[2] = funnel_r(x2, x1, 26) & M29;
+    r.a[3] = funnel_r(x3, x2, 23);
+    r.e = (uint32_t) (x.hi >> 48) & 0x7fff;
+    r.s = (uint32_t) (x.hi >> 63);
+    return r;
+}
+
+// The product of two normal operands' digits, rounded (RNE) to 113 bits, in
+// limbs: *r and true when it is normal; false otherwise.  The significands
+// in [2^112, 2^113), the product in [2^224, 2^226) with its leading bit at
+// 224 + top, so the cut is at bit 112 + top.  A digit product is < 2^58, so a
+// column of at most four sums in 64 bits with no carry between the 16
+// multiply-adds; each column's chain starts from the previous column's
+// carry, giving the product's digits d0..d7; the significand is four funnel
+// shifts of the digits above 2^87 (V), those below only feed the sticky bit.
+MPIX_SDEV bool quad_mul_digits(const QDigits &x, const QDigits &y, QLimbs *r)
+{
+    constexpr uint32_t M29 = (1u << 29) - 1u;
+    // column c, with the carry of column c - 1 as the first addend of its
+    // multiply-add chain: < 4 x 2^58 + 2^35 < 2^61
+    uint32_t d[8];
+    uint64_t t = 0;
+#pragma unroll
+    for (int c = 0; c < 7; ++c) {
+        t >>= 29;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (c - i >= 0 && c - i < 4)
+                t += (uint64_t) x.a[i] * y.a[c - i];
+        d[c] = (uint32_t) t & M29;
+    }
+    d[7] = (uint32_t) (t >> 29);                // < 2^23
+    // V = digits 3..7 as 32-bit words (bits 87.. of the product)
+    const uint32_t v[5] = {d[3] | (d[4] << 29), (d[4] >> 3) | (d[5] << 26),
+                           (d[5] >> 6) | (d[6] << 23), (d[6] >> 9) | (d[7] << 20), d[7] >> 12};
+    const uint32_t top = d[7] >> 22;            // leading bit 225 (1) or 224 (0)
+    const uint32_t c = 25u + top;               // the cut, bit 112 + top of the product
+    uint32_t *q = r->q;
+    q[0] = funnel_r(v[1], v[0], c);
+    q[1] = funnel_r(v[2], v[1], c);
+    q[2] = funnel_r(v[3], v[2], c);
+    q[3] = funnel_r(v[4], v[3], c);
+    const uint32_t rnd = (v[0] >> (c - 1u)) & 1u;
+    const uint32_t sticky = (v[0] & ((1u << (c - 1u)) - 1u)) | d[2] | d[1] | d[0];
+    uint64_t k = rnd & ((sticky != 0) | (q[0] & 1u));
+    for (int i = 0; i < 4; ++i) {
+        k += q[i];
+        q[i] = (uint32_t) k;
+        k >>= 32;
+    }
+    int32_t E = (int32_t) (x.e + y.e + top) - 16383;
+    if (q[3] >> 17) {                   // carried out of the significand: 2^113
+        q[3] = 0x10000u;                // (q[0..2] are 0)
+        E += 1;
+    }
+    r->e = (uint32_t) E;
+    r->s = x.s ^ y.s;
+    return E >= 1 && E <= 0x7ffe;
+}
+
 // x * y of two normal operands whose product is normal: *r and true; false
 // for anything else.  The same product as quad_mul_fast_wide in fewer
-// instructions: 29-bit digits, no carry between the multiply-adds
+// instructions (quad_mul_digits)
 MPIX_SDEV bool quad_mul_fast(const Quad &x, const Quad &y, Quad *r)
 {
     const uint32_t ex = (uint32_t) (x.hi >> 48) & 0x7fff, ey = (uint32_t) (y.hi >> 48) & 0x7fff;
     if (!(ex - 1u < 0x7ffeu && ey - 1u < 0x7ffeu))
         return false;
-    {
-        // both normal: significands in [2^112, 2^113), the product in
-        // [2^224, 2^226) with its leading bit at 224 + top, so the cut below
-        // the 113-bit result is at bit 112 + top (the general path's shifts
-        // constant).  The significands as four 29-bit digits: a digit
-        // product is < 2^58, so a column of at most four sums in 64 bits
-        // with no carry between the 16 multiply-adds; each column starts from
-        // the previous one's carry, giving the digits d0..d7; the significand is the value
-        // above 2^87 (digits 3..7, V) shifted right by 25 + top -- the digits
-        // below only decide the sticky bit.  A denormal or overflowing result
-        // takes the general path.
-        constexpr uint32_t M29 = (1u << 29) - 1u;
-        const uint32_t x0 = (uint32_t) x.lo, x1 = (uint32_t) (x.lo >> 32), x2 = (uint32_t) x.hi;
-        const uint32_t x3 = ((uint32_t) (x.hi >> 32) & 0xffffu) | 0x10000u;
-        const uint32_t y0 = (uint32_t) y.lo, y1 = (uint32_t) (y.lo >> 32), y2 = (uint32_t) y.hi;
-        const uint32_t y3 = ((uint32_t) (y.hi >> 32) & 0xffffu) | 0x10000u;
-        const uint32_t a[4] = {x0 & M29, funnel_r(x1, x0, 29) & M29, funnel_r(x2, x1, 26) & M29,
-                               funnel_r(x3, x2, 23)};
-        const uint32_t b[4] = {y0 & M29, funnel_r(y1, y0, 29) & M29, funnel_r(y2, y1, 26) & M29,
-                               funnel_r(y3, y2, 23)};
-        // column c, with the carry of column c - 1 as the first addend of its
-        // multiply-add chain: < 4 x 2^58 + 2^35 < 2^61
-        uint32_t d[8];
-        uint64_t t = 0;
-#pragma unroll
-        for (int c = 0; c < 7; ++c) {
-            t >>= 29;
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                if (c - i >= 0 && c - i < 4)
-                    t += (uint64_t) a[i] * b[c - i];
-            d[c] = (uint32_t) t & M29;
-        }
-        d[7] = (uint32_t) (t >> 29);            // < 2^23
-        // V = digits 3..7 as 32-bit words (bits 87.. of the product)
-        const uint32_t v[5] = {d[3] | (d[4] << 29), (d[4] >> 3) | (d[5] << 26),
-                               (d[5] >> 6) | (d[6] << 23), (d[6] >> 9) | (d[7] << 20), d[7] >> 12};
-        const uint32_t top = d[7] >> 22;        // leading bit 225 (1) or 224 (0)
-        const uint32_t c = 25u + top;           // the cut, bit 112 + top of the product
-        uint32_t q[4] = {funnel_r(v[1], v[0], c), funnel_r(v[2], v[1], c), funnel_r(v[3], v[2], c),
-                         funnel_r(v[4], v[3], c)};
-        const uint32_t rnd = (v[0] >> (c - 1u)) & 1u;
-        const uint32_t sticky = (v[0] & ((1u << (c - 1u)) - 1u)) | d[2] | d[1] | d[0];
-        uint64_t k = rnd & ((sticky != 0) | (q[0] & 1u));
-        for (int i = 0; i < 4; ++i) {
-            k += q[i];
-            q[i] = (uint32_t) k;
-            k >>= 32;
-        }
-        int32_t E = (int32_t) (ex + ey + top) - 16383;
-        if (q[3] >> 17) {               // carried out of the significand: 2^113
-            q[3] = 0x10000u;            // (q[0..2] are 0)
-            E += 1;
-        }
-        r->lo = ((uint64_t) q[1] << 32) | q[0];
-        r->hi = (((x.hi ^ y.hi) >> 63) << 63) | ((uint64_t) E << 48) |
-                ((uint64_t) (q[3] & 0xffffu) << 32) | q[2];
-        return E >= 1 && E <= 0x7ffe;
-    }
+    QLimbs p;
+    if (!quad_mul_digits(quad_digits(x), quad_digits(y), &p))
+        return false;
+    r->lo = ((uint64_t) p.q[1] << 32) | p.q[0];
+    r->hi = ((uint64_t) p.s << 63) | ((uint64_t) p.e << 48) | ((uint64_t) (p.q[3] & 0xffffu) << 32) |
+            p.q[2];
+    return true;
 }
 
 // x * y: __multf3 (the 226-bit product folded to 128 bits plus a sticky bit)
@@ -776,20 +815,20 @@ struct QuadCProd {
     }
     static MPIX_SDEV QuadC apply_fast(QuadC c, QuadC b, const Params &, bool &ok)
     {
+        // each operand's digits once (every one feeds two products), the
+        // products kept in limbs for the sums (no pack / unpack between)
+        const QDigits cr = quad_digits(c.re), ci = quad_digits(c.im);
+        const QDigits br = quad_digits(b.re), bi = quad_digits(b.im);
+        ok = cr.e - 1u < 0x7ffeu && ci.e - 1u < 0x7ffeu && br.e - 1u < 0x7ffeu &&
+             bi.e - 1u < 0x7ffeu;
         QuadC r;
-        Quad p0, p1, p2, p3;
-#if MPIX_QUAD_CMUL_WIDE
-#define MPIX_QMF quad_mul_fast_wide
-#else
-#define MPIX_QMF quad_mul_fast
-#endif
-        ok = MPIX_QMF(c.re, b.re, &p0);
-        ok &= MPIX_QMF(c.im, b.im, &p1);
-        ok &= quad_add_fast(p0, p1, true, &r.re);
-        ok &= MPIX_QMF(c.im, b.re, &p2);
-        ok &= MPIX_QMF(c.re, b.im, &p3);
-#undef MPIX_QMF
-        ok &= quad_add_fast(p2, p3, false, &r.im);
+        QLimbs p0, p1, p2, p3;
+        ok &= quad_mul_digits(cr, br, &p0);
+        ok &= quad_mul_digits(ci, bi, &p1);
+        ok &= quad_add_limbs(p0, p1, true, &r.re);
+        ok &= quad_mul_digits(ci, br, &p2);
+        ok &= quad_mul_digits(cr, bi, &p3);
+        ok &= quad_add_limbs(p2, p3, false, &r.im);
         return ok ? r : c;
     }
 };
