@@ -79,7 +79,7 @@ def parse(argv=None):
                    help='N>1: skip the interleaved A/B of the overlap and store-policy defaults')
     p.add_argument('--ab-reps', type=int, default=3, help='N>1 defaults A/B: calls per variant')
     p.add_argument('--ab-rounds', type=int, default=2, help='N>1 defaults A/B: interleaved passes')
-    p.add_argument('--pmc', default=os.path.join(ROOT, 'profiles', 'r05e_pmc_summary.json'),
+    p.add_argument('--pmc', default=os.path.join(ROOT, 'profiles', 'r06f_pmc_summary.json'),
                    help='PMC traffic summary (from tools/pmc_summary.py) to quote as traffic')
     return p.parse_args(argv)
 
@@ -306,28 +306,6 @@ def event_time_per_launch(launch, reps, stream, rounds=3):
     return sum(per) / len(per), per[len(per) // 2], per[0]
 
 
-def isolated_event_time(launch, reps, stream, lead_cycles=200000):
-    """duration of one `launch()` started from an idle GPU, as in the timed
-    synchronous loop: per launch, a short spin kernel (torch.cuda._sleep,
-    ~0.1 ms) holds the stream while the host enqueues the start event, the
-    launch and the end event, so the event pair brackets the kernel alone and
-    no host launch latency; then the host waits.  Returns (avg, median, min)
-    in ms over `reps` launches."""
-    per = []
-    with torch.cuda.stream(stream):
-        for _ in range(reps):
-            s0 = torch.cuda.Event(enable_timing=True)
-            s1 = torch.cuda.Event(enable_timing=True)
-            torch.cuda._sleep(lead_cycles)
-            s0.record(stream)
-            launch()
-            s1.record(stream)
-            s1.synchronize()
-            per.append(s0.elapsed_time(s1))
-    per.sort()
-    return sum(per) / len(per), per[len(per) // 2], per[0]
-
-
 def fill_uniform(t, seed):
     g = torch.Generator(device=t.device)
     g.manual_seed(seed)
@@ -415,7 +393,12 @@ def cpu_baseline(seconds, count, crossover_rows):
     quota = topo['cgroup_cpu_quota']
     nq = max(1, min(len(phys), int(quota))) if quota else len(phys)
     one = leg(phys[:1], seconds * 0.35)
-    allc = leg(phys, seconds * 0.25)
+    # every physical core only where no cgroup quota throttles them: with a
+    # quota below the thread count the threads run out of it within a pass
+    # and the reduce / triad pair is split across throttle windows (the
+    # paired ratio read 0.94 and 2.77 on one box, r06f) -- the quota leg is
+    # then the multi-core figure
+    allc = leg(phys, seconds * 0.25) if nq >= len(phys) else None
     c1 = leg(phys[:1], seconds * 0.1, n=4194304)
     quota_leg = None
     if nq < len(phys):
@@ -455,10 +438,12 @@ def cpu_baseline(seconds, count, crossover_rows):
                       note='one pinned thread per physical core of this process (%d sockets), '
                            'each first-touching its own slice of both operands (NUMA-local); '
                            'value = median pass; host triad = a += 0.5 b on the same threads '
-                           'and layout (12 B per element, the combine\'s own traffic); with a '
-                           'cgroup quota below the thread count the passes run in the quota\'s '
-                           'run windows and `sustained` (all passes / their wall span) is the '
-                           'throttled rate' % topo['sockets']),
+                           'and layout (12 B per element, the combine\'s own traffic)'
+                           % topo['sockets']) if allc else
+        dict(skipped='the cgroup CPU quota (%s CPUs) is below the %d physical cores: %d threads '
+                     'would exhaust it within a pass and split each reduce / triad pair across '
+                     'throttle windows; quota_threads is the multi-core figure'
+                     % (quota, len(phys), len(phys))),
         quota_threads=quota_leg,
         config1_16MiB_1core=dict(value=c1['gibs'], reps=c1['reps'],
                                  note='BASELINE config 1; 48 MiB per call is cache-resident on '
@@ -537,19 +522,20 @@ def reduce_local_leg(args, world, rank, dev):
     kreps = max(10, min(args.steps, 50))
     call = lambda: redop.check(redop.reduce_local_async(inb, inout, n, H.MPI_FLOAT, H.MPI_SUM,  # noqa
                                                          stream))
-    # the kernel as the timed loop runs it: each launch from an idle GPU, with
-    # the synchronous entry's store policy (its own XCD mask since round 6)
-    pol = redop.get_store_policy()
-    sync_mask = redop.get_sync_store_policy()
-    redop.check(redop.set_store_policy(sync_mask, pol['every'], pol['phase'], pol['tail_blocks']))
+    # the kernel as the timed loop runs it: the same synchronous calls from C,
+    # back to back, the library recording a HIP event pair around each launch
+    # on its own stream (MPIX_Redop_sync_timing) -- the entry's store policy,
+    # idle gap and completion wait all as in the timed loop
+    dev_index = dev.index if getattr(dev, 'index', None) is not None else torch.cuda.current_device()
+    redop.sync_timing(dev_index, 3 * kreps)
     try:
-        k_avg, k_med, k_min = isolated_event_time(call, 3 * kreps, stream)
+        steps(3 * kreps)
     finally:
-        # back to the default (-1) unless the environment fixed a mask: an
-        # explicit mask would become the synchronous entry's too
-        env_mask = os.environ.get('MPIX_REDOP_WT_XCD')
-        redop.check(redop.set_store_policy(-1 if env_mask is None else pol['xcd_mask'],
-                                           pol['every'], pol['phase'], pol['tail_blocks']))
+        per = sorted(redop.sync_timing_read(dev_index))
+    if len(per) != 3 * kreps:
+        raise RuntimeError('sync timing recorded %d of %d calls' % (len(per), 3 * kreps))
+    k_avg, k_med, k_min = sum(per) / len(per), per[len(per) // 2], per[0]
+    sync_mask = redop.get_sync_store_policy()
     # and back to back with the stream-ordered entries' policy (a
     # stream-ordered caller's steady state)
     b_avg, b_med, b_min = event_time_per_launch(call, kreps, stream)
@@ -596,10 +582,10 @@ def single_gpu(args, dev):
                               if traffic_src else None,
             'kernel_ms_avg': round(leg['k_avg'], 4), 'kernel_ms_median': round(leg['k_med'], 4),
             'kernel_ms_min': round(leg['k_min'], 4), 'kernel_launches_timed': 3 * kreps,
-            'kernel_timing': 'HIP events around each launch on its stream, every launch started '
-                             'from an idle GPU as in the timed synchronous loop (a short spin '
-                             'kernel holds the stream while the events and the launch are '
-                             'enqueued), with the synchronous entry\'s store policy',
+            'kernel_timing': 'HIP events recorded by the library around the launch of each of '
+                             '%d synchronous MPIX_Reduce_local calls on its own stream '
+                             '(MPIX_Redop_sync_timing), the calls issued from C back to back '
+                             'right after the timed loop exactly as in it' % (3 * kreps),
             'algorithmic_bytes_per_launch': nbytes_alg,
             'back_to_back': {'kernel_ms_avg': round(leg['b_avg'], 4),
                              'achieved': round(nbytes_alg / (leg['b_avg'] * 1e-3) / 1e9, 1),
@@ -607,8 +593,7 @@ def single_gpu(args, dev):
                              'launches': 3 * kreps,
                              'note': 'one event pair around batches of launches issued back to '
                                      'back (a stream-ordered caller, with the stream-ordered '
-                                     'entries\' store policy); an idle-start launch runs longer '
-                                     'with the one-wave blocks (DESIGN.md §8)'},
+                                     'entries\' store policy, DESIGN.md §8)'},
         },
     }
     if traced and traced.get('avg_duration_ns'):
@@ -622,7 +607,8 @@ def single_gpu(args, dev):
             frac_traced=round(nbytes_alg / t_ns / HBM_PEAK_GBS, 4),
             traced_kernel_ms_avg=round(t_ns * 1e-6, 4),
             traced_launches=traced.get('idle_start_launches') or traced.get('launches_traced'),
-            traced_which='idle-start launches' if traced.get('idle_start_avg_ns') else 'all launches',
+            traced_which=('launches after an idle gap (the synchronous calls)'
+                          if traced.get('idle_start_avg_ns') else 'all launches'),
             traced_all_launches_ms_avg=round(float(traced['avg_duration_ns']) * 1e-6, 4),
             traced_run_ms_per_step=traced.get('traced_run_ms_per_step'),
             traced_source=traffic_src)

@@ -420,6 +420,17 @@ int MPIX_Redop_get_store_policy(int *xcd_mask, int *every, int *phase, int *tail
 int MPIX_Redop_set_sync_store_policy(int xcd_mask);
 int MPIX_Redop_get_sync_store_policy(int *xcd_mask);
 
+/* Kernel timing of the synchronous entry, for measurement (bench.py's
+ * roofline figure): the calling thread's next ncalls synchronous calls on
+ * `device` (MPIX_Reduce_local on device or page-locked operands) record a HIP
+ * event pair around their launch on the library's stream -- the combine as the
+ * call runs it, nothing else changed.  ncalls = 0 stops; at most 65536.
+ * _read waits for the recorded pairs, stores up to cap durations (ms, call
+ * order) in ms[], their number in *got, and stops the recording.  No
+ * counterpart in MPICH (a tool interface, like the MPIX_Redop_set_* knobs). */
+int MPIX_Redop_sync_timing(int device, int ncalls);
+int MPIX_Redop_sync_timing_read(int device, float *ms, int cap, int *got);
+
 /* ---- large pageable host operands (performance knob) ----
  * threads > 0: pageable operands of at least 2 * chunk_bytes go through that many
  * host threads (the caller is one of them).  Default form, "wave": the

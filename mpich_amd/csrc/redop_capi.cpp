@@ -430,6 +430,7 @@ void read_env()
 thread_local int t_last_error = 0;
 
 constexpr int kMaxDev = 64;
+constexpr int kSyncTimingMax = 1 << 16;    // calls one MPIX_Redop_sync_timing covers
 struct DevState {
     bool init = false;
     hipStream_t s[2] = {nullptr, nullptr};
@@ -451,6 +452,10 @@ struct DevState {
     char *bounce = nullptr;     // pinned host: in half + inout half, bounce_half bytes each
     char *bounce_dev = nullptr; // its device mapping
     size_t bounce_half = 0;
+    // MPIX_Redop_sync_timing: an event pair around the launch of each of the
+    // next t_cap synchronous calls on s[0] (t_used recorded so far)
+    std::vector<hipEvent_t> tev;
+    int t_cap = 0, t_used = 0;
 };
 
 // Large pageable operands: one stream + pinned slot pair per host worker, ONE
@@ -767,18 +772,43 @@ int run_sync(DevState *d, const void *in, void *io, uint64_t count, uint32_t it,
              uint32_t op, bool zero_copy = false)
 {
     launch_cfg();       // environment read before g_sync is consulted
+    // timed call (MPIX_Redop_sync_timing): the pair brackets the launch on
+    // the state's stream, nothing else changes
+    const int ti = d->t_used < d->t_cap ? d->t_used++ : -1;
+    if (ti >= 0) {
+        int rc = hip_err(hipEventRecord(d->tev[2 * ti], d->s[0]));
+        if (rc)
+            return rc;
+    }
+    struct Stop {
+        DevState *d;
+        int ti;
+        ~Stop()
+        {
+            if (ti >= 0)
+                (void) hipEventRecord(d->tev[2 * ti + 1], d->s[0]);
+        }
+    };
     if (g_sync.load() == 2 && d->flag) {
         const uint32_t seq = ++d->seq;
         bool signalled = false;
-        int rc = enqueue(in, io, count, it, ext, op, d->s[0], (uint32_t *) d->flag, d->flag_ctr,
+        int rc;
+        {
+            Stop stop{d, ti};
+            rc = enqueue(in, io, count, it, ext, op, d->s[0], (uint32_t *) d->flag, d->flag_ctr,
                          seq, &signalled, zero_copy, true);
+        }
         if (signalled)      // the kernel stores the word itself
             return spin_on_flag(d, d->s[0], seq);
         int rc2 = wait_stream(d, d->s[0]);
         return rc ? rc : rc2;
     }
-    int rc = enqueue(in, io, count, it, ext, op, d->s[0], nullptr, nullptr, 0, nullptr, zero_copy,
+    int rc;
+    {
+        Stop stop{d, ti};
+        rc = enqueue(in, io, count, it, ext, op, d->s[0], nullptr, nullptr, 0, nullptr, zero_copy,
                      true);
+    }
     int rc2 = wait_stream(d, d->s[0]);
     return rc ? rc : rc2;
 }
@@ -1831,6 +1861,8 @@ static void free_states(DevState *arr)
         }
         if (d.bounce)
             (void) hipHostFree(d.bounce);
+        for (hipEvent_t e : d.tev)
+            (void) hipEventDestroy(e);
         d = DevState();
     }
     delete[] arr;
@@ -2525,6 +2557,49 @@ int MPIX_Redop_get_sync_store_policy(int *xcd_mask)
     // not settled (no launch so far)
     const int ws = g_wt_xcd_sync.load(), x = g_wt_xcd.load();
     *xcd_mask = ws != kWtAuto ? ws : x != kWtAuto ? x : g_wt_sync_default.load();
+    return MPIX_REDOP_SUCCESS;
+}
+
+int MPIX_Redop_sync_timing(int device, int ncalls)
+{
+    env();
+    if (device < 0 || device >= kMaxDev || ncalls < 0 || ncalls > kSyncTimingMax)
+        return set_err(MPIX_REDOP_ERR_ARG);
+    DeviceGuard g(device);
+    DevState *d = dev_state(device);
+    if (!d)
+        return set_err(MPIX_REDOP_ERR_OTHER);
+    while (d->tev.size() < 2 * (size_t) ncalls) {
+        hipEvent_t e = nullptr;
+        int rc = hip_err(hipEventCreate(&e));
+        if (rc)
+            return set_err(rc);
+        d->tev.push_back(e);
+    }
+    d->t_cap = ncalls;
+    d->t_used = 0;
+    return MPIX_REDOP_SUCCESS;
+}
+
+int MPIX_Redop_sync_timing_read(int device, float *ms, int cap, int *got)
+{
+    env();
+    if (device < 0 || device >= kMaxDev || !got || cap < 0 || (cap > 0 && !ms))
+        return set_err(MPIX_REDOP_ERR_ARG);
+    DeviceGuard g(device);
+    DevState *d = dev_state(device);
+    if (!d)
+        return set_err(MPIX_REDOP_ERR_OTHER);
+    const int n = d->t_used < cap ? d->t_used : cap;
+    for (int i = 0; i < n; ++i) {
+        int rc = hip_err(hipEventSynchronize(d->tev[2 * i + 1]));
+        if (!rc)
+            rc = hip_err(hipEventElapsedTime(&ms[i], d->tev[2 * i], d->tev[2 * i + 1]));
+        if (rc)
+            return set_err(rc);
+    }
+    *got = n;
+    d->t_cap = d->t_used = 0;
     return MPIX_REDOP_SUCCESS;
 }
 

@@ -77,6 +77,9 @@ def lib():
             'MPIX_Redop_get_store_policy': ([ctypes.POINTER(i32)] * 4, i32),
             'MPIX_Redop_set_sync_store_policy': ([i32], i32),
             'MPIX_Redop_get_sync_store_policy': ([ctypes.POINTER(i32)], i32),
+            'MPIX_Redop_sync_timing': ([i32, i32], i32),
+            'MPIX_Redop_sync_timing_read': ([i32, ctypes.POINTER(ctypes.c_float), i32,
+                                             ctypes.POINTER(i32)], i32),
             'MPIX_Redop_set_pageable': ([i32, aint], i32),
             'MPIX_Redop_get_pageable': ([ctypes.POINTER(i32), ctypes.POINTER(aint)], i32),
             'MPIX_Redop_last_error': ([], i32),
@@ -442,6 +445,20 @@ def get_sync_store_policy():
     x = ctypes.c_int()
     check(lib().MPIX_Redop_get_sync_store_policy(ctypes.byref(x)))
     return x.value
+
+
+def sync_timing(device, ncalls):
+    """Record a HIP event pair around the launch of the calling thread's next
+    `ncalls` synchronous calls on `device` (MPIX_Redop_sync_timing)."""
+    check(lib().MPIX_Redop_sync_timing(int(device), int(ncalls)))
+
+
+def sync_timing_read(device, cap=1 << 16):
+    """The recorded kernel durations in ms, call order; stops the recording."""
+    buf = (ctypes.c_float * cap)()
+    got = ctypes.c_int()
+    check(lib().MPIX_Redop_sync_timing_read(int(device), buf, cap, ctypes.byref(got)))
+    return list(buf[:got.value])
 
 
 def error_string(code):

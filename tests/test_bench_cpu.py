@@ -465,5 +465,11 @@ def test_cpu_baseline_reads_reduce_and_triad_from_the_same_passes(oracle):
     for k in ('frac_of_host_triad_1core', 'frac_of_host_triad_1core_per_pass',
               'host_triad_1core_gibs', 'host_triad_timing'):
         assert k in c, k
-    assert 'frac_of_host_triad_per_pass' in c['allcores']
-    assert 0 < c['frac_of_host_triad_1core'] < 3 and 0 < c['allcores']['frac_of_host_triad'] < 3
+    assert 0 < c['frac_of_host_triad_1core'] < 3
+    # every core where no quota throttles them, else the quota leg instead
+    quota, ncores = c['cgroup_cpu_quota'], c['physical_cores']
+    if quota is not None and quota < ncores:
+        assert 'skipped' in c['allcores'] and c['quota_threads']['threads'] == max(1, int(quota))
+    else:
+        assert 'frac_of_host_triad_per_pass' in c['allcores']
+        assert 0 < c['allcores']['frac_of_host_triad'] < 3
