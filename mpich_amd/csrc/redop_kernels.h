@@ -586,6 +586,14 @@ k_elem(const typename C::unit *__restrict__ in, typename C::unit *__restrict__ i
 struct alignas(16) Pk32 {
     v4u lo, hi;
 };
+#ifndef MPIX_REDOP_BLOCK32
+#define MPIX_REDOP_BLOCK32 64       // k_contig32 / k_batch32 block
+#endif
+#ifdef MPIX_C32_WAVES_N
+#define MPIX_C32_WAVES __attribute__((amdgpu_waves_per_eu(MPIX_C32_WAVES_N)))
+#else
+#define MPIX_C32_WAVES
+#endif
 
 // Split combiners (C::kSplit, the soft complex products): C::apply_fast(a, b,
 // prm, ok) runs only the normal-operand fast paths and returns a unchanged
@@ -656,6 +664,47 @@ __device__ __forceinline__ void contig32_tile(const typename C::unit *in, const 
                 prm.fixup[unit0 >> 6] = mask;
     };
     const uint64_t tile = nt * U;
+    // (the split combiners too: a unit per lane for every tile, two 16-byte
+    // loads 16 bytes apart, saves the swaps' selects and DPP moves but ran
+    // COMPLEX32 PROD 4.97 -> 4.51 and C_LONG_DOUBLE_COMPLEX PROD 6.24 -> 4.47
+    // TB/s, profiles/r06_soft_rows_ab6.jsonl)
+#ifndef MPIX_C32_LDS
+#define MPIX_C32_LDS 1
+#endif
+    if constexpr (split && MPIX_C32_LDS) {
+        // the split combiners are issue-bound: the packets go through LDS
+        // (unit m of the run = packets 2m, 2m + 1 to lane m), which costs no
+        // VALU, instead of the DPP swap and its selects; the lane's unit is
+        // then in run order, so its ballot is the fixup word itself
+        if ((t + 1) * tile <= n) {
+            __shared__ v4u lds[MPIX_REDOP_BLOCK32 / 64][2][128];
+            const unsigned lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+            v4u *la = lds[wave][0], *lb = lds[wave][1];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint64_t run0 = t * tile + u * nt + wave * 64;
+                const uint64_t q = 2 * run0 + lane;
+                const v4u a0 = ld16<NTL>(vio + q), a1 = ld16<NTL>(vio + q + 64);
+                const v4u b0 = ld16<NTL>(vin + q), b1 = ld16<NTL>(vin + q + 64);
+                la[lane] = a0;
+                la[lane + 64] = a1;
+                lb[lane] = b0;
+                lb[lane + 64] = b1;
+                __syncthreads();
+                const Pk32 r = f(Pk32{la[2 * lane], la[2 * lane + 1]},
+                                 Pk32{lb[2 * lane], lb[2 * lane + 1]});
+                __syncthreads();
+                la[2 * lane] = r.lo;
+                la[2 * lane + 1] = r.hi;
+                __syncthreads();
+                st16_pol<NTS>(vout + q, la[lane], wt);
+                st16_pol<NTS>(vout + q + 64, la[lane + 64], wt);
+                record(run0, __ballot(!ok));
+                __syncthreads();
+            }
+            return;
+        }
+    }
     if ((t + 1) * tile <= n) {
         const unsigned lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
         const bool odd = lane & 1;
@@ -690,7 +739,8 @@ __device__ __forceinline__ void contig32_tile(const typename C::unit *in, const 
                 record(t * tile + u * nt + wave * 64, lanes_to_units(__ballot(!ok)));
         }
     } else {
-        for (uint64_t k = t * tile + threadIdx.x; k < n; k += nt) {
+        const uint64_t end = (t + 1) * tile < n ? (t + 1) * tile : n;    // this tile only
+        for (uint64_t k = t * tile + threadIdx.x; k < end; k += nt) {
             const Pk32 r = f(Pk32{ld16<NTL>(vio + 2 * k), ld16<NTL>(vio + 2 * k + 1)},
                              Pk32{ld16<NTL>(vin + 2 * k), ld16<NTL>(vin + 2 * k + 1)});
             st16_pol<NTS>(vout + 2 * k, r.lo, wt);
@@ -702,7 +752,7 @@ __device__ __forceinline__ void contig32_tile(const typename C::unit *in, const 
 }
 
 template <class C, int U, bool NTL, bool NTS>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256) MPIX_C32_WAVES
 k_contig32(const typename C::unit *in, const typename C::unit *io, typename C::unit *out, uint64_t n,
            Params prm, uint32_t nblk, uint32_t nthreads)
 {
@@ -906,9 +956,6 @@ inline void set_store_policy(Params &p, const LaunchCfg &cfg, unsigned grid)
 // 7.06-7.09 TB/s, the complex long double / binary128 rows even to +2 %
 #ifndef MPIX_REDOP_VBLOCK
 #define MPIX_REDOP_VBLOCK 64        // the stride-2 vector target's block
-#endif
-#ifndef MPIX_REDOP_BLOCK32
-#define MPIX_REDOP_BLOCK32 64
 #endif
 constexpr unsigned kContig32Block = MPIX_REDOP_BLOCK32;
 

@@ -189,6 +189,47 @@ MPIX_SDEV uint32_t funnel_l(uint32_t hi, uint32_t lo, uint32_t s)
 
 MPIX_SDEV uint32_t clz32(uint32_t x) { return x ? (uint32_t) __builtin_clz(x) : 32u; }
 
+// a + b + cin (cin 0 or 1), the carry out in *cout: one v_addc_co_u32 (the
+// 64-bit accumulate-and-shift form compiles to an add, a select of the carry
+// and a 64-bit add per limb)
+MPIX_SDEV uint32_t addc32(uint32_t a, uint32_t b, uint32_t cin, uint32_t *cout)
+{
+#ifdef MPIX_SOFT_HOST
+    const uint64_t t = (uint64_t) a + b + cin;
+    *cout = (uint32_t) (t >> 32);
+    return (uint32_t) t;
+#else
+    unsigned c;
+    const uint32_t r = __builtin_addc(a, b, cin, &c);
+    *cout = c;
+    return r;
+#endif
+}
+
+// q += inc (inc 0 or 1) over four limbs; the carry out of q[3] is dropped
+MPIX_SDEV void inc128(uint32_t q[4], uint32_t inc)
+{
+    uint32_t c;
+    q[0] = addc32(q[0], inc, 0u, &c);
+    q[1] = addc32(q[1], 0u, c, &c);
+    q[2] = addc32(q[2], 0u, c, &c);
+    q[3] = addc32(q[3], 0u, c, &c);
+}
+
+// z + x * y (v_mad_u64_u32): as a chain the compiler keeps in order -- left
+// to itself it sums a column's products first and adds the carry with one more
+// 64-bit add per column
+MPIX_SDEV uint64_t mad64(uint32_t x, uint32_t y, uint64_t z)
+{
+#ifdef MPIX_SOFT_HOST
+    return z + (uint64_t) x * y;
+#else
+    uint64_t r, carry;      // the carry-out pair is never set (no overflow)
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(carry) : "v"(x), "v"(y), "v"(z));
+    return r;
+#endif
+}
+
 // v >>= d (d in 0..127); returns the OR of the bits shifted out
 MPIX_SDEV uint32_t shr128_lost(uint32_t v[4], uint32_t d)
 {
@@ -230,12 +271,9 @@ MPIX_SDEV bool add_normal_limbs(const uint32_t A[4], uint32_t B[4], uint32_t d, 
     // S = A + B, or A - B = A + ~B + 1 (A >= B, so no borrow out)
     const uint32_t m = sub ? 0xffffffffu : 0u;
     uint32_t S[4];
-    uint64_t c = sub ? 1u : 0u;
-    for (int i = 0; i < 4; ++i) {
-        c += (uint64_t) A[i] + (B[i] ^ m);
-        S[i] = (uint32_t) c;
-        c >>= 32;
-    }
+    uint32_t c = sub ? 1u : 0u;
+    for (int i = 0; i < 4; ++i)
+        S[i] = addc32(A[i], B[i] ^ m, c, &c);
     const uint32_t lz = clz32(S[3]);
     uint32_t rnd, sticky;
     if constexpr (BITS == 64) {
@@ -264,12 +302,7 @@ MPIX_SDEV bool add_normal_limbs(const uint32_t A[4], uint32_t B[4], uint32_t d, 
     }
     int32_t e = xa + 1 - (int32_t) lz;
     const uint32_t inc = rnd & ((sticky != 0) | (q[0] & 1u));
-    uint64_t k = inc;
-    for (int i = 0; i < 4; ++i) {
-        k += q[i];
-        q[i] = (uint32_t) k;
-        k >>= 32;
-    }
+    inc128(q, inc);
     // carried out of the significand: it was all ones, it is now 2^BITS
     bool ovf;
     if constexpr (BITS == 64)
@@ -521,10 +554,11 @@ MPIX_SDEV bool quad_add_limbs(const QLimbs &x, const QLimbs &y, bool sub, Quad *
     const QLimbs &big = swap ? y : x, &small = swap ? x : y;
     const uint32_t xa = big.e, d = big.e - small.e;
     // significand << 14: the leading bit at 126
-    const uint32_t A[4] = {big.q[0] << 14, funnel_l(big.q[1], big.q[0], 14),
-                           funnel_l(big.q[2], big.q[1], 14), funnel_l(big.q[3], big.q[2], 14)};
-    uint32_t B[4] = {small.q[0] << 14, funnel_l(small.q[1], small.q[0], 14),
-                     funnel_l(small.q[2], small.q[1], 14), funnel_l(small.q[3], small.q[2], 14)};
+    // (a left funnel by 14 is a right funnel by 18: one v_alignbit_b32 a limb)
+    const uint32_t A[4] = {big.q[0] << 14, funnel_r(big.q[1], big.q[0], 18),
+                           funnel_r(big.q[2], big.q[1], 18), funnel_r(big.q[3], big.q[2], 18)};
+    uint32_t B[4] = {small.q[0] << 14, funnel_r(small.q[1], small.q[0], 18),
+                     funnel_r(small.q[2], small.q[1], 18), funnel_r(small.q[3], small.q[2], 18)};
     uint32_t q[4];
     int32_t e;
     if (!add_normal_limbs<113>(A, B, d < 127u ? d : 127u, sa != sb, (int32_t) xa, q, &e))
@@ -675,7 +709,7 @@ MPIX_SDEV bool quad_mul_digits(const QDigits &x, const QDigits &y, QLimbs *r)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
             if (c - i >= 0 && c - i < 4)
-                t += (uint64_t) x.a[i] * y.a[c - i];
+                t = mad64(x.a[i], y.a[c - i], t);
         d[c] = (uint32_t) t & M29;
     }
     d[7] = (uint32_t) (t >> 29);                // < 2^23
@@ -691,12 +725,7 @@ MPIX_SDEV bool quad_mul_digits(const QDigits &x, const QDigits &y, QLimbs *r)
     q[3] = funnel_r(v[4], v[3], c);
     const uint32_t rnd = (v[0] >> (c - 1u)) & 1u;
     const uint32_t sticky = (v[0] & ((1u << (c - 1u)) - 1u)) | d[2] | d[1] | d[0];
-    uint64_t k = rnd & ((sticky != 0) | (q[0] & 1u));
-    for (int i = 0; i < 4; ++i) {
-        k += q[i];
-        q[i] = (uint32_t) k;
-        k >>= 32;
-    }
+    inc128(q, rnd & ((sticky != 0) | (q[0] & 1u)));
     int32_t E = (int32_t) (x.e + y.e + top) - 16383;
     if (q[3] >> 17) {                   // carried out of the significand: 2^113
         q[3] = 0x10000u;                // (q[0..2] are 0)
