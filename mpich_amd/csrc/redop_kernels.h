@@ -596,9 +596,9 @@ struct alignas(16) Pk32 {
 #endif
 
 // Split combiners (C::kSplit, the soft complex products): C::apply_fast(a, b,
-// prm, ok) runs only the normal-operand fast paths and returns a unchanged
-// with ok false when any of them declines; the contiguous 32-byte kernel then
-// records the unit in Params::fixup (one 64-bit word per 64 units, written
+// prm, ok) runs only the normal-operand fast paths and sets ok false when any
+// of them declines (its result is then unspecified); the contiguous 32-byte
+// kernel leaves such a unit as it was, records it in Params::fixup (one 64-bit word per 64 units, written
 // for every group) and k_fixup32 combines the recorded units with the full
 // C::apply in a second launch.  The general paths stay out of the streaming
 // kernel, whose registers -- and so its waves per SIMD -- are the fast path's
@@ -671,12 +671,12 @@ __device__ __forceinline__ void contig32_tile(const typename C::unit *in, const 
 #ifndef MPIX_C32_LDS
 #define MPIX_C32_LDS 1
 #endif
-    if constexpr (split && MPIX_C32_LDS) {
-        // the split combiners are issue-bound: the packets go through LDS
-        // (unit m of the run = packets 2m, 2m + 1 to lane m), which costs no
-        // VALU, instead of the DPP swap and its selects; the lane's unit is
-        // then in run order, so its ballot is the fixup word itself
-        if ((t + 1) * tile <= n) {
+    if ((t + 1) * tile <= n) {
+        if constexpr (split && MPIX_C32_LDS) {
+            // the split combiners are issue-bound: the packets go through LDS
+            // (unit m of the run = packets 2m, 2m + 1 to lane m), which costs
+            // no VALU, instead of the DPP swap and its selects; the lane's
+            // unit is then in run order, so its ballot is the fixup word
             __shared__ v4u lds[MPIX_REDOP_BLOCK32 / 64][2][128];
             const unsigned lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
             v4u *la = lds[wave][0], *lb = lds[wave][1];
@@ -694,55 +694,60 @@ __device__ __forceinline__ void contig32_tile(const typename C::unit *in, const 
                 const Pk32 r = f(Pk32{la[2 * lane], la[2 * lane + 1]},
                                  Pk32{lb[2 * lane], lb[2 * lane + 1]});
                 __syncthreads();
-                la[2 * lane] = r.lo;
-                la[2 * lane + 1] = r.hi;
+                if (ok) {       // a declined unit stays as it was (k_fixup32 reads it)
+                    la[2 * lane] = r.lo;
+                    la[2 * lane + 1] = r.hi;
+                }
                 __syncthreads();
                 st16_pol<NTS>(vout + q, la[lane], wt);
                 st16_pol<NTS>(vout + q + 64, la[lane + 64], wt);
                 record(run0, __ballot(!ok));
                 __syncthreads();
             }
-            return;
-        }
-    }
-    if ((t + 1) * tile <= n) {
-        const unsigned lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-        const bool odd = lane & 1;
-        // the unit a lane holds after the swap: run unit lane/2 (even) or 32 + lane/2 (odd)
-        auto gather = [&](v4u p0, v4u p1) {
-            const v4u y = swap_pair(odd ? p0 : p1);
-            return odd ? Pk32{y, p1} : Pk32{p0, y};
-        };
-        v4u a0[U], a1[U], b0[U], b1[U];
-        // run u of this wave: units [t*tile + u*nt + wave*64, +64) = packets from q
+        } else {
+            const unsigned lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+            const bool odd = lane & 1;
+            // the unit a lane holds after the swap: run unit lane/2 (even) or 32 + lane/2 (odd)
+            auto gather = [&](v4u p0, v4u p1) {
+                const v4u y = swap_pair(odd ? p0 : p1);
+                return odd ? Pk32{y, p1} : Pk32{p0, y};
+            };
+            v4u a0[U], a1[U], b0[U], b1[U];
+            // run u of this wave: units [t*tile + u*nt + wave*64, +64) = packets from q
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint64_t q = 2 * (t * tile + u * nt + wave * 64) + lane;
-            a0[u] = ld16<NTL>(vio + q);
-            a1[u] = ld16<NTL>(vio + q + 64);
-        }
+            for (int u = 0; u < U; ++u) {
+                const uint64_t q = 2 * (t * tile + u * nt + wave * 64) + lane;
+                a0[u] = ld16<NTL>(vio + q);
+                a1[u] = ld16<NTL>(vio + q + 64);
+            }
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint64_t q = 2 * (t * tile + u * nt + wave * 64) + lane;
-            b0[u] = ld16<NTL>(vin + q);
-            b1[u] = ld16<NTL>(vin + q + 64);
-        }
-        __builtin_amdgcn_sched_barrier(0);
+            for (int u = 0; u < U; ++u) {
+                const uint64_t q = 2 * (t * tile + u * nt + wave * 64) + lane;
+                b0[u] = ld16<NTL>(vin + q);
+                b1[u] = ld16<NTL>(vin + q + 64);
+            }
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const Pk32 r = f(gather(a0[u], a1[u]), gather(b0[u], b1[u]));
-            const v4u y = swap_pair(odd ? r.lo : r.hi);
-            const uint64_t q = 2 * (t * tile + u * nt + wave * 64) + lane;
-            st16_pol<NTS>(vout + q, odd ? y : r.lo, wt);
-            st16_pol<NTS>(vout + q + 64, odd ? r.hi : y, wt);
-            if constexpr (split)
-                record(t * tile + u * nt + wave * 64, lanes_to_units(__ballot(!ok)));
+            for (int u = 0; u < U; ++u) {
+                const Pk32 ga = gather(a0[u], a1[u]);
+                Pk32 r = f(ga, gather(b0[u], b1[u]));
+                if constexpr (split)
+                    r = ok ? r : ga;    // a declined unit stays as it was
+                const v4u y = swap_pair(odd ? r.lo : r.hi);
+                const uint64_t q = 2 * (t * tile + u * nt + wave * 64) + lane;
+                st16_pol<NTS>(vout + q, odd ? y : r.lo, wt);
+                st16_pol<NTS>(vout + q + 64, odd ? r.hi : y, wt);
+                if constexpr (split)
+                    record(t * tile + u * nt + wave * 64, lanes_to_units(__ballot(!ok)));
+            }
         }
     } else {
         const uint64_t end = (t + 1) * tile < n ? (t + 1) * tile : n;    // this tile only
         for (uint64_t k = t * tile + threadIdx.x; k < end; k += nt) {
-            const Pk32 r = f(Pk32{ld16<NTL>(vio + 2 * k), ld16<NTL>(vio + 2 * k + 1)},
-                             Pk32{ld16<NTL>(vin + 2 * k), ld16<NTL>(vin + 2 * k + 1)});
+            const Pk32 a{ld16<NTL>(vio + 2 * k), ld16<NTL>(vio + 2 * k + 1)};
+            Pk32 r = f(a, Pk32{ld16<NTL>(vin + 2 * k), ld16<NTL>(vin + 2 * k + 1)});
+            if constexpr (split)
+                r = ok ? r : a;         // a declined unit stays as it was
             st16_pol<NTS>(vout + 2 * k, r.lo, wt);
             st16_pol<NTS>(vout + 2 * k + 1, r.hi, wt);
             if constexpr (split)        // a unit per lane: the mask is in unit order

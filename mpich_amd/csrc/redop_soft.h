@@ -828,8 +828,8 @@ struct QuadCSum {
 };
 // The complex products are split combiners (is_split, redop_kernels.h): the
 // contiguous kernel runs apply_fast -- all six operations' normal-operand
-// fast paths, one flag for the lot, the unit left unchanged when any declines
-// -- and a second launch combines those units with apply, each operation's
+// fast paths, one flag for the lot (the result unspecified when any declines:
+// the kernel then leaves the unit as it was) -- and a second launch combines those units with apply, each operation's
 // fast path or general path.  The general paths' registers stay out of the
 // streaming kernel.
 struct QuadCProd {
@@ -858,7 +858,7 @@ struct QuadCProd {
         ok &= quad_mul_digits(ci, br, &p2);
         ok &= quad_mul_digits(cr, bi, &p3);
         ok &= quad_add_limbs(p2, p3, false, &r.im);
-        return ok ? r : c;
+        return r;
     }
 };
 struct alignas(16) X87C {
@@ -902,7 +902,7 @@ struct X87CProd {
         X87C r;     // stored with fstpt: each part keeps inout's padding
         r.re = x87_make(x.re, (re.se >> 15) & 1, (uint32_t) re.se & 0x7fff, re.m);
         r.im = x87_make(x.im, (im.se >> 15) & 1, (uint32_t) im.se & 0x7fff, im.m);
-        return ok ? r : x;
+        return r;
     }
     static MPIX_SDEV X87C apply(X87C x, X87C y, const Params &)
     {

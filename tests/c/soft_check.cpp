@@ -36,8 +36,7 @@ struct QuadSumGeneral {
 };
 
 // a split combiner as the kernels run it: apply_fast, and where it declined
-// (the unit must come back unchanged) the full apply -- returns -2 when a
-// declined unit came back changed
+// (its result unspecified: the kernels keep the unit as it was) the full apply
 template <class C>
 static int run_split(const void *in, void *inout, long n)
 {
@@ -49,11 +48,8 @@ static int run_split(const void *in, void *inout, long n)
         memcpy(&b, (const char *) in + i * sizeof(T), sizeof(T));
         bool ok = false;
         T r = C::apply_fast(a, b, prm, ok);
-        if (!ok) {
-            if (memcmp(&r, &a, sizeof(T)))
-                return -2;
+        if (!ok)
             r = C::apply(a, b, prm);
-        }
         memcpy((char *) inout + i * sizeof(T), &r, sizeof(T));
     }
     return 0;
