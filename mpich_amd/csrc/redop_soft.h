@@ -189,6 +189,9 @@ MPIX_SDEV uint32_t funnel_l(uint32_t hi, uint32_t lo, uint32_t s)
 
 MPIX_SDEV uint32_t clz32(uint32_t x) { return x ? (uint32_t) __builtin_clz(x) : 32u; }
 
+// x != 0 as 0 / 1: one full-rate v_min_u32 (a compare and a select otherwise)
+MPIX_SDEV uint32_t nz32(uint32_t x) { return x < 1u ? x : 1u; }
+
 // a + b + cin (cin 0 or 1), the carry out in *cout: one v_addc_co_u32 (the
 // 64-bit accumulate-and-shift form compiles to an add, a select of the carry
 // and a 64-bit add per limb)
@@ -230,6 +233,19 @@ MPIX_SDEV uint64_t mad64(uint32_t x, uint32_t y, uint64_t z)
 #endif
 }
 
+// x * y as the first link of such a chain (the zero addend inline, not a
+// register pair set to zero)
+MPIX_SDEV uint64_t mul64(uint32_t x, uint32_t y)
+{
+#ifdef MPIX_SOFT_HOST
+    return (uint64_t) x * y;
+#else
+    uint64_t r, carry;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(r), "=s"(carry) : "v"(x), "v"(y));
+    return r;
+#endif
+}
+
 // v >>= d (d in 0..127); returns the OR of the bits shifted out
 MPIX_SDEV uint32_t shr128_lost(uint32_t v[4], uint32_t d)
 {
@@ -266,8 +282,20 @@ template <int BITS>
 MPIX_SDEV bool add_normal_limbs(const uint32_t A[4], uint32_t B[4], uint32_t d, bool sub, int32_t xa,
                                 uint32_t q[4], int32_t *E)
 {
-    if (shr128_lost(B, d))
-        B[0] |= 1u;
+    // exponents less than 32 apart (nearly every pair of products in a
+    // complex product) need no limb selects: a branch a wave takes only when
+    // one of its lanes is further apart
+    uint32_t lost;
+    if (d < 32u) {
+        lost = B[0] & ((1u << d) - 1u);
+        B[0] = funnel_r(B[1], B[0], d);
+        B[1] = funnel_r(B[2], B[1], d);
+        B[2] = funnel_r(B[3], B[2], d);
+        B[3] >>= d;
+    } else {
+        lost = shr128_lost(B, d);
+    }
+    B[0] |= nz32(lost);
     // S = A + B, or A - B = A + ~B + 1 (A >= B, so no borrow out)
     const uint32_t m = sub ? 0xffffffffu : 0u;
     uint32_t S[4];
@@ -296,23 +324,25 @@ MPIX_SDEV bool add_normal_limbs(const uint32_t A[4], uint32_t B[4], uint32_t d, 
         q[1] = funnel_r(S[2], S[1], cut);
         q[2] = funnel_r(S[3], S[2], cut);
         q[3] = S[3] >> cut;
-        const uint32_t half = (1u << cut) >> 1;         // the round bit (0: none below)
-        rnd = (S[0] & half) != 0;
-        sticky = S[0] & (half - 1u) & (cut ? 0xffffffffu : 0u);
+        // the bits below the cut, left-aligned (none when cut = 0)
+        const uint32_t low = funnel_r(S[0], 0u, cut);
+        rnd = low >> 31;
+        sticky = low << 1;
     }
     int32_t e = xa + 1 - (int32_t) lz;
-    const uint32_t inc = rnd & ((sticky != 0) | (q[0] & 1u));
+    const uint32_t inc = rnd & (nz32(sticky) | (q[0] & 1u));
     inc128(q, inc);
-    // carried out of the significand: it was all ones, it is now 2^BITS
-    bool ovf;
-    if constexpr (BITS == 64)
-        ovf = (q[2] & 1u) != 0;
-    else
-        ovf = (q[3] >> (BITS - 96)) != 0;
-    if (ovf) {
-        q[0] = q[1] = q[2] = q[3] = 0;
-        q[(BITS - 1) / 32] = 1u << ((BITS - 1) % 32);
-        e += 1;
+    // carried out of the significand: it was all ones, it is now 2^BITS (the
+    // limbs below the top one already zero)
+    if constexpr (BITS == 64) {
+        const uint32_t ovf = q[2] & 1u;
+        q[1] |= ovf << 31;
+        q[2] = 0;
+        e += (int32_t) ovf;
+    } else {
+        const uint32_t ovf = q[3] >> (BITS - 96);
+        q[3] >>= ovf;
+        e += (int32_t) ovf;
     }
     *E = e;
     return e >= 1 && e <= 0x7ffe;
@@ -709,7 +739,7 @@ MPIX_SDEV bool quad_mul_digits(const QDigits &x, const QDigits &y, QLimbs *r)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
             if (c - i >= 0 && c - i < 4)
-                t = mad64(x.a[i], y.a[c - i], t);
+                t = c == 0 ? mul64(x.a[i], y.a[c - i]) : mad64(x.a[i], y.a[c - i], t);
         d[c] = (uint32_t) t & M29;
     }
     d[7] = (uint32_t) (t >> 29);                // < 2^23
@@ -723,14 +753,14 @@ MPIX_SDEV bool quad_mul_digits(const QDigits &x, const QDigits &y, QLimbs *r)
     q[1] = funnel_r(v[2], v[1], c);
     q[2] = funnel_r(v[3], v[2], c);
     q[3] = funnel_r(v[4], v[3], c);
-    const uint32_t rnd = (v[0] >> (c - 1u)) & 1u;
-    const uint32_t sticky = (v[0] & ((1u << (c - 1u)) - 1u)) | d[2] | d[1] | d[0];
-    inc128(q, rnd & ((sticky != 0) | (q[0] & 1u)));
-    int32_t E = (int32_t) (x.e + y.e + top) - 16383;
-    if (q[3] >> 17) {                   // carried out of the significand: 2^113
-        q[3] = 0x10000u;                // (q[0..2] are 0)
-        E += 1;
-    }
+    const uint32_t low = v[0] << (32u - c);     // V's bits below the cut, left-aligned
+    const uint32_t rnd = low >> 31;
+    const uint32_t sticky = (low << 1) | d[2] | d[1] | d[0];
+    inc128(q, rnd & (nz32(sticky) | (q[0] & 1u)));
+    // carried out of the significand: 2^113 (q[0..2] are 0)
+    const uint32_t ovf = q[3] >> 17;
+    q[3] >>= ovf;
+    const int32_t E = (int32_t) (x.e + y.e + top + ovf) - 16383;
     r->e = (uint32_t) E;
     r->s = x.s ^ y.s;
     return E >= 1 && E <= 0x7ffe;
