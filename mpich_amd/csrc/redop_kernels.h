@@ -602,7 +602,7 @@ struct alignas(16) Pk32 {
 // for every group) and k_fixup32 combines the recorded units with the full
 // C::apply in a second launch.  The general paths stay out of the streaming
 // kernel, whose registers -- and so its waves per SIMD -- are the fast path's
-// (QuadCProd: 107 VGPRs with the general paths inline, 79 without; it is
+// (QuadCProd: 107 VGPRs with the general paths inline, 70 without; it is
 // VALU- and latency-bound).
 template <class C, class = void> struct is_split : std::false_type {};
 template <class C> struct is_split<C, std::void_t<decltype(C::kSplit)>>
