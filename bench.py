@@ -79,7 +79,7 @@ def parse(argv=None):
                    help='N>1: skip the interleaved A/B of the overlap and store-policy defaults')
     p.add_argument('--ab-reps', type=int, default=3, help='N>1 defaults A/B: calls per variant')
     p.add_argument('--ab-rounds', type=int, default=2, help='N>1 defaults A/B: interleaved passes')
-    p.add_argument('--pmc', default=os.path.join(ROOT, 'profiles', 'r06f_pmc_summary.json'),
+    p.add_argument('--pmc', default=os.path.join(ROOT, 'profiles', 'r06g_pmc_summary.json'),
                    help='PMC traffic summary (from tools/pmc_summary.py) to quote as traffic')
     return p.parse_args(argv)
 
