@@ -429,34 +429,37 @@ MPIX_SDEV bool x87_mul_fast(const X87 &a, const X87 &b, X87 *r)
     const uint32_t ea = (uint32_t) a.se & 0x7fff, eb = (uint32_t) b.se & 0x7fff;
     if (!(ea - 1u < 0x7ffeu && eb - 1u < 0x7ffeu && (a.m >> 63) && (b.m >> 63)))
         return false;
-    {
-        // both normal: the product of the significands is in [2^126, 2^128),
-        // so its leading bit sits at 126 + top and the rounding cut at a
-        // fixed place -- the general path below with its shifts constant.
-        // A result that would be denormal or overflow takes the general path.
-        const u128 P = (u128) a.m * b.m;
-        const uint64_t hi = (uint64_t) (P >> 64), lo = (uint64_t) P;
-        const int top = (int) (hi >> 63);
-        const uint64_t q0 = top ? hi : (hi << 1) | (lo >> 63);
-        const bool rnd = top ? (lo >> 63) != 0 : ((lo >> 62) & 1) != 0;
-        const bool sticky = top ? (lo << 1) != 0 : (lo << 2) != 0;
-        int64_t E = (int64_t) ea + eb - 16383 + top;
-        if (E >= 1) {
-            uint64_t q = q0;
-            if (rnd && (sticky || (q & 1))) {
-                q += 1;
-                if (q == 0) {           // carried out of the significand
-                    q = 1ull << 63;
-                    E += 1;
-                }
-            }
-            if (E <= 0x7ffe) {
-                *r = x87_make(a, ((a.se ^ b.se) >> 15) & 1, (uint32_t) E, q);
-                return true;
-            }
-        }
-    }
-    return false;
+    // both normal: the product of the significands is in [2^126, 2^128), so
+    // its leading bit sits at 126 + top and the rounding cut at a fixed place
+    // (the general path with its shifts constant), in 32-bit limbs w3..w0
+    // from four multiply-adds.  A result that would be denormal or overflow
+    // takes the general path.
+    const uint32_t al = (uint32_t) a.m, ah = (uint32_t) (a.m >> 32);
+    const uint32_t bl = (uint32_t) b.m, bh = (uint32_t) (b.m >> 32);
+    const uint64_t p0 = mul64(al, bl);
+    const uint64_t t1 = mad64(al, bh, p0 >> 32);
+    const uint64_t t2 = mad64(ah, bl, (uint32_t) t1);
+    const uint64_t t3 = mad64(ah, bh, (t1 >> 32) + (t2 >> 32));
+    const uint32_t w0 = (uint32_t) p0, w1 = (uint32_t) t2;
+    const uint32_t w2 = (uint32_t) t3, w3 = (uint32_t) (t3 >> 32);
+    const uint32_t top = w3 >> 31;
+    // the significand: {w3, w2} (top) or {w3, w2, w1} << 1; the bits below
+    // the cut left-aligned in `low`, w0 under them
+    uint32_t q0 = top ? w2 : funnel_r(w2, w1, 31);
+    uint32_t q1 = top ? w3 : funnel_r(w3, w2, 31);
+    const uint32_t low = w1 << (1u - top);
+    const uint32_t rnd = low >> 31;
+    const uint32_t inc = rnd & (nz32((low << 1) | w0) | (q0 & 1u));
+    uint32_t c;
+    q0 = addc32(q0, inc, 0u, &c);
+    q1 = addc32(q1, 0u, c, &c);
+    q1 |= c << 31;          // carried out of the significand: 2^64 -> 2^63, E + 1
+    // denormal before rounding (E0 < 1: the cut is elsewhere) or overflowing
+    const int32_t E0 = (int32_t) (ea + eb + top) - 16383, E = E0 + (int32_t) c;
+    if (E0 < 1 || E > 0x7ffe)
+        return false;
+    *r = x87_make(a, ((a.se ^ b.se) >> 15) & 1, (uint32_t) E, ((uint64_t) q1 << 32) | q0);
+    return true;
 }
 
 MPIX_SDEV X87 x87_mul(const X87 &a, const X87 &b)
