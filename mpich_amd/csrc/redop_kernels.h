@@ -623,6 +623,19 @@ __device__ __forceinline__ uint64_t lanes_to_units(uint64_t m)
     return even(m) | (even(m >> 1) << 32);
 }
 
+// ok ? r : a, a component at a time (a select of the two aggregates compiles
+// to a pointer select over stack copies: scratch)
+__device__ __forceinline__ Pk32 select_pk(bool ok, const Pk32 &r, const Pk32 &a)
+{
+    Pk32 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        o.lo[e] = ok ? r.lo[e] : a.lo[e];
+        o.hi[e] = ok ? r.hi[e] : a.hi[e];
+    }
+    return o;
+}
+
 // v from the other lane of each adjacent pair (quad_perm [1,0,3,2])
 __device__ __forceinline__ v4u swap_pair(v4u v)
 {
@@ -732,7 +745,7 @@ __device__ __forceinline__ void contig32_tile(const typename C::unit *in, const 
                 const Pk32 ga = gather(a0[u], a1[u]);
                 Pk32 r = f(ga, gather(b0[u], b1[u]));
                 if constexpr (split)
-                    r = ok ? r : ga;    // a declined unit stays as it was
+                    r = select_pk(ok, r, ga);   // a declined unit stays as it was
                 const v4u y = swap_pair(odd ? r.lo : r.hi);
                 const uint64_t q = 2 * (t * tile + u * nt + wave * 64) + lane;
                 st16_pol<NTS>(vout + q, odd ? y : r.lo, wt);
@@ -747,7 +760,7 @@ __device__ __forceinline__ void contig32_tile(const typename C::unit *in, const 
             const Pk32 a{ld16<NTL>(vio + 2 * k), ld16<NTL>(vio + 2 * k + 1)};
             Pk32 r = f(a, Pk32{ld16<NTL>(vin + 2 * k), ld16<NTL>(vin + 2 * k + 1)});
             if constexpr (split)
-                r = ok ? r : a;         // a declined unit stays as it was
+                r = select_pk(ok, r, a);    // a declined unit stays as it was
             st16_pol<NTS>(vout + 2 * k, r.lo, wt);
             st16_pol<NTS>(vout + 2 * k + 1, r.hi, wt);
             if constexpr (split)        // a unit per lane: the mask is in unit order
