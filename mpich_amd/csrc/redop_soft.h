@@ -227,8 +227,11 @@ MPIX_SDEV uint64_t mad64(uint32_t x, uint32_t y, uint64_t z)
 #ifdef MPIX_SOFT_HOST
     return z + (uint64_t) x * y;
 #else
-    uint64_t r, carry;      // the carry-out pair is never set (no overflow)
-    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(carry) : "v"(x), "v"(y), "v"(z));
+    // the accumulator in place (dst = src2, as the compiler's own code has
+    // it), early-clobber against the 32-bit sources; the carry-out pair is
+    // never set (no overflow)
+    uint64_t r = z, carry;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+&v"(r), "=s"(carry) : "v"(x), "v"(y));
     return r;
 #endif
 }
@@ -241,7 +244,7 @@ MPIX_SDEV uint64_t mul64(uint32_t x, uint32_t y)
     return (uint64_t) x * y;
 #else
     uint64_t r, carry;
-    asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(r), "=s"(carry) : "v"(x), "v"(y));
+    asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=&v"(r), "=s"(carry) : "v"(x), "v"(y));
     return r;
 #endif
 }
