@@ -636,6 +636,17 @@ MPIX_SDEV Quad quad_add(const Quad &x, const Quad &y, bool sub)
     }
     if (cx == kX87Zero && cy == kX87Zero)
         return quad_make(sa && sb, 0, 0);
+    // one zero: the other operand exactly (soft-fp's NORMAL/ZERO cases copy
+    // it; a denormal packs back to the same bits), y with the subtraction's
+    // sign -- no alignment or rounding (real values stored as complex meet
+    // this in every unit)
+    if (cy == kX87Zero)
+        return x;
+    if (cx == kX87Zero) {
+        Quad r = y;
+        r.hi = (r.hi & ~(1ull << 63)) | ((uint64_t) sb << 63);
+        return r;
+    }
     if (xa < xb || (xa == xb && ma < mb)) {
         u128 t = ma; ma = mb; mb = t;
         int64_t u = xa; xa = xb; xb = u;
