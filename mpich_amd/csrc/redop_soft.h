@@ -401,6 +401,12 @@ MPIX_SDEV X87 x87_add(const X87 &a, const X87 &b, bool sub)
     }
     if (ca == kX87Zero && cb == kX87Zero)
         return x87_make(a, sa && sb, 0, 0);
+    // one zero, the other normal: that operand exactly (a denormal or
+    // pseudo-denormal one goes on below, where rounding renormalises it)
+    if (cb == kX87Zero && ea != 0)
+        return x87_make(a, sa, ea, a.m);
+    if (ca == kX87Zero && eb != 0)
+        return x87_make(a, sb, eb, b.m);
     uint64_t ma = a.m, mb = b.m;
     int64_t xa = ea ? ea : 1, xb = eb ? eb : 1;
     if (xa < xb || (xa == xb && ma < mb)) {     // |a| >= |b|
