@@ -221,3 +221,29 @@ def test_split_fixup_buffer_grows_on_a_stream(R, oracle):
             assert R.reduce_local_async(db, da, n, dt, S.MPI_PROD, s) == 0
         s.synchronize()
         _same(da.cpu().numpy(), want, n, ('grow', n))
+
+
+@pytest.mark.parametrize('dt', [S.COMPLEX32, S.C_LD_COMPLEX], ids=['complex32', 'c_long_double'])
+def test_split_product_every_unit_declined(R, oracle, dt):
+    """real values stored as complex: every product has a zero operand, so
+    the fast kernel declines every unit and the fixup launch combines whole
+    words of them (densely marked words, ragged tails, the tree form)"""
+    rng = np.random.default_rng(0x5EED0940 + dt)
+    s = torch.cuda.current_stream()
+    for n in (1, 63, 64, 65, 4099, 70001):
+        a, b = _split_operands(rng, dt, n, [])
+        a[:, 16:] = 0           # the imaginary parts: +0
+        b[:, 16:] = 0
+        want = _oracle_prod(oracle, dt, a, b)
+        da, db = dev(a), dev(b)
+        assert R.MPI_Reduce_local(db, da, n, dt, S.MPI_PROD) == 0
+        _same(da.cpu().numpy(), want, n, ('sync', n))
+        da = dev(a)
+        assert R.reduce_local_async(db, da, n, dt, S.MPI_PROD, s) == 0
+        s.synchronize()
+        _same(da.cpu().numpy(), want, n, ('async', n))
+        da = dev(a)
+        out = torch.full_like(da, 0x5A)
+        assert R.reduce_local_tree_async([da, db], out, n, dt, S.MPI_PROD, s) == 0
+        s.synchronize()
+        _same(out.cpu().numpy(), want, n, ('tree', n))
